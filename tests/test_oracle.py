@@ -1,0 +1,101 @@
+"""The CPU oracle is pinned against fixtures produced by running the reference
+(tests/golden/gen_golden.py).  Everything here runs on CPU."""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as om
+from oracle import loss as ol
+from oracle import post as op
+from conftest import GOLDEN
+
+
+def _batch(d):
+    return {"cls": torch.from_numpy(d["cls"]), "bboxes": torch.from_numpy(d["bboxes"]),
+            "batch_idx": torch.from_numpy(d["batch_idx"])}
+
+
+@pytest.mark.parametrize("scale", ["n", "s", "m"])
+def test_structure_keys(scale):
+    ref = json.loads((GOLDEN / "structure.json").read_text())[scale]
+    layers, save, P = om.build(om.load_cfg(scale))
+    assert save == ref["save"]
+    assert [[k, list(v.shape)] for k, v in P.items()] == [[k, s] for k, s, _ in ref["keys"]]
+    n_params = sum(v.numel() for k, v in P.items() if "running" not in k and "num_batches" not in k)
+    assert n_params == ref["n_params"]
+    assert float(P["model.0.bn.running_var"][0]) == pytest.approx(ref["bn_running_var"])
+    assert float(P["model.23.cv3.0.2.bias"][0]) == pytest.approx(ref["detect_bias_cls"])
+
+
+def test_nms_oracle_bitexact(golden):
+    d = golden("nms.npz")
+    for n in (0, 1, 2, 100, 1000, 6700):
+        keep = op.nms(d[f"n{n}_boxes"], d[f"n{n}_scores"], 0.45)
+        np.testing.assert_array_equal(keep, d[f"n{n}_keep"])
+    out = op.iou_row(d["iou_b1"], d["iou_b2"])
+    np.testing.assert_array_equal(out.view(np.uint32), d["iou_out"].astype(np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("kind", ["am", "lit"])
+def test_decode_oracle(golden, kind):
+    d = golden("decode.npz")
+    outs = op.decode(d[f"{kind}_in"], 640, 0.25, 0.45)
+    counts = np.asarray([len(o[1]) for o in outs])
+    np.testing.assert_array_equal(counts, d[f"{kind}_counts"])
+    np.testing.assert_array_equal(np.concatenate([o[0] for o in outs]), d[f"{kind}_boxes"])
+    np.testing.assert_array_equal(np.concatenate([o[1] for o in outs]), d[f"{kind}_scores"])
+    np.testing.assert_array_equal(np.concatenate([o[2] for o in outs]), d[f"{kind}_labels"])
+
+
+def test_model_n320_forward_loss_grads(golden):
+    d = golden("model_n320.npz")
+    layers, save, P = om.build(om.load_cfg("n"))
+    params = {k: v.requires_grad_(True) for k, v in P.items() if v.is_floating_point() and "running" not in k}
+    x = torch.from_numpy(d["img"])
+    heads = om.forward(P, layers, save, x, training=True)
+    for i in range(3):
+        torch.testing.assert_close(heads[i], torch.from_numpy(d[f"head{i}"]), rtol=1e-4, atol=1e-4)
+    loss, items = ol.v8_loss(heads, _batch(d))
+    torch.testing.assert_close(loss.detach().reshape(1), torch.from_numpy(d["loss"]), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(items, torch.from_numpy(d["items"]), rtol=1e-5, atol=1e-5)
+    loss.backward()
+    names = list(d["grad_names"])
+    ref_norm = dict(zip(names, d["grad_norm"]))
+    for k, p in params.items():
+        if k.endswith("dfl.conv.weight"):
+            continue
+        r = ref_norm[k]
+        assert abs(float(p.grad.norm()) - r) <= 1e-3 * max(r, 1e-3), k
+    for k in [n for n in d.files if n.startswith("grad:")]:
+        torch.testing.assert_close(params[k[5:]].grad, torch.from_numpy(d[k]), rtol=1e-3, atol=1e-5)
+    for k in [n for n in d.files if n.startswith("state:")]:
+        torch.testing.assert_close(P[k[6:]], torch.from_numpy(d[k]), rtol=1e-4, atol=1e-6)
+    with torch.no_grad():
+        y, feats = om.forward(P, layers, save, x, training=False)
+        torch.testing.assert_close(y, torch.from_numpy(d["eval_y"]), rtol=1e-4, atol=1e-3)
+        vl, vi = ol.v8_loss(feats, _batch(d))
+        torch.testing.assert_close(vi, torch.from_numpy(d["eval_items"]), rtol=1e-4, atol=1e-5)
+
+
+def test_assigner_and_loss_oracle(golden):
+    d = golden("assigner.npz")
+    feats = [torch.from_numpy(d[f"feat{i}"]).clone().requires_grad_(True) for i in range(3)]
+    loss, items, inner = ol.v8_loss(feats, _batch(d), return_internals=True)
+    np.testing.assert_array_equal(inner["fg"].numpy(), d["fg"])
+    np.testing.assert_array_equal(inner["tgi"].numpy(), d["tgi"])
+    torch.testing.assert_close(inner["target_scores"], torch.from_numpy(d["target_scores"]), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(items, torch.from_numpy(d["items"]), rtol=1e-5, atol=1e-6)
+    loss.backward()
+    for i in range(3):
+        torch.testing.assert_close(feats[i].grad, torch.from_numpy(d[f"dfeat{i}"]), rtol=1e-4, atol=1e-6)
+    # empty batch (M = 0)
+    fe = [torch.from_numpy(d[f"feat{i}"]).clone().requires_grad_(True) for i in range(3)]
+    empty = {"cls": torch.zeros(0, 1, dtype=torch.long), "bboxes": torch.zeros(0, 4),
+             "batch_idx": torch.zeros(0, dtype=torch.long)}
+    le, ie = ol.v8_loss(fe, empty)
+    torch.testing.assert_close(ie, torch.from_numpy(d["empty_items"]), rtol=1e-5, atol=1e-6)
+    le.backward()
+    for i in range(3):
+        torch.testing.assert_close(fe[i].grad, torch.from_numpy(d[f"empty_dfeat{i}"]), rtol=1e-5, atol=1e-7)
