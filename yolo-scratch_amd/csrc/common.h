@@ -1,0 +1,53 @@
+// Shared device/host helpers for libyolomi (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/yolomi.h"
+
+namespace ym {
+
+// thread-local last-error string behind ym_last_error()
+void set_error(const char* fmt, ...);
+
+#define YM_CHECK_ARG(cond, ...)                    \
+    do {                                           \
+        if (!(cond)) {                             \
+            ::ym::set_error(__VA_ARGS__);          \
+            return YM_ERR_ARG;                     \
+        }                                          \
+    } while (0)
+
+#define YM_LAUNCH_CHECK(what)                                                        \
+    do {                                                                             \
+        hipError_t e_ = hipGetLastError();                                           \
+        if (e_ != hipSuccess) {                                                      \
+            ::ym::set_error("%s: launch failed: %s", what, hipGetErrorString(e_));   \
+            return YM_ERR_HIP;                                                       \
+        }                                                                            \
+    } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+typedef uint16_t bf16_t;   // raw bf16 bits in memory
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+// round-to-nearest-even f32 -> bf16 (NaN kept as a quiet NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) {
+    uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ __forceinline__ float silu_f(float u) { return u / (1.0f + __expf(-u)); }
+
+}  // namespace ym

@@ -1,0 +1,409 @@
+// Decode + class-agnostic greedy NMS, one workgroup per image (gfx950).
+//
+// Replaces decode_predictions_for_metrics / nms_simple / calculate_iou_batch_simple
+// (/root/reference/yolo_scratch_cuda/train_yolo11_cuda.py:265-437).  Bit-exact
+// with the reference on tie-free scores: the IoU is evaluated in the same fp32
+// op order and this file is compiled with -ffp-contract=off.
+//
+// Pipeline per call
+//   1. rowmax kernel      grid over rows: max/argmax over the C class scores,
+//                         `> conf` flag, xywh -> xyxy            (:296-329)
+//   2. nms_image kernel   one 1024-thread workgroup per image:
+//        a. order-preserving compaction of flagged rows (block scan)
+//        b. bitonic sort of 64-bit keys (~score, filtered index): score
+//           descending, index ascending (the reference's argsort is unstable;
+//           golden inputs are tie-free)                          (:377)
+//        c. greedy loop: the head box is broadcast through LDS, every thread
+//           tests the boxes it holds in registers, drops IoU > thr, and a
+//           block min-reduction finds the next alive head        (:380-397)
+//        d. write kept boxes / img_size clamped to [0,1]          (:342-350)
+#include "common.h"
+
+namespace ym {
+namespace {
+
+constexpr int NMS_THREADS = 1024;
+constexpr int NMS_WAVES = NMS_THREADS / 64;
+constexpr int SORT_LDS_KEYS = 16384;   // 128 KiB of keys in LDS
+constexpr int REG_ITEMS = 8;           // boxes held in registers per thread (K <= 8192)
+
+struct Ws {
+    float4* box;      // [B][N] xyxy of every row
+    float* score;     // [B][N]
+    int32_t* label;   // [B][N]
+    int32_t* flag;    // [B][N]
+    int32_t* frow;    // [B][N] filtered index -> row
+    uint64_t* keys;   // [B][N] (global sort path)
+};
+
+__host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+inline int64_t pow2_at_least(int64_t x) {
+    int64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+inline Ws carve(void* base, int64_t B, int64_t N) {
+    char* p = static_cast<char*>(base);
+    size_t n = size_t(B) * size_t(N);
+    Ws w;
+    w.box = reinterpret_cast<float4*>(p);   p += align256(n * sizeof(float4));
+    w.score = reinterpret_cast<float*>(p);  p += align256(n * sizeof(float));
+    w.label = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
+    w.flag = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
+    w.frow = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
+    w.keys = reinterpret_cast<uint64_t*>(p);
+    return w;
+}
+
+inline size_t ws_bytes(int64_t B, int64_t N) {
+    size_t n = size_t(B) * size_t(N);
+    return align256(n * 16) + 4 * align256(n * 4) + align256(size_t(B) * pow2_at_least(N) * 8) + 256;
+}
+
+// IoU in the reference's op order (train_yolo11_cuda.py:418-435).
+__device__ __forceinline__ float iou_ref(float4 a, float4 b) {
+    float x1 = fmaxf(a.x, b.x), y1 = fmaxf(a.y, b.y);
+    float x2 = fminf(a.z, b.z), y2 = fminf(a.w, b.w);
+    float iw = x2 - x1, ih = y2 - y1;
+    iw = iw < 0.0f ? 0.0f : iw;
+    ih = ih < 0.0f ? 0.0f : ih;
+    float inter = iw * ih;
+    float a1 = (a.z - a.x) * (a.w - a.y);
+    float a2 = (b.z - b.x) * (b.w - b.y);
+    float uni = a1 + a2;
+    uni = uni - inter;
+    return inter / (uni + 1e-6f);
+}
+
+__device__ __forceinline__ uint32_t desc_bits(float s) {
+    uint32_t u = __float_as_uint(s);
+    uint32_t ord = (u & 0x80000000u) ? ~u : (u | 0x80000000u);   // ascending-order bits
+    return ~ord;                                                  // descending
+}
+
+// ---------------------------------------------------------------- stage 1
+// thread per row (C small) — max/argmax with the first maximal index winning
+__global__ void rowmax_thread_kernel(const float* __restrict__ pred, int64_t B, int64_t N, int64_t C,
+                                     int64_t rs, int64_t is, float conf, Ws w) {
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= B * N) return;
+    int64_t b = i / N, n = i - b * N;
+    const float* r = pred + b * is + n * rs;
+    float mx = r[4];
+    int lab = 0;
+    for (int64_t c = 1; c < C; ++c) {
+        float v = r[4 + c];
+        if (v > mx) { mx = v; lab = int(c); }
+    }
+    float x = r[0], y = r[1], hw = r[2] / 2.0f, hh = r[3] / 2.0f;
+    w.box[i] = make_float4(x - hw, y - hh, x + hw, y + hh);
+    w.score[i] = mx;
+    w.label[i] = lab;
+    w.flag[i] = (mx > conf) ? 1 : 0;
+}
+
+// wave per row (C large, e.g. the literal (B, 4+nc, A) eval layout)
+__global__ void rowmax_wave_kernel(const float* __restrict__ pred, int64_t B, int64_t N, int64_t C,
+                                   int64_t rs, int64_t is, float conf, Ws w) {
+    int64_t i = int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
+    int lane = threadIdx.x & 63;
+    if (i >= B * N) return;
+    int64_t b = i / N, n = i - b * N;
+    const float* r = pred + b * is + n * rs;
+    float mx = -INFINITY;
+    int64_t lab = INT64_MAX;
+    for (int64_t c = lane; c < C; c += 64) {
+        float v = r[4 + c];
+        if (v > mx || (v == mx && c < lab)) { mx = v; lab = c; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float om = __shfl_xor(mx, o, 64);
+        int64_t ol = __shfl_xor(lab, o, 64);
+        if (om > mx || (om == mx && ol < lab)) { mx = om; lab = ol; }
+    }
+    if (lane == 0) {
+        float x = r[0], y = r[1], hw = r[2] / 2.0f, hh = r[3] / 2.0f;
+        w.box[i] = make_float4(x - hw, y - hh, x + hw, y + hh);
+        w.score[i] = mx;
+        w.label[i] = int32_t(lab);
+        w.flag[i] = (mx > conf) ? 1 : 0;
+    }
+}
+
+// direct candidates (nms_simple): every box is a candidate
+__global__ void direct_kernel(const float4* __restrict__ boxes, const float* __restrict__ scores, int64_t n, Ws w) {
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    w.box[i] = boxes[i];
+    w.score[i] = scores[i];
+    w.label[i] = 0;
+    w.flag[i] = 1;
+}
+
+// ---------------------------------------------------------------- stage 2 helpers
+__device__ int block_excl_scan(int v, int* sh, int& total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[wv] = x;
+    __syncthreads();
+    if (wv == 0) {
+        int s = lane < NMS_WAVES ? sh[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            int y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < NMS_WAVES) sh[lane] = s;
+    }
+    __syncthreads();
+    int before = (wv > 0 ? sh[wv - 1] : 0) + x - v;
+    total = sh[NMS_WAVES - 1];
+    __syncthreads();
+    return before;
+}
+
+__device__ int block_min(int v, int* sh) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    if (lane == 0) sh[wv] = v;
+    __syncthreads();
+    int r = sh[0];
+#pragma unroll
+    for (int k = 1; k < NMS_WAVES; ++k) r = min(r, sh[k]);
+    __syncthreads();
+    return r;
+}
+
+template <bool IN_LDS>
+__device__ void bitonic(uint64_t* keys, int P) {
+    for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
+                int l = i ^ j;
+                if (l > i) {
+                    uint64_t a = keys[i], c = keys[l];
+                    bool up = (i & k) == 0;
+                    if ((a > c) == up) { keys[i] = c; keys[l] = a; }
+                }
+            }
+            if (IN_LDS) __syncthreads();
+            else { __threadfence_block(); __syncthreads(); }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- stage 2
+__global__ void __launch_bounds__(NMS_THREADS)
+nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp_norm, Ws w,
+                 int32_t* __restrict__ out_count, float* __restrict__ out_boxes, float* __restrict__ out_scores,
+                 int64_t* __restrict__ out_labels, int64_t* __restrict__ out_index) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint64_t* skeys = reinterpret_cast<uint64_t*>(smem);            // SORT_LDS_KEYS
+    __shared__ int sh[NMS_WAVES + 1];
+    __shared__ float4 head_box;
+    __shared__ int kept_pos_count;
+
+    const int64_t b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int64_t base = b * N;
+
+    // a. order-preserving compaction (chunk per thread)
+    const int cpt = int((N + NMS_THREADS - 1) / NMS_THREADS);
+    const int64_t r0 = int64_t(tid) * cpt;
+    int cnt = 0;
+    for (int k = 0; k < cpt; ++k) {
+        int64_t r = r0 + k;
+        if (r < N) cnt += w.flag[base + r];
+    }
+    int K;
+    int off = block_excl_scan(cnt, sh, K);
+    for (int k = 0; k < cpt; ++k) {
+        int64_t r = r0 + k;
+        if (r < N && w.flag[base + r]) w.frow[base + off++] = int32_t(r);
+    }
+    __syncthreads();
+    if (K == 0) {
+        if (tid == 0) out_count[b] = 0;
+        return;
+    }
+
+    // b. sort (score desc, filtered index asc)
+    int P = 1;
+    while (P < K) P <<= 1;
+    const bool lds_sort = P <= SORT_LDS_KEYS;
+    uint64_t* keys = lds_sort ? skeys : (w.keys + b * KP);   // KP >= P
+    for (int i = tid; i < P; i += NMS_THREADS) {
+        uint64_t key = ~0ull;
+        if (i < K) key = (uint64_t(desc_bits(w.score[base + w.frow[base + i]])) << 32) | uint32_t(i);
+        keys[i] = key;
+    }
+    __syncthreads();
+    if (lds_sort) bitonic<true>(keys, P);
+    else bitonic<false>(keys, P);
+
+    // c. greedy loop; sorted position s -> filtered index f = keys[s] low bits
+    float4 mybox[REG_ITEMS];
+    bool alive[REG_ITEMS];
+    const bool in_regs = K <= REG_ITEMS * NMS_THREADS;
+    if (in_regs) {
+#pragma unroll
+        for (int it = 0; it < REG_ITEMS; ++it) {
+            int s = tid + it * NMS_THREADS;
+            alive[it] = s < K;
+            if (s < K) {
+                int f = int(uint32_t(keys[s]));
+                mybox[it] = w.box[base + w.frow[base + f]];
+            }
+        }
+    }
+    // alive flags for the large-K path live in out_index scratch as bytes: reuse w.flag (now free)
+    int32_t* galive = w.flag + base;
+    if (!in_regs) {
+        for (int s = tid; s < K; s += NMS_THREADS) galive[s] = 1;
+    }
+    if (tid == 0) kept_pos_count = 0;
+    __syncthreads();
+
+    int head = 0;
+    while (head < K) {
+        // record + broadcast the head box
+        if (tid == 0) {
+            int f = int(uint32_t(keys[head]));
+            head_box = w.box[base + w.frow[base + f]];
+            out_index[base + kept_pos_count] = head;   // sorted position for now
+            kept_pos_count++;
+        }
+        __syncthreads();
+        const float4 hb = head_box;
+        int next = INT32_MAX;
+        if (in_regs) {
+#pragma unroll
+            for (int it = 0; it < REG_ITEMS; ++it) {
+                int s = tid + it * NMS_THREADS;
+                if (alive[it] && s > head) {
+                    float v = iou_ref(hb, mybox[it]);
+                    if (!(v <= iou_thr)) alive[it] = false;     // reference keeps IoU <= thr (:396)
+                    else next = min(next, s);
+                } else if (s <= head) {
+                    alive[it] = false;
+                }
+            }
+        } else {
+            for (int s = tid; s < K; s += NMS_THREADS) {
+                if (s > head && galive[s]) {
+                    int f = int(uint32_t(keys[s]));
+                    float v = iou_ref(hb, w.box[base + w.frow[base + f]]);
+                    if (!(v <= iou_thr)) galive[s] = 0;
+                    else next = min(next, s);
+                }
+            }
+        }
+        head = block_min(next, sh);
+    }
+    __syncthreads();
+
+    // d. outputs
+    const int nk = kept_pos_count;
+    for (int k = tid; k < nk; k += NMS_THREADS) {
+        int s = int(out_index[base + k]);
+        int f = int(uint32_t(keys[s]));
+        int64_t row = base + w.frow[base + f];
+        float4 bx = w.box[row];
+        if (clamp_norm) {
+            bx.x = fminf(fmaxf(bx.x / img_size, 0.0f), 1.0f);
+            bx.y = fminf(fmaxf(bx.y / img_size, 0.0f), 1.0f);
+            bx.z = fminf(fmaxf(bx.z / img_size, 0.0f), 1.0f);
+            bx.w = fminf(fmaxf(bx.w / img_size, 0.0f), 1.0f);
+        }
+        int64_t o = base + k;
+        reinterpret_cast<float4*>(out_boxes)[o] = bx;
+        out_scores[o] = w.score[row];
+        out_labels[o] = w.label[row];
+        out_index[o] = f;
+    }
+    if (tid == 0) out_count[b] = nk;
+}
+
+int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int clamp_norm, Ws w,
+               int32_t* out_count, float* out_boxes, float* out_scores, int64_t* out_labels, int64_t* out_index,
+               hipStream_t st) {
+    size_t lds = size_t(SORT_LDS_KEYS) * sizeof(uint64_t);
+    hipLaunchKernelGGL(nms_image_kernel, dim3(unsigned(B)), dim3(NMS_THREADS), lds, st, Nalloc,
+                       pow2_at_least(Nalloc), iou_thr, img_size,
+                       clamp_norm, w, out_count, out_boxes, out_scores, out_labels, out_index);
+    YM_LAUNCH_CHECK("nms_image_kernel");
+    return YM_OK;
+}
+
+}  // namespace
+}  // namespace ym
+
+using namespace ym;
+
+extern "C" size_t ym_nms_workspace_size(int64_t B, int64_t N) { return 2 * ws_bytes(B, N); }
+
+__global__ void ym_iou_row_kernel(const float4* __restrict__ b1, const float4* __restrict__ b2, int64_t m,
+                                  float* __restrict__ out) {
+    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = iou_ref(*b1, b2[i]);
+}
+
+extern "C" int ym_iou_row(const float* box1, const float* boxes2, int64_t m, float* out, void* stream) {
+    YM_CHECK_ARG(m >= 0, "ym_iou_row: m < 0");
+    if (m == 0) return YM_OK;
+    hipLaunchKernelGGL(ym_iou_row_kernel, dim3(unsigned((m + 255) / 256)), dim3(256), 0, as_stream(stream),
+                       reinterpret_cast<const float4*>(box1), reinterpret_cast<const float4*>(boxes2), m, out);
+    YM_LAUNCH_CHECK("ym_iou_row");
+    return YM_OK;
+}
+
+extern "C" int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C, int64_t row_stride,
+                             int64_t img_stride, float conf, float iou_thr, float img_size, void* workspace,
+                             size_t workspace_bytes, int32_t* out_count, float* out_boxes, float* out_scores,
+                             int64_t* out_labels, int64_t* out_index, void* stream) {
+    YM_CHECK_ARG(B >= 0 && N >= 0 && C >= 1, "ym_decode_nms: bad shape B=%lld N=%lld C=%lld", (long long)B,
+                 (long long)N, (long long)C);
+    YM_CHECK_ARG(row_stride >= 4 + C, "ym_decode_nms: row_stride < 4+C");
+    YM_CHECK_ARG(N < (int64_t(1) << 30), "ym_decode_nms: N too large");
+    if (B == 0) return YM_OK;
+    hipStream_t st = as_stream(stream);
+    if (N == 0) return hipMemsetAsync(out_count, 0, B * sizeof(int32_t), st) == hipSuccess ? YM_OK : YM_ERR_HIP;
+    YM_CHECK_ARG(workspace_bytes >= ws_bytes(B, N), "ym_decode_nms: workspace too small (%zu < %zu)",
+                 workspace_bytes, ws_bytes(B, N));
+    Ws w = carve(workspace, B, N);
+    if (C <= 64)
+        hipLaunchKernelGGL(rowmax_thread_kernel, dim3(unsigned((B * N + 255) / 256)), dim3(256), 0, st, pred, B, N,
+                           C, row_stride, img_stride, conf, w);
+    else
+        hipLaunchKernelGGL(rowmax_wave_kernel, dim3(unsigned((B * N + 3) / 4)), dim3(256), 0, st, pred, B, N, C,
+                           row_stride, img_stride, conf, w);
+    YM_LAUNCH_CHECK("rowmax");
+    return launch_nms(B, N, iou_thr, img_size, 1, w, out_count, out_boxes, out_scores, out_labels, out_index, st);
+}
+
+extern "C" int ym_nms(const float* boxes, const float* scores, int64_t n, float iou_thr, void* workspace,
+                      size_t workspace_bytes, int64_t* keep, int32_t* count, void* stream) {
+    YM_CHECK_ARG(n >= 0, "ym_nms: n < 0");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) return hipMemsetAsync(count, 0, sizeof(int32_t), st) == hipSuccess ? YM_OK : YM_ERR_HIP;
+    YM_CHECK_ARG(workspace_bytes >= ws_bytes(1, n) + ws_bytes(1, n), "ym_nms: workspace too small");
+    Ws w = carve(workspace, 1, n);
+    // scratch outputs (boxes/scores/labels) after the candidate arrays
+    char* extra = static_cast<char*>(workspace) + ws_bytes(1, n);
+    float* ob = reinterpret_cast<float*>(extra);
+    float* os = reinterpret_cast<float*>(extra + align256(n * 16));
+    int64_t* ol = reinterpret_cast<int64_t*>(extra + align256(n * 16) + align256(n * 4));
+    hipLaunchKernelGGL(direct_kernel, dim3(unsigned((n + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(boxes), scores, n, w);
+    YM_LAUNCH_CHECK("nms direct");
+    return launch_nms(1, n, iou_thr, 1.0f, 0, w, count, ob, os, ol, keep, st);
+}

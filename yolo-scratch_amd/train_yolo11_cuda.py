@@ -1,0 +1,272 @@
+"""Train YOLOv11 on MI355X — drop-in for the reference entry point.
+
+Same CLI flags, same functions and return conventions as the reference's
+train_yolo11_cuda.py (/root/reference/yolo_scratch_cuda/train_yolo11_cuda.py):
+train_one_epoch :31-98, validate :101-262, decode_predictions_for_metrics
+:265-358, nms_simple :361-399, calculate_iou_batch_simple :402-437,
+cosine_lr_schedule :440-451, main :454-661.
+
+What differs underneath: the model forward/backward, the loss and the decode +
+NMS postprocess run as hand-written HIP kernels for gfx950 (libyolomi.so);
+per-step loss items are accumulated on the device and read back every
+`LOG_EVERY` steps instead of four host syncs per step; `--synthetic N` trains
+on N synthetic batches when no dataset is mounted; multi-GPU data parallelism
+is enabled by launching with torchrun (one process per GPU, RCCL).
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).parent))
+
+from models.yolo11_model import build_yolo11  # noqa: E402
+from losses.yolo_v8_loss import v8DetectionLoss  # noqa: E402
+from datasets import collate_fn_cuda  # noqa: E402
+from utils.metrics import evaluate_detections  # noqa: E402
+from yolomi import post as _post  # noqa: E402
+
+collate_fn = collate_fn_cuda
+LOG_EVERY = 10
+
+
+def _tqdm(it, **kw):
+    try:
+        from tqdm import tqdm
+        return tqdm(it, **kw)
+    except Exception:  # pragma: no cover
+        return it
+
+
+def train_one_epoch(model, dataloader, optimizer, criterion, device, epoch, epochs, dp=None):
+    """One epoch (reference :31-98).  `dp` is an optional yolomi.dist.GradSync."""
+    model.train()
+    pbar = _tqdm(dataloader, desc=f"Epoch {epoch}/{epochs}")
+    sums = torch.zeros(4, device=device)
+    n = 0
+    for batch_idx, batch in enumerate(pbar):
+        for k, v in batch.items():
+            if isinstance(v, torch.Tensor):
+                batch[k] = v.to(device, non_blocking=True)
+        optimizer.zero_grad(set_to_none=True)
+        preds = model(batch["img"])
+        loss, loss_items = criterion(preds, batch)
+        loss.backward()
+        if dp is not None:
+            dp.sync()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
+        optimizer.step()
+        sums[0] += loss.detach()
+        sums[1:] += loss_items.detach()
+        n += 1
+        if hasattr(pbar, "set_postfix") and (batch_idx + 1) % LOG_EVERY == 0:
+            s = (sums / n).tolist()
+            pbar.set_postfix({"loss": f"{s[0]:.4f}", "box": f"{s[1]:.4f}", "cls": f"{s[2]:.4f}", "dfl": f"{s[3]:.4f}"})
+    s = (sums / max(len(dataloader), 1)).tolist()
+    return {"loss": s[0], "box_loss": s[1], "cls_loss": s[2], "dfl_loss": s[3]}
+
+
+@torch.no_grad()
+def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_threshold=0.45, max_batches=None):
+    """Validation + metrics (reference :101-262)."""
+    model.eval()
+    sums = torch.zeros(4, device=device)
+    all_predictions, all_targets = [], []
+    batches = 0
+    for batch in _tqdm(dataloader, desc="Validating"):
+        for k, v in batch.items():
+            if isinstance(v, torch.Tensor):
+                batch[k] = v.to(device, non_blocking=True)
+        preds = model(batch["img"])
+        loss, loss_items = criterion(preds, batch)
+        sums[0] += loss
+        sums[1:] += loss_items
+        if isinstance(preds, tuple) and len(preds) == 2:
+            predictions = decode_predictions_for_metrics(preds[0], batch["img"].shape[-1], conf_threshold,
+                                                         iou_threshold, device)
+        else:
+            decoded = model(batch["img"])
+            predictions = decode_predictions_for_metrics(decoded[0], batch["img"].shape[-1], conf_threshold,
+                                                         iou_threshold, device)
+        all_predictions.extend(predictions)
+        bidx, bboxes, cls = batch["batch_idx"], batch["bboxes"], batch["cls"]
+        for i in range(batch["img"].shape[0]):
+            m = bidx == i
+            all_targets.append({"boxes": bboxes[m], "labels": cls[m].reshape(-1)})
+        batches += 1
+        if max_batches is not None and batches >= max_batches:
+            break
+    for p in all_predictions:
+        for k in ("boxes", "scores", "labels"):
+            p[k] = p[k].cpu()
+    for t in all_targets:
+        t["boxes"], t["labels"] = t["boxes"].cpu(), t["labels"].cpu()
+    metrics = evaluate_detections(all_predictions, all_targets, conf_threshold=conf_threshold, iou_threshold=0.5)
+    nb = batches if max_batches else len(dataloader)
+    s = (sums / max(nb, 1)).tolist()
+    return {"loss": s[0], "box_loss": s[1], "cls_loss": s[2], "dfl_loss": s[3], **metrics}
+
+
+def decode_predictions_for_metrics(preds, img_size, conf_threshold, iou_threshold, device):
+    """Per-image boxes/scores/labels (normalised xyxy) from decoded predictions.
+
+    Reads `preds` as (batch, rows, 4+C) exactly like the reference (:289-301),
+    including when it is handed the (B, 4+nc, A) eval tensor.
+    One batched GPU launch pair; one host sync for the per-image counts.
+    """
+    pred = preds[0] if isinstance(preds, tuple) and len(preds) == 2 else preds
+    return _post.decode_nms(pred, img_size, conf_threshold, iou_threshold)
+
+
+def nms_simple(boxes, scores, iou_threshold):
+    """Greedy class-agnostic NMS; returns the list of kept indices (reference :361-399)."""
+    if len(boxes) == 0:
+        return []
+    return _post.nms(boxes, scores, iou_threshold).cpu().tolist()
+
+
+def calculate_iou_batch_simple(boxes1, boxes2):
+    """IoU of boxes1 (1,4) against boxes2 (M,4) (reference :402-437)."""
+    if boxes1.dim() == 1:
+        boxes1 = boxes1.unsqueeze(0)
+    rows = [_post.iou_row(b, boxes2) for b in boxes1]
+    iou = torch.stack(rows) if rows else boxes2.new_zeros(0, boxes2.shape[0])
+    return iou.squeeze() if iou.dim() > 1 and iou.shape[0] == 1 else iou
+
+
+def cosine_lr_schedule(optimizer, epoch, epochs, lr_min=1e-6, lr_max=1e-3, warmup_epochs=3):
+    """Per-epoch cosine schedule with linear warm-up (reference :440-451)."""
+    if epoch < warmup_epochs:
+        lr = lr_min + (lr_max - lr_min) * (epoch / warmup_epochs)
+    else:
+        progress = (epoch - warmup_epochs) / (epochs - warmup_epochs)
+        lr = lr_min + (lr_max - lr_min) * 0.5 * (1 + math.cos(math.pi * progress))
+    for g in optimizer.param_groups:
+        g["lr"] = lr
+    return lr
+
+
+class _SyntheticLoader:
+    def __init__(self, n, batch, imgsz, seed):
+        from datasets.synthetic import synth_batch
+        self._mk = lambda i: synth_batch(batch, imgsz, seed + i)
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        for i in range(self.n):
+            yield self._mk(i)
+
+
+def main():
+    ap = argparse.ArgumentParser(description="Train YOLOv11 for Crater Detection (MI355X)")
+    ap.add_argument("--data", type=str, default="/content/data/train")
+    ap.add_argument("--cfg", type=str, default=str(Path(__file__).parent / "configs" / "yolo11n_crater.yaml"))
+    ap.add_argument("--scale", type=str, default="s", choices=["n", "s", "m", "l", "x"])
+    ap.add_argument("--epochs", type=int, default=150)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--imgsz", type=int, default=640)
+    ap.add_argument("--device", type=str, default="cuda")
+    ap.add_argument("--workers", type=int, default=4)
+    ap.add_argument("--lr", type=float, default=0.001)
+    ap.add_argument("--weight-decay", type=float, default=0.0005)
+    ap.add_argument("--val-split", type=float, default=0.2)
+    ap.add_argument("--save-dir", type=str, default="/content/drive/MyDrive/YOLO11_crater_cuda")
+    ap.add_argument("--resume", type=str, default="/content/drive/MyDrive/YOLO11_crater_cuda/last.pt")
+    ap.add_argument("--max-val-batches", type=int, default=None)
+    ap.add_argument("--val-conf", type=float, default=0.25)
+    ap.add_argument("--synthetic", type=int, default=0, help="train on N synthetic batches (no dataset needed)")
+    args = ap.parse_args()
+
+    from yolomi import dist as ydist
+    dp_ctx = ydist.init_from_env()
+    if not torch.cuda.is_available():
+        raise SystemExit("yolomi runs on MI355X GPUs only (no CPU fallback)")
+    device = torch.device("cuda", dp_ctx.local_rank if dp_ctx else 0)
+    torch.cuda.set_device(device)
+    rank0 = dp_ctx is None or dp_ctx.rank == 0
+    save_dir = Path(args.save_dir)
+    if rank0:
+        save_dir.mkdir(parents=True, exist_ok=True)
+
+    if args.synthetic:
+        seed = 1000 * (dp_ctx.rank if dp_ctx else 0)
+        train_loader = _SyntheticLoader(args.synthetic, args.batch, args.imgsz, seed)
+        val_loader = _SyntheticLoader(max(1, args.synthetic // 5), args.batch, args.imgsz, seed + 10 ** 6)
+    else:
+        from datasets import CraterDatasetCUDA
+        from torch.utils.data import DataLoader, Subset
+        dataset = CraterDatasetCUDA(args.data, img_size=args.imgsz, cache_images=False, augment=True)
+        val_size = int(len(dataset) * args.val_split)
+        idx = torch.randperm(len(dataset), generator=torch.Generator().manual_seed(42)).tolist()
+        tr, va = Subset(dataset, idx[: len(dataset) - val_size]), Subset(dataset, idx[len(dataset) - val_size:])
+        if dp_ctx:
+            tr = Subset(tr, list(range(dp_ctx.rank, len(tr), dp_ctx.world)))
+        nw = min(args.workers, 4)
+        kw = dict(batch_size=args.batch, num_workers=nw, collate_fn=collate_fn, pin_memory=True,
+                  persistent_workers=nw > 0, prefetch_factor=2 if nw > 0 else None, drop_last=False)
+        train_loader = DataLoader(tr, shuffle=True, **kw)
+        val_loader = DataLoader(va, shuffle=False, **kw)
+
+    import yaml
+    with open(args.cfg) as f:
+        cfg_dict = yaml.safe_load(f)
+    cfg_dict["scale"] = args.scale
+    model = build_yolo11(cfg=cfg_dict, ch=1, nc=5).to(device)
+    if rank0:
+        n_params = sum(p.numel() for p in model.parameters())
+        print(f"Total parameters: {n_params:,} ({n_params / 1e6:.2f}M)")
+    criterion = v8DetectionLoss(model, tal_topk=10)
+    optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+    dp = ydist.GradSync(model, dp_ctx) if dp_ctx else None
+    start_epoch, best_loss, best_mAP50 = 0, float("inf"), 0.0
+    if args.resume and os.path.isfile(args.resume):
+        ckpt = torch.load(args.resume, map_location=device, weights_only=True)
+        model.load_state_dict(ckpt["model_state_dict"])
+        optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        start_epoch = ckpt["epoch"] + 1
+        best_loss = ckpt.get("best_loss", best_loss)
+        best_mAP50 = ckpt.get("best_mAP50", best_mAP50)
+    if dp:
+        dp.broadcast_state()
+
+    for epoch in range(start_epoch, args.epochs):
+        lr = cosine_lr_schedule(optimizer, epoch, args.epochs, lr_min=args.lr * 0.01, lr_max=args.lr, warmup_epochs=3)
+        criterion.epoch = epoch
+        tm = train_one_epoch(model, train_loader, optimizer, criterion, device, epoch + 1, args.epochs, dp)
+        vm = validate(model, val_loader, criterion, device, conf_threshold=args.val_conf, iou_threshold=0.45,
+                      max_batches=args.max_val_batches)
+        if not rank0:
+            continue
+        print(f"\nEpoch {epoch + 1}/{args.epochs} | LR: {lr:.6f}")
+        print(f"  Train - Loss: {tm['loss']:.4f}, Box: {tm['box_loss']:.4f}, Cls: {tm['cls_loss']:.4f}, "
+              f"DFL: {tm['dfl_loss']:.4f}")
+        print(f"  Val   - Loss: {vm['loss']:.4f}, Box: {vm['box_loss']:.4f}, Cls: {vm['cls_loss']:.4f}, "
+              f"DFL: {vm['dfl_loss']:.4f}")
+        print(f"  Metrics - P: {vm.get('precision', 0.0):.4f}, R: {vm.get('recall', 0.0):.4f}, "
+              f"mAP50: {vm.get('mAP50', 0.0):.4f}, mAP50-95: {vm.get('mAP50-95', 0.0):.4f}")
+        ckpt = {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
+                "train_metrics": tm, "val_metrics": vm, "best_loss": best_loss, "best_mAP50": best_mAP50}
+        torch.save(ckpt, save_dir / "last.pt")
+        if "mAP50" in vm:
+            if vm["mAP50"] > best_mAP50:
+                best_mAP50 = vm["mAP50"]
+                ckpt["best_mAP50"] = best_mAP50
+                torch.save(ckpt, save_dir / "best.pt")
+        elif vm["loss"] < best_loss:
+            best_loss = vm["loss"]
+            ckpt["best_loss"] = best_loss
+            torch.save(ckpt, save_dir / "best.pt")
+    if dp_ctx:
+        ydist.shutdown()
+
+
+if __name__ == "__main__":
+    main()
