@@ -18,7 +18,9 @@
  *    stride, pixel stride `ld`), all in elements; channel c of pixel p of
  *    image n lives at base[n*bstride + p*ld + c].  Channel slices (concat /
  *    split) are expressed by offsetting `base` and keeping `ld`.
- *  - bf16 tensors are raw uint16 bit patterns.
+ *  - 16-bit tensors are raw uint16 bit patterns.  Activations are fp16,
+ *    gradients bf16, pre-BatchNorm conv outputs fp16, master weights fp32
+ *    (converted per step to an fp16 forward copy and a bf16 dgrad copy).
  *  - Return value: YM_OK (0) or a negative YM_ERR_*; ym_last_error() gives a
  *    thread-local message.  Nothing throws across the ABI.
  */
@@ -70,6 +72,143 @@ int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C, int64_t ro
  * keep[0..*count) are indices into boxes in kept (score-descending) order. */
 int ym_nms(const float* boxes, const float* scores, int64_t n, float iou_thr, void* workspace,
            size_t workspace_bytes, int64_t* keep, int32_t* count, void* stream);
+
+
+/* ------------------------------------------------------------------ convolution
+ * Replaces nn.Conv2d forward/backward inside Conv (models/yolo11_modules.py:21-33)
+ * and the Detect head's bias convs (:221-234).  NHWC; fp16 forward / bf16 backward MFMA, fp32 accumulate.
+ */
+typedef struct {
+    int32_t n, h, w, cin;      /* input  (n, h, w, cin)  */
+    int32_t oh, ow, cout;      /* output (n, oh, ow, cout) */
+    int32_t k, stride, pad;    /* square kernel */
+    int64_t x_bs, x_ld;        /* input view: image stride, pixel stride (elements) */
+    int64_t y_bs, y_ld;        /* output view */
+    int32_t out_f32;           /* fwd output: 0 bf16, 1 fp32, 2 fp16 (pre-BatchNorm z) */
+    int32_t accumulate;        /* add into the destination instead of overwriting */
+} ym_conv_desc;
+
+typedef struct {
+    const float* src;          /* fp32 OIHW master weight */
+    uint16_t* dst_fwd;         /* bf16 [cout][kh][kw][cin] or NULL */
+    uint16_t* dst_t;           /* bf16 [cin][kh][kw][cout] (dgrad) or NULL */
+    int64_t elem_offset;       /* running element offset of this entry */
+    int32_t cout, cin, kh, kw;
+    int32_t cout_t;            /* row length of dst_t (>= cout; zero padding is the caller's) */
+} ym_wprep_entry;
+
+/* Number of grid-x blocks (= rows of the BN statistics partials) ym_conv_fwd uses. */
+int ym_conv_stat_blocks(int64_t m, int cout);
+/* y = conv(x, w) (+bias); optional per-block channel sum / sum-of-squares partials
+ * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
+int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
+                float* stat_sum, float* stat_sq, void* stream);
+/* dx (+)= conv_transpose(dz, w) using the [cin][kh][kw][cout] weight copy. */
+int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream);
+/* dw_ohwi[cout][k*k][cin] += sum over pixels (fp32 atomics; caller zeroes). */
+int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, float* dw_ohwi, void* stream);
+/* [cout][taps][cin] -> [cout][cin][taps] (PyTorch OIHW grad layout). */
+int ym_wgrad_to_oihw(const float* src, float* dst, int cout, int cin, int taps, int accumulate, void* stream);
+/* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0). */
+int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
+                      int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
+int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
+                        int cout, int stride, int pad, void* stream);
+/* Depthwise 3x3 s1 p1 (Attention.pe, yolo11_modules.py:122); input channel c reads source
+ * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
+int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
+                 uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks, void* stream);
+int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
+                 const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
+                 int c, int accumulate, void* stream);
+/* All conv weights fp32 OIHW -> bf16 fwd / dgrad layouts in one launch (table in device memory). */
+int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream);
+
+/* ------------------------------------------------------------------ BatchNorm2d (train) + SiLU
+ * Replaces BatchNorm2d + the shared in-place SiLU of Conv (models/yolo11_modules.py:24-33;
+ * eps 1e-3 / momentum 0.03 from yolo11_model.py:183-185).  z is the dense (m, c) conv output in
+ * fp16 (written by ym_conv_fwd with out_f32 = 2); dz (bf16) may overwrite it in place.
+ */
+int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count, const float* gamma,
+                   const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                   float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* stream);
+int ym_bn_eval_coeff(int c, const float* gamma, const float* beta, const float* running_mean,
+                     const float* running_var, float eps, float* scale, float* shift, void* stream);
+/* out_view = act(z*scale+shift) (+ res_view); act: 0 identity, 1 SiLU; hw = pixels per image */
+int ym_bn_apply(const uint16_t* z, int64_t m, int c, int hw, const float* scale, const float* shift, int act,
+                const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* out, int64_t o_bs, int64_t o_ld,
+                float* out32, void* stream);   /* out32: optional fp32 dense copy (SPPF pool chain) */
+int ym_bn_bwd_blocks(int64_t m, int c);
+int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
+                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
+                     float* part_sum, float* part_dot, void* stream);
+int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
+                       const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
+                       float* coef, void* stream);
+int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
+                    const float* scale, const float* shift, const float* mean, const float* rstd, int act,
+                    const float* coef, uint16_t* dz, void* stream);
+
+/* ------------------------------------------------------------------ graph ops
+ * SPPF max-pool (yolo11_modules.py:92-105), nearest 2x upsample (yaml head rows 11, 14),
+ * C2PSA attention core (yolo11_modules.py:124-136), view conversions, Detect grad split.
+ */
+int ym_maxpool5_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int n,
+                    int h, int w, int c, void* stream);
+/* dx_f32 (dense, +=) from dy_f32 (dense) through the argmax of each 5x5 window of x */
+int ym_maxpool5_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, const float* dy, float* dx, int n, int h, int w,
+                    int c, void* stream);
+/* SPPF's three chained pools on fp32 values (tie semantics of the fp32 reference): y32 and a bf16 view copy */
+int ym_maxpool5_f32_fwd(const float* x, float* y, uint16_t* yb, int64_t y_bs, int64_t y_ld, int n, int h, int w,
+                        int c, void* stream);
+int ym_maxpool5_f32_bwd(const float* x, const float* dy, float* dx, int n, int h, int w, int c, void* stream);
+int ym_upsample2_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int n,
+                     int h, int w, int c, void* stream);
+int ym_upsample2_bwd(const uint16_t* dy, int64_t d_bs, int64_t d_ld, uint16_t* dx, int64_t x_bs, int64_t x_ld, int n,
+                     int h, int w, int c, int accumulate, void* stream);
+int ym_view_to_f32(const uint16_t* x, int64_t bs, int64_t ld, float* y, int64_t m, int c, int hw, void* stream);
+int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t ld, int64_t m, int c, int hw, int accumulate,
+                   void* stream);
+/* dhead (B, A, 64+nc) fp32 rows of one pyramid level -> bf16 dz for the box / cls 1x1 convs
+ * (cls zero-padded to 8 channels) and bias grads (+=). */
+int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc, uint16_t* dz_box,
+                 uint16_t* dz_cls, float* dbias_box, float* dbias_cls, void* stream);
+int ym_attn_fwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, int b, int heads, int n, int key_dim, int head_dim,
+                float scale, uint16_t* out, int64_t o_bs, int64_t o_ld, float* lse, void* stream);
+size_t ym_attn_workspace_size(int b, int heads, int n);
+int ym_attn_bwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, const uint16_t* out, int64_t o_bs, int64_t o_ld,
+                const uint16_t* dout, int64_t d_bs, int64_t d_ld, const float* lse, int b, int heads, int n,
+                float scale, float* workspace, uint16_t* dqkv, int64_t g_bs, int64_t g_ld, int acc_q, int acc_k,
+                int acc_v, void* stream);
+/* dst_view = src_view (+ dst_view when accumulate); src NULL zero-fills dst */
+int ym_view_axpy(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int64_t m,
+                 int c, int hw, int accumulate, int half, void* stream);   /* half: 1 fp16 data, 0 bf16 */
+
+/* ------------------------------------------------------------------ detection loss + decode
+ * Replaces v8DetectionLoss.__call__ and its TaskAlignedAssigner / BboxLoss
+ * (losses/yolo_v8_loss.py:64-538) and Detect.inference (models/yolo11_modules.py:248-266).
+ * head: (B, A, 64+nc) fp32 rows, levels concatenated (level l: h[l] x w[l] anchors, stride[l]).
+ * Host arrays: level_h, level_w, strides.  Targets: the collate batch dict on the device
+ * (batch_idx int64 (N,), cls int64 (N,1), bboxes fp32 (N,4) normalised xyxy); M = max boxes
+ * per image.  gt_box (B,M,4) / gt_lab (B,M) / gt_valid (B,M) are caller-allocated outputs.
+ * out[0] = loss (sum(items) * B), out[1..3] = items (box, cls, dfl with gains), out[4] = tss,
+ * out[5] = number of foreground anchors.
+ */
+size_t ym_loss_workspace_size(int64_t B, int64_t A, int M);
+int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h, const int* level_w,
+                const float* strides, const int64_t* batch_idx, const int64_t* cls, const float* bboxes,
+                int64_t n_targets, int M, float imgsz_h, float imgsz_w, void* workspace, size_t workspace_bytes,
+                float* gt_box, float* gt_lab, int* gt_valid, float* out, void* stream);
+/* dhead = d(out[0] * grad_out[0]) / d head, using the assignment left in the workspace by ym_loss_fwd. */
+int ym_loss_bwd(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h, const int* level_w,
+                const float* strides, int M, void* workspace, size_t workspace_bytes, const float* gt_box,
+                const float* gt_lab, const float* out, const float* grad_out, float* dhead, void* stream);
+/* Device pointers to the assignment (target_gt_idx, fg_mask, target-score magnitude) in the workspace. */
+int ym_loss_assignment(void* workspace, int64_t B, int64_t A, int M, const int** tgi, const int** fg,
+                       const float** norm);
+/* y (B, 4+nc, A): xywh * stride from the DFL projection with weights dfl_w[16], sigmoid(cls). */
+int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h,
+                     const int* level_w, const float* strides, const float* dfl_w, float* y, void* stream);
 
 #ifdef __cplusplus
 }

@@ -257,8 +257,8 @@ def inference(P, pre, outs, nc, strides):
     return torch.cat((dbox, cls.sigmoid()), 1)
 
 
-def forward(P, layers, save, x, training=True, strides=(8.0, 16.0, 32.0)):
-    """YOLOv11._forward_once (yolo11_model.py:60-71)."""
+def forward(P, layers, save, x, training=True, strides=(8.0, 16.0, 32.0), keep_all=None):
+    """YOLOv11._forward_once (yolo11_model.py:60-71).  keep_all: optional list receiving every layer output."""
     ys = []
     for L in layers:
         f, t, pre = L["f"], L["type"], f"model.{L['i']}"
@@ -279,6 +279,8 @@ def forward(P, layers, save, x, training=True, strides=(8.0, 16.0, 32.0)):
         else:
             x = F.interpolate(x, scale_factor=2.0, mode="nearest")
         ys.append(x if L["i"] in save else None)
+        if keep_all is not None:
+            keep_all.append(x)
     return x
 
 

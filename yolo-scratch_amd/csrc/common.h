@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -40,6 +41,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
     if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
     u += 0x7fffu + ((u >> 16) & 1u);
     return (bf16_t)(u >> 16);
+}
+
+// fp16 bits <-> f32 (pre-BatchNorm conv outputs are kept in fp16: 3 more mantissa bits than
+// bf16 where normalisation amplifies rounding; |z| is clamped below the fp16 range)
+__device__ __forceinline__ float h2f(uint16_t v) { return __half2float(__ushort_as_half(v)); }
+__device__ __forceinline__ uint16_t f2h(float f) {
+    f = fminf(fmaxf(f, -65504.f), 65504.f);
+    return __half_as_ushort(__float2half(f));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -1,0 +1,671 @@
+// Non-GEMM graph ops of the YOLOv11 neck/backbone, NHWC bf16 (gfx950):
+//   SPPF max-pool 5x5 s1 p2 fwd/bwd     (yolo11_modules.py:92-105)
+//   nearest 2x upsample fwd/bwd         (configs/yolo11n_crater.yaml head rows 0, 3; nn.Upsample)
+//   C2PSA attention core fwd/bwd        (yolo11_modules.py:124-136): softmax(q^T k * kd^-0.5), v attn^T
+//   dtype/view conversions and the Detect-head gradient split (+ bias grads)
+// Activation buffers are fp16, gradient buffers bf16 (see yolomi/graph.py).
+#include <algorithm>
+
+#include "common.h"
+
+namespace ym {
+namespace {
+
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = bf2f(bf16_t(w[i] & 0xffff));
+        f[2 * i + 1] = bf2f(bf16_t(w[i] >> 16));
+    }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// activations are fp16, gradients bf16
+__device__ __forceinline__ void unpack8h(uint4 v, float* f) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f[2 * i] = h2f(uint16_t(w[i] & 0xffff));
+        f[2 * i + 1] = h2f(uint16_t(w[i] >> 16));
+    }
+}
+__device__ __forceinline__ uint4 pack8h(const float* f) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2h(f[2 * i])) | (uint32_t(f2h(f[2 * i + 1])) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+int grid_for(int64_t work, int threads = 256, int cap = 8192) {
+    int64_t g = (work + threads - 1) / threads;
+    return int(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
+}
+
+// ------------------------------------------------------------------ max pool 5x5, stride 1, pad 2
+__global__ void maxpool5_fwd_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld, bf16_t* __restrict__ y,
+                                    int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
+    const int cg = C / 8;
+    const int64_t total = int64_t(N) * H * W * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg;
+        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
+        int h = int(pix / W), w = int(pix % W);
+        float mx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mx[k] = -INFINITY;
+        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
+            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
+                float v[8];
+                unpack8h(*reinterpret_cast<const uint4*>(x + n * x_bs + (int64_t(ih) * W + iw) * x_ld + g * 8), v);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) mx[k] = (v[k] > mx[k] || v[k] != v[k]) ? v[k] : mx[k];
+            }
+        *reinterpret_cast<uint4*>(y + n * y_bs + pix * y_ld + g * 8) = pack8h(mx);
+    }
+}
+
+// fp32 chain for SPPF: y32 = maxpool(x32) and its bf16 copy into the concat slice
+__global__ void maxpool5_f32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, bf16_t* __restrict__ yb,
+                                        int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
+    const int64_t total = int64_t(N) * H * W * C;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int c = int(i % C);
+        int64_t m = i / C;
+        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
+        int h = int(pix / W), w = int(pix % W);
+        float mx = -INFINITY;
+        bool first = true;
+        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
+            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
+                float v = x[(n * H * W + int64_t(ih) * W + iw) * C + c];
+                if (v > mx || v != v || first) { mx = v; first = false; }
+            }
+        y[m * C + c] = mx;
+        yb[n * y_bs + pix * y_ld + c] = f2h(mx);
+    }
+}
+
+__global__ void maxpool5_f32_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                        float* __restrict__ dx, int N, int H, int W, int C) {
+    const int64_t total = int64_t(N) * H * W * C;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int c = int(i % C);
+        int64_t m = i / C;
+        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
+        int h = int(pix / W), w = int(pix % W);
+        float mx = -INFINITY;
+        int64_t arg = -1;
+        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
+            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
+                float v = x[(n * H * W + int64_t(ih) * W + iw) * C + c];
+                if (v > mx || v != v || arg < 0) { mx = v; arg = int64_t(ih) * W + iw; }
+            }
+        float g = dy[m * C + c];
+        if (g != 0.f) atomicAdd(&dx[(n * H * W + arg) * C + c], g);
+    }
+}
+
+// dx_f32[argmax] += dy_f32 (first maximal element in kh-major scan order, as ATen's CPU kernel)
+__global__ void maxpool5_bwd_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld,
+                                    const float* __restrict__ dy, float* __restrict__ dx, int N, int H, int W, int C) {
+    const int64_t total = int64_t(N) * H * W * C;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int c = int(i % C);
+        int64_t m = i / C;
+        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
+        int h = int(pix / W), w = int(pix % W);
+        float mx = -INFINITY;
+        int64_t arg = -1;
+        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
+            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
+                float v = h2f(x[n * x_bs + (int64_t(ih) * W + iw) * x_ld + c]);
+                if (v > mx || v != v || arg < 0) { mx = v; arg = int64_t(ih) * W + iw; }
+            }
+        float g = dy[m * C + c];
+        if (g != 0.f) atomicAdd(&dx[(n * H * W + arg) * C + c], g);
+    }
+}
+
+// ------------------------------------------------------------------ nearest 2x upsample
+__global__ void upsample2_fwd_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld, bf16_t* __restrict__ y,
+                                     int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
+    const int cg = C / 8, OH = 2 * H, OW = 2 * W;
+    const int64_t total = int64_t(N) * OH * OW * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg;
+        int64_t n = m / (int64_t(OH) * OW), pix = m - n * OH * OW;
+        int oh = int(pix / OW), ow = int(pix % OW);
+        uint4 v = *reinterpret_cast<const uint4*>(x + n * x_bs + (int64_t(oh >> 1) * W + (ow >> 1)) * x_ld + g * 8);
+        *reinterpret_cast<uint4*>(y + n * y_bs + pix * y_ld + g * 8) = v;
+    }
+}
+
+__global__ void upsample2_bwd_kernel(const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld, bf16_t* __restrict__ dx,
+                                     int64_t x_bs, int64_t x_ld, int N, int H, int W, int C, int accumulate) {
+    const int cg = C / 8, OW = 2 * W;
+    const int64_t total = int64_t(N) * H * W * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg;
+        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
+        int h = int(pix / W), w = int(pix % W);
+        float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int a = 0; a < 2; ++a)
+            for (int b = 0; b < 2; ++b) {
+                float v[8];
+                unpack8(*reinterpret_cast<const uint4*>(dy + n * d_bs + (int64_t(2 * h + a) * OW + 2 * w + b) * d_ld + g * 8), v);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s[k] += v[k];
+            }
+        bf16_t* o = dx + n * x_bs + pix * x_ld + g * 8;
+        if (accumulate) {
+            float v[8];
+            unpack8(*reinterpret_cast<const uint4*>(o), v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s[k] += v[k];
+        }
+        *reinterpret_cast<uint4*>(o) = pack8(s);
+    }
+}
+
+// ------------------------------------------------------------------ conversions
+__global__ void view_to_f32_kernel(const bf16_t* __restrict__ x, int64_t bs, int64_t ld, float* __restrict__ y,
+                                   int64_t M, int C, int HW) {
+    const int cg = C / 8;
+    const int64_t total = M * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg, n = m / HW, pix = m - n * HW;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + n * bs + pix * ld + g * 8), v);
+        float4* o = reinterpret_cast<float4*>(y + m * C + g * 8);
+        o[0] = make_float4(v[0], v[1], v[2], v[3]);
+        o[1] = make_float4(v[4], v[5], v[6], v[7]);
+    }
+}
+
+__global__ void f32_to_view_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t bs, int64_t ld,
+                                   int64_t M, int C, int HW, int accumulate) {
+    const int cg = C / 8;
+    const int64_t total = M * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg, n = m / HW, pix = m - n * HW;
+        const float4* s = reinterpret_cast<const float4*>(x + m * C + g * 8);
+        float4 a = s[0], b = s[1];
+        float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        bf16_t* o = y + n * bs + pix * ld + g * 8;
+        if (accumulate) {
+            float u[8];
+            unpack8(*reinterpret_cast<const uint4*>(o), u);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] += u[k];
+        }
+        *reinterpret_cast<uint4*>(o) = pack8(v);
+    }
+}
+
+// dst_view = src_view (+ dst_view); zero-fill when src is null
+__global__ void view_axpy_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld, bf16_t* __restrict__ y,
+                                 int64_t y_bs, int64_t y_ld, int64_t M, int C, int HW, int accumulate, int half) {
+    const int cg = C / 8;
+    const int64_t total = M * cg;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % cg);
+        int64_t m = i / cg, n = m / HW, pix = m - n * HW;
+        bf16_t* o = y + n * y_bs + pix * y_ld + g * 8;
+        if (!x) { *reinterpret_cast<uint4*>(o) = make_uint4(0, 0, 0, 0); continue; }
+        uint4 v = *reinterpret_cast<const uint4*>(x + n * x_bs + pix * x_ld + g * 8);
+        if (accumulate) {
+            float a[8], b[8];
+            if (half) { unpack8h(v, a); unpack8h(*reinterpret_cast<const uint4*>(o), b); }
+            else { unpack8(v, a); unpack8(*reinterpret_cast<const uint4*>(o), b); }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) a[k] += b[k];
+            v = half ? pack8h(a) : pack8(a);
+        }
+        *reinterpret_cast<uint4*>(o) = v;
+    }
+}
+
+// ------------------------------------------------------------------ Detect head gradient split
+// dhead (B, A, 64+nc) fp32 rows for one level (anchor offset `aoff`, HW anchors per image) ->
+// dz_box bf16 [M][64], dz_cls bf16 [M][8] (nc <= 8, zero padded), bias grads (+=, atomics)
+__global__ void head_grad_kernel(const float* __restrict__ dh, int64_t A, int64_t aoff, int HW, int64_t M, int nc,
+                                 bf16_t* __restrict__ dbox, bf16_t* __restrict__ dcls, float* __restrict__ dbias_box,
+                                 float* __restrict__ dbias_cls) {
+    __shared__ float red[72];
+    const int no = 64 + nc;
+    for (int i = threadIdx.x; i < 72; i += blockDim.x) red[i] = 0.f;
+    __syncthreads();
+    // thread -> (pixel, 8-channel group); 9 groups: 8 box + 1 cls
+    const int64_t total = M * 9;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
+        int g = int(i % 9);
+        int64_t m = i / 9;
+        int64_t n = m / HW, pix = m - n * HW;
+        const float* row = dh + (n * A + aoff + pix) * no;
+        float v[8];
+        if (g < 8) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = row[g * 8 + k];
+            *reinterpret_cast<uint4*>(dbox + m * 64 + g * 8) = pack8(v);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = k < nc ? row[64 + k] : 0.f;
+            *reinterpret_cast<uint4*>(dcls + m * 8) = pack8(v);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(&red[g * 8 + k], v[k]);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 + nc; i += blockDim.x) {
+        if (i < 64) atomicAdd(&dbias_box[i], red[i]);
+        else atomicAdd(&dbias_cls[i - 64], red[i]);
+    }
+}
+
+// ------------------------------------------------------------------ attention core (flash-style, fp32 VALU)
+constexpr int KD = 32, HD = 64, QT = 64;
+
+struct AttnArgs {
+    const bf16_t* qkv; int64_t q_bs, q_ld;   // per head h: q = h*(2KD+HD) + [0,KD), k = +KD, v = +2KD
+    int N, heads;
+    float scale;
+};
+
+__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a, bf16_t* __restrict__ out, int64_t o_bs, int64_t o_ld,
+                                                       float* __restrict__ lse) {
+    __shared__ float Ks[QT][KD + 1];
+    __shared__ float Vs[QT][HD + 1];
+    __shared__ float Ps[QT][QT + 1];
+    const int t = threadIdx.x, qi = t >> 2, sub = t & 3;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int i = blockIdx.x * QT + qi;
+    const int hs = 2 * KD + HD;
+    const bf16_t* base = a.qkv + int64_t(b) * a.q_bs + h * hs;
+    float q[KD];
+    if (i < a.N) {
+#pragma unroll
+        for (int c = 0; c < KD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(i) * a.q_ld + c * 8), q + c * 8);
+    } else {
+#pragma unroll
+        for (int d = 0; d < KD; ++d) q[d] = 0.f;
+    }
+    float o[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[e] = 0.f;
+    float m = -INFINITY, l = 0.f;
+    for (int k0 = 0; k0 < a.N; k0 += QT) {
+        {   // K tile: 64 keys x 32 d
+            int key = t >> 2, d0 = (t & 3) * 8;
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (k0 + key < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(k0 + key) * a.q_ld + KD + d0), v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Ks[key][d0 + e] = v[e];
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {   // V tile: 64 keys x 64 d
+            int id = t + 256 * it, key = id >> 3, d0 = (id & 7) * 8;
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (k0 + key < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(k0 + key) * a.q_ld + 2 * KD + d0), v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Vs[key][d0 + e] = v[e];
+        }
+        __syncthreads();
+        float s[16];
+        float tmax = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            int kk = sub * 16 + e;
+            float acc = 0.f;
+#pragma unroll
+            for (int d = 0; d < KD; ++d) acc += q[d] * Ks[kk][d];
+            s[e] = (k0 + kk < a.N) ? acc * a.scale : -INFINITY;
+            tmax = fmaxf(tmax, s[e]);
+        }
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 1, 64));
+        tmax = fmaxf(tmax, __shfl_xor(tmax, 2, 64));
+        const float mn = fmaxf(m, tmax);
+        const float alpha = __expf(m - mn);
+        float psum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            float p = __expf(s[e] - mn);
+            Ps[qi][sub * 16 + e] = p;
+            psum += p;
+        }
+        psum += __shfl_xor(psum, 1, 64);
+        psum += __shfl_xor(psum, 2, 64);
+        l = l * alpha + psum;
+        m = mn;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[e] *= alpha;
+        __syncthreads();
+        for (int kk = 0; kk < QT; ++kk) {
+            float p = Ps[qi][kk];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[e] += p * Vs[kk][sub * 16 + e];
+        }
+        __syncthreads();
+    }
+    if (i < a.N) {
+        float inv = 1.0f / l;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[e] *= inv;
+        bf16_t* op = out + int64_t(b) * o_bs + int64_t(i) * o_ld + h * HD + sub * 16;
+        *reinterpret_cast<uint4*>(op) = pack8h(o);
+        *reinterpret_cast<uint4*>(op + 8) = pack8h(o + 8);
+        if (sub == 0) lse[(int64_t(b) * a.heads + h) * a.N + i] = m + __logf(l);
+    }
+}
+
+// D[b,h,i] = sum_d dO[i][h*HD+d] * O[i][h*HD+d]
+__global__ void attn_bwd_pre_kernel(const bf16_t* __restrict__ o, int64_t o_bs, int64_t o_ld, const bf16_t* __restrict__ dout,
+                                    int64_t d_bs, int64_t d_ld, int B, int heads, int N, float* __restrict__ D) {
+    int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (idx >= int64_t(B) * heads * N) return;
+    int i = int(idx % N);
+    int h = int((idx / N) % heads);
+    int b = int(idx / (int64_t(N) * heads));
+    float s = 0.f;
+    for (int c = 0; c < HD / 8; ++c) {
+        float x[8], y[8];
+        unpack8h(*reinterpret_cast<const uint4*>(o + int64_t(b) * o_bs + int64_t(i) * o_ld + h * HD + c * 8), x);
+        unpack8(*reinterpret_cast<const uint4*>(dout + int64_t(b) * d_bs + int64_t(i) * d_ld + h * HD + c * 8), y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += x[k] * y[k];
+    }
+    D[idx] = s;
+}
+
+// block owns 64 keys of one (b, h); loops over query tiles; dq via fp32 atomics
+__global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a, const bf16_t* __restrict__ dout, int64_t d_bs,
+                                                       int64_t d_ld, const float* __restrict__ lse,
+                                                       const float* __restrict__ D, bf16_t* __restrict__ dqkv,
+                                                       int64_t g_bs, int64_t g_ld, float* __restrict__ dq,
+                                                       int acc_k, int acc_v) {
+    __shared__ float Qs[QT][KD + 1];
+    __shared__ float dOs[QT][HD + 1];
+    __shared__ float Ks[QT][KD + 1];
+    __shared__ float PT[QT][QT + 1];
+    __shared__ float dST[QT][QT + 1];
+    __shared__ float Ls[QT], Ds[QT];
+    const int t = threadIdx.x, kk = t >> 2, sub = t & 3;
+    const int h = blockIdx.y, b = blockIdx.z;
+    const int j = blockIdx.x * QT + kk;
+    const int hs = 2 * KD + HD;
+    const bf16_t* base = a.qkv + int64_t(b) * a.q_bs + h * hs;
+    float kr[KD], vr[HD];
+    if (j < a.N) {
+#pragma unroll
+        for (int c = 0; c < KD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(j) * a.q_ld + KD + c * 8), kr + c * 8);
+#pragma unroll
+        for (int c = 0; c < HD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(j) * a.q_ld + 2 * KD + c * 8), vr + c * 8);
+    } else {
+#pragma unroll
+        for (int d = 0; d < KD; ++d) kr[d] = 0.f;
+#pragma unroll
+        for (int d = 0; d < HD; ++d) vr[d] = 0.f;
+    }
+    {   // K tile in LDS for the dq product
+        int key = t >> 2, d0 = (t & 3) * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Ks[key][d0 + e] = kr[d0 + e];
+    }
+    float dk[8], dv[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dk[e] = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) dv[e] = 0.f;
+    const float* lse_bh = lse + (int64_t(b) * a.heads + h) * a.N;
+    const float* D_bh = D + (int64_t(b) * a.heads + h) * a.N;
+    for (int q0 = 0; q0 < a.N; q0 += QT) {
+        {
+            int qq = t >> 2, d0 = (t & 3) * 8;
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (q0 + qq < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(q0 + qq) * a.q_ld + d0), v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) Qs[qq][d0 + e] = v[e];
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            int id = t + 256 * it, qq = id >> 3, d0 = (id & 7) * 8;
+            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (q0 + qq < a.N)
+                unpack8(*reinterpret_cast<const uint4*>(dout + int64_t(b) * d_bs + int64_t(q0 + qq) * d_ld + h * HD + d0), v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dOs[qq][d0 + e] = v[e];
+        }
+        if (t < QT) {
+            bool ok = q0 + t < a.N;
+            Ls[t] = ok ? lse_bh[q0 + t] : INFINITY;
+            Ds[t] = ok ? D_bh[q0 + t] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int e = 0; e < 16; ++e) {
+            int qi = sub * 16 + e;
+            float s = 0.f, dp = 0.f;
+#pragma unroll
+            for (int d = 0; d < KD; ++d) s += Qs[qi][d] * kr[d];
+#pragma unroll
+            for (int d = 0; d < HD; ++d) dp += dOs[qi][d] * vr[d];
+            float p = (j < a.N) ? __expf(s * a.scale - Ls[qi]) : 0.f;
+            PT[kk][qi] = p;
+            dST[kk][qi] = p * (dp - Ds[qi]);
+        }
+        __syncthreads();
+        for (int qi = 0; qi < QT; ++qi) {
+            float p = PT[kk][qi], ds = dST[kk][qi];
+#pragma unroll
+            for (int e = 0; e < 16; ++e) dv[e] += p * dOs[qi][sub * 16 + e];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dk[e] += ds * Qs[qi][sub * 8 + e];
+        }
+        {   // dq for query (t>>2), d in sub*8 .. +8
+            int qi = t >> 2;
+            if (q0 + qi < a.N) {
+                float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                for (int k2 = 0; k2 < QT; ++k2) {
+                    float ds = dST[k2][qi];
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) acc[e] += ds * Ks[k2][sub * 8 + e];
+                }
+                float* dqp = dq + (int64_t(b) * a.N + q0 + qi) * (a.heads * KD) + h * KD + sub * 8;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) atomicAdd(dqp + e, acc[e] * a.scale);
+            }
+        }
+        __syncthreads();
+    }
+    if (j < a.N) {
+        bf16_t* g = dqkv + int64_t(b) * g_bs + int64_t(j) * g_ld + h * hs;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dk[e] *= a.scale;
+        bf16_t* pk = g + KD + sub * 8;
+        bf16_t* pv = g + 2 * KD + sub * 16;
+        if (acc_k) {
+            float u[8];
+            unpack8(*reinterpret_cast<const uint4*>(pk), u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dk[e] += u[e];
+        }
+        if (acc_v) {
+            float u[8];
+            unpack8(*reinterpret_cast<const uint4*>(pv), u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dv[e] += u[e];
+            unpack8(*reinterpret_cast<const uint4*>(pv + 8), u);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dv[8 + e] += u[e];
+        }
+        *reinterpret_cast<uint4*>(pk) = pack8(dk);
+        *reinterpret_cast<uint4*>(pv) = pack8(dv);
+        *reinterpret_cast<uint4*>(pv + 8) = pack8(dv + 8);
+    }
+}
+
+// dq fp32 [B][N][heads*KD] -> q channels of dqkv
+__global__ void attn_dq_store_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv, int64_t g_bs, int64_t g_ld,
+                                     int B, int N, int heads, int accumulate) {
+    int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;   // one per (b, i, h, 8-chunk)
+    const int per = heads * (KD / 8);
+    if (idx >= int64_t(B) * N * per) return;
+    int c = int(idx % per);
+    int64_t bi = idx / per;
+    int h = c / (KD / 8), d0 = (c % (KD / 8)) * 8;
+    int64_t b = bi / N, i = bi % N;
+    const float* s = dq + bi * (heads * KD) + h * KD + d0;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = s[e];
+    bf16_t* o = dqkv + b * g_bs + i * g_ld + h * (2 * KD + HD) + d0;
+    if (accumulate) {
+        float u[8];
+        unpack8(*reinterpret_cast<const uint4*>(o), u);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += u[e];
+    }
+    *reinterpret_cast<uint4*>(o) = pack8(v);
+}
+
+}  // namespace
+}  // namespace ym
+
+using namespace ym;
+
+#define VIEW_ALIGNED(bs, ld) ((bs) % 8 == 0 && (ld) % 8 == 0)
+
+extern "C" int ym_maxpool5_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld,
+                               int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(x_bs, x_ld) && VIEW_ALIGNED(y_bs, y_ld), "ym_maxpool5_fwd: alignment");
+    hipLaunchKernelGGL(maxpool5_fwd_kernel, dim3(grid_for(int64_t(n) * h * w * (c / 8))), dim3(256), 0,
+                       as_stream(stream), x, x_bs, x_ld, y, y_bs, y_ld, n, h, w, c);
+    YM_LAUNCH_CHECK("ym_maxpool5_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_maxpool5_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, const float* dy, float* dx, int n, int h,
+                               int w, int c, void* stream) {
+    hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0, as_stream(stream), x,
+                       x_bs, x_ld, dy, dx, n, h, w, c);
+    YM_LAUNCH_CHECK("ym_maxpool5_bwd");
+    return YM_OK;
+}
+
+extern "C" int ym_maxpool5_f32_fwd(const float* x, float* y, uint16_t* yb, int64_t y_bs, int64_t y_ld, int n, int h,
+                                   int w, int c, void* stream) {
+    hipLaunchKernelGGL(maxpool5_f32_fwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0,
+                       as_stream(stream), x, y, yb, y_bs, y_ld, n, h, w, c);
+    YM_LAUNCH_CHECK("ym_maxpool5_f32_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_maxpool5_f32_bwd(const float* x, const float* dy, float* dx, int n, int h, int w, int c,
+                                   void* stream) {
+    hipLaunchKernelGGL(maxpool5_f32_bwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0,
+                       as_stream(stream), x, dy, dx, n, h, w, c);
+    YM_LAUNCH_CHECK("ym_maxpool5_f32_bwd");
+    return YM_OK;
+}
+
+extern "C" int ym_upsample2_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld,
+                                int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(x_bs, x_ld) && VIEW_ALIGNED(y_bs, y_ld), "ym_upsample2_fwd: alignment");
+    hipLaunchKernelGGL(upsample2_fwd_kernel, dim3(grid_for(int64_t(n) * 4 * h * w * (c / 8))), dim3(256), 0,
+                       as_stream(stream), x, x_bs, x_ld, y, y_bs, y_ld, n, h, w, c);
+    YM_LAUNCH_CHECK("ym_upsample2_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_upsample2_bwd(const uint16_t* dy, int64_t d_bs, int64_t d_ld, uint16_t* dx, int64_t x_bs,
+                                int64_t x_ld, int n, int h, int w, int c, int accumulate, void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(d_bs, d_ld) && VIEW_ALIGNED(x_bs, x_ld), "ym_upsample2_bwd: alignment");
+    hipLaunchKernelGGL(upsample2_bwd_kernel, dim3(grid_for(int64_t(n) * h * w * (c / 8))), dim3(256), 0,
+                       as_stream(stream), dy, d_bs, d_ld, dx, x_bs, x_ld, n, h, w, c, accumulate);
+    YM_LAUNCH_CHECK("ym_upsample2_bwd");
+    return YM_OK;
+}
+
+extern "C" int ym_view_axpy(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld,
+                            int64_t m, int c, int hw, int accumulate, int half, void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(y_bs, y_ld) && (!x || VIEW_ALIGNED(x_bs, x_ld)), "ym_view_axpy: alignment");
+    if (m == 0) return YM_OK;
+    hipLaunchKernelGGL(view_axpy_kernel, dim3(grid_for(m * (c / 8))), dim3(256), 0, as_stream(stream), x, x_bs, x_ld, y,
+                       y_bs, y_ld, m, c, hw, accumulate, half);
+    YM_LAUNCH_CHECK("ym_view_axpy");
+    return YM_OK;
+}
+
+extern "C" int ym_view_to_f32(const uint16_t* x, int64_t bs, int64_t ld, float* y, int64_t m, int c, int hw,
+                              void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(bs, ld), "ym_view_to_f32: alignment");
+    hipLaunchKernelGGL(view_to_f32_kernel, dim3(grid_for(m * (c / 8))), dim3(256), 0, as_stream(stream), x, bs, ld, y, m,
+                       c, hw);
+    YM_LAUNCH_CHECK("ym_view_to_f32");
+    return YM_OK;
+}
+
+extern "C" int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t ld, int64_t m, int c, int hw,
+                              int accumulate, void* stream) {
+    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(bs, ld), "ym_f32_to_view: alignment");
+    hipLaunchKernelGGL(f32_to_view_kernel, dim3(grid_for(m * (c / 8))), dim3(256), 0, as_stream(stream), x, y, bs, ld, m,
+                       c, hw, accumulate);
+    YM_LAUNCH_CHECK("ym_f32_to_view");
+    return YM_OK;
+}
+
+extern "C" int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc,
+                            uint16_t* dz_box, uint16_t* dz_cls, float* dbias_box, float* dbias_cls, void* stream) {
+    YM_CHECK_ARG(nc >= 1 && nc <= 8, "ym_head_grad: nc must be in [1, 8]");
+    hipLaunchKernelGGL(head_grad_kernel, dim3(grid_for(m * 9, 256, 2048)), dim3(256), 0, as_stream(stream), dhead,
+                       a_total, a_off, hw, m, nc, dz_box, dz_cls, dbias_box, dbias_cls);
+    YM_LAUNCH_CHECK("ym_head_grad");
+    return YM_OK;
+}
+
+extern "C" int ym_attn_fwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, int b, int heads, int n, int key_dim,
+                           int head_dim, float scale, uint16_t* out, int64_t o_bs, int64_t o_ld, float* lse,
+                           void* stream) {
+    YM_CHECK_ARG(key_dim == KD && head_dim == HD, "ym_attn_fwd: only key_dim=32, head_dim=64 (got %d, %d)", key_dim,
+                 head_dim);
+    AttnArgs a{qkv, q_bs, q_ld, n, heads, scale};
+    hipLaunchKernelGGL(attn_fwd_kernel, dim3((n + QT - 1) / QT, heads, b), dim3(256), 0, as_stream(stream), a, out,
+                       o_bs, o_ld, lse);
+    YM_LAUNCH_CHECK("ym_attn_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_attn_bwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, const uint16_t* out, int64_t o_bs,
+                           int64_t o_ld, const uint16_t* dout, int64_t d_bs, int64_t d_ld, const float* lse, int b,
+                           int heads, int n, float scale, float* workspace, uint16_t* dqkv, int64_t g_bs, int64_t g_ld,
+                           int acc_q, int acc_k, int acc_v, void* stream) {
+    // workspace: D [b*heads*n] + dq [b*n*heads*KD] fp32
+    hipStream_t st = as_stream(stream);
+    float* D = workspace;
+    float* dq = workspace + int64_t(b) * heads * n;
+    int64_t nD = int64_t(b) * heads * n;
+    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3(unsigned((nD + 255) / 256)), dim3(256), 0, st, out, o_bs, o_ld, dout,
+                       d_bs, d_ld, b, heads, n, D);
+    if (hipMemsetAsync(dq, 0, size_t(b) * n * heads * KD * sizeof(float), st) != hipSuccess) return YM_ERR_HIP;
+    AttnArgs a{qkv, q_bs, q_ld, n, heads, scale};
+    hipLaunchKernelGGL(attn_bwd_kernel, dim3((n + QT - 1) / QT, heads, b), dim3(256), 0, st, a, dout, d_bs, d_ld, lse, D,
+                       dqkv, g_bs, g_ld, dq, acc_k, acc_v);
+    int64_t nq = int64_t(b) * n * heads * (KD / 8);
+    hipLaunchKernelGGL(attn_dq_store_kernel, dim3(unsigned((nq + 255) / 256)), dim3(256), 0, st, dq, dqkv, g_bs, g_ld, b,
+                       n, heads, acc_q);
+    YM_LAUNCH_CHECK("ym_attn_bwd");
+    return YM_OK;
+}
+
+extern "C" size_t ym_attn_workspace_size(int b, int heads, int n) {
+    return (size_t(b) * heads * n + size_t(b) * n * heads * KD) * sizeof(float);
+}

@@ -17,14 +17,67 @@ LIB_PATH = Path(os.environ.get("YOLOMI_LIB", _PKG / "libyolomi.so"))
 _c = ctypes
 P, I64, I32, F32, SZ = _c.c_void_p, _c.c_int64, _c.c_int32, _c.c_float, _c.c_size_t
 
+INT, F64 = _c.c_int, _c.c_double
+
+
+class ConvDesc(ctypes.Structure):
+    """ym_conv_desc (include/yolomi.h)."""
+    _fields_ = [("n", I32), ("h", I32), ("w", I32), ("cin", I32), ("oh", I32), ("ow", I32), ("cout", I32),
+                ("k", I32), ("stride", I32), ("pad", I32), ("x_bs", I64), ("x_ld", I64), ("y_bs", I64),
+                ("y_ld", I64), ("out_f32", I32), ("accumulate", I32)]
+
+
+class WPrepEntry(ctypes.Structure):
+    """ym_wprep_entry (include/yolomi.h)."""
+    _fields_ = [("src", P), ("dst_fwd", P), ("dst_t", P), ("elem_offset", I64), ("cout", I32), ("cin", I32),
+                ("kh", I32), ("kw", I32), ("cout_t", I32)]
+
+
+R = _c.c_int
 # name -> (restype, argtypes); must match include/yolomi.h
 SIGNATURES = {
     "ym_last_error": (_c.c_char_p, []),
-    "ym_version": (_c.c_int, []),
-    "ym_iou_row": (_c.c_int, [P, P, I64, P, P]),
+    "ym_version": (R, []),
+    "ym_iou_row": (R, [P, P, I64, P, P]),
     "ym_nms_workspace_size": (SZ, [I64, I64]),
-    "ym_decode_nms": (_c.c_int, [P, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
-    "ym_nms": (_c.c_int, [P, P, I64, F32, P, SZ, P, P, P]),
+    "ym_decode_nms": (R, [P, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
+    "ym_nms": (R, [P, P, I64, F32, P, SZ, P, P, P]),
+    "ym_conv_stat_blocks": (R, [I64, INT]),
+    "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
+    "ym_conv_dgrad": (R, [P, P, P, P, P]),
+    "ym_conv_wgrad": (R, [P, P, P, P, P]),
+    "ym_wgrad_to_oihw": (R, [P, P, INT, INT, INT, INT, P]),
+    "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
+    "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P]),
+    "ym_prep_weights": (R, [P, INT, I64, P]),
+    "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P]),
+    "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
+    "ym_bn_apply": (R, [P, I64, INT, INT, P, P, INT, P, I64, I64, P, I64, I64, P, P]),
+    "ym_bn_bwd_blocks": (R, [I64, INT]),
+    "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
+    "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P]),
+    "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
+    "ym_maxpool5_fwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, P]),
+    "ym_maxpool5_bwd": (R, [P, I64, I64, P, P, INT, INT, INT, INT, P]),
+    "ym_maxpool5_f32_fwd": (R, [P, P, P, I64, I64, INT, INT, INT, INT, P]),
+    "ym_maxpool5_f32_bwd": (R, [P, P, P, INT, INT, INT, INT, P]),
+    "ym_upsample2_fwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, P]),
+    "ym_upsample2_bwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, INT, P]),
+    "ym_view_to_f32": (R, [P, I64, I64, P, I64, INT, INT, P]),
+    "ym_f32_to_view": (R, [P, P, I64, I64, I64, INT, INT, INT, P]),
+    "ym_view_axpy": (R, [P, I64, I64, P, I64, I64, I64, INT, INT, INT, INT, P]),
+    "ym_head_grad": (R, [P, I64, I64, INT, I64, INT, P, P, P, P, P]),
+    "ym_attn_fwd": (R, [P, I64, I64, INT, INT, INT, INT, INT, F32, P, I64, I64, P, P]),
+    "ym_attn_workspace_size": (SZ, [INT, INT, INT]),
+    "ym_attn_bwd": (R, [P, I64, I64, P, I64, I64, P, I64, I64, P, INT, INT, INT, F32, P, P, I64, I64, INT, INT, INT,
+                        P]),
+    "ym_loss_workspace_size": (SZ, [I64, I64, INT]),
+    "ym_loss_fwd": (R, [P, I64, I64, INT, INT, P, P, P, P, P, P, I64, INT, F32, F32, P, SZ, P, P, P, P, P]),
+    "ym_loss_bwd": (R, [P, I64, I64, INT, INT, P, P, P, INT, P, SZ, P, P, P, P, P, P]),
+    "ym_loss_assignment": (R, [P, I64, I64, INT, P, P, P]),
+    "ym_detect_decode": (R, [P, I64, I64, INT, INT, P, P, P, P, P, P]),
 }
 
 _LIB = None

@@ -1,0 +1,893 @@
+"""NHWC execution plan for the YOLOv11 module tree on MI355X.
+
+A module (the whole YOLOv11 or any building block: Conv, C3k2, SPPF, C2PSA,
+Detect ...) is lowered ONCE per input shape into a flat list of ops over
+preallocated NHWC activation buffers (fp16; gradients bf16).  Concatenations and splits of the
+reference (yolo11_modules.py C2f:59-63, C3k:78, SPPF:104-105, PSA:156-159,
+C2PSA:175-177, Concat:284-285, yaml head rows) become channel slices: every
+producer writes straight into its slice of the consumer's buffer.  Forward
+runs the ops in order; backward runs them in reverse over a mirrored set of
+gradient buffers, deciding per slice whether to overwrite or accumulate.
+
+Every arithmetic step is a libyolomi kernel; this file only plans buffers and
+launches.  Parameter gradients land in one flat fp32 buffer per plan
+(`Plan.grad_flat`), with each parameter's `.grad` a view of it, so the
+data-parallel all-reduce is one RCCL call.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from ._lib import ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
+
+BF16 = torch.bfloat16
+F16 = torch.float16
+F32 = torch.float32
+ACT_DTYPE, GRAD_DTYPE = F16, BF16      # activations fp16 (precision), gradients bf16 (range)
+BN_EPS, BN_MOM = 1e-3, 0.03
+
+
+# ----------------------------------------------------------------------------- buffers
+class Act:
+    """One NHWC activation buffer (B, H, W, C) and its gradient mirror."""
+
+    def __init__(self, plan, C, H, W, dtype=ACT_DTYPE, name=""):
+        self.plan, self.C, self.H, self.W, self.dtype, self.name = plan, C, H, W, dtype, name
+        self.t = torch.empty(plan.B, H, W, C, dtype=dtype, device=plan.dev)
+        self.g = None
+        self.written = np.zeros(C, bool)
+        plan.acts.append(self)
+
+    @property
+    def bs(self):
+        return self.H * self.W * self.C
+
+    @property
+    def M(self):
+        return self.plan.B * self.H * self.W
+
+    def grad(self):
+        if self.g is None:
+            self.g = torch.empty(self.t.shape, dtype=GRAD_DTYPE, device=self.t.device)
+        return self.g
+
+
+class View:
+    """Channel slice [c0, c0+c) of an Act."""
+
+    def __init__(self, act: Act, c0: int = 0, c: int | None = None):
+        self.act, self.c0 = act, c0
+        self.c = act.C - c0 if c is None else c
+
+    def sub(self, c0, c):
+        return View(self.act, self.c0 + c0, c)
+
+    @property
+    def H(self):
+        return self.act.H
+
+    @property
+    def W(self):
+        return self.act.W
+
+    @property
+    def bs(self):
+        return self.act.bs
+
+    @property
+    def ld(self):
+        return self.act.C
+
+    @property
+    def M(self):
+        return self.act.M
+
+    def ptr(self):
+        return self.act.t.data_ptr() + self.c0 * self.act.t.element_size()
+
+    def gptr(self):
+        g = self.act.grad()
+        return g.data_ptr() + self.c0 * g.element_size()
+
+    # --- gradient bookkeeping (backward)
+    def grad_for_write(self, st):
+        """Accumulate flag for writing this slice's gradient; zero-fills a partially written slice."""
+        w = self.act.written[self.c0:self.c0 + self.c]
+        if w.all():
+            return 1
+        if w.any():
+            call("ym_view_axpy", None, 0, 0, self.gptr(), self.bs, self.ld, self.M, self.c, self.H * self.W, 0, 0, st)
+            self.act.written[self.c0:self.c0 + self.c] = True
+            return 1
+        return 0
+
+    def mark(self):
+        self.act.written[self.c0:self.c0 + self.c] = True
+
+    def grad_for_read(self, st):
+        """Gradient of this slice, zero-filled where no consumer wrote it."""
+        if not self.act.written[self.c0:self.c0 + self.c].all():
+            acc = self.grad_for_write(st)
+            if not acc:
+                call("ym_view_axpy", None, 0, 0, self.gptr(), self.bs, self.ld, self.M, self.c, self.H * self.W, 0, 0, st)
+            self.mark()
+        return self.gptr()
+
+
+# ----------------------------------------------------------------------------- weights
+class WeightStore:
+    """bf16 copies of every conv weight of a plan in the two kernel layouts."""
+
+    def __init__(self, plan):
+        self.plan = plan
+        self.items = []          # (module_param, fwd tensor, t tensor, cout_t)
+        self.table_dev = None
+        self.key = None
+
+    def add(self, w: torch.nn.Parameter, need_t: bool, cout_t: int | None = None):
+        co, ci, kh, kw = w.shape
+        cout_t = cout_t or co
+        fwd = torch.empty(co, kh, kw, ci, dtype=F16, device=self.plan.dev)
+        t = torch.zeros(ci, kh, kw, cout_t, dtype=BF16, device=self.plan.dev) if need_t else None
+        self.items.append((w, fwd, t, cout_t))
+        return fwd, t
+
+    def refresh(self, st):
+        """One launch converting every fp32 OIHW master weight (after each optimizer step)."""
+        if not self.items:
+            return
+        key = tuple(w.data_ptr() for w, *_ in self.items)
+        if key != self.key:
+            arr = (WPrepEntry * len(self.items))()
+            off = 0
+            for e, (w, fwd, t, cout_t) in zip(arr, self.items):
+                co, ci, kh, kw = w.shape
+                e.src, e.dst_fwd, e.dst_t = w.data_ptr(), fwd.data_ptr(), (t.data_ptr() if t is not None else None)
+                e.elem_offset, e.cout, e.cin, e.kh, e.kw, e.cout_t = off, co, ci, kh, kw, cout_t
+                off += w.numel()
+            raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self.table_dev = raw.to(self.plan.dev)
+            self.total = off
+            self.key = key
+        call("ym_prep_weights", self.table_dev.data_ptr(), len(self.items), self.total, st)
+
+
+# ----------------------------------------------------------------------------- ops
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class ConvBN:
+    """Conv2d (k in {1,3}, groups=1) -> BatchNorm2d -> SiLU|Identity (+ residual) — reference Conv :21-33."""
+
+    def __init__(self, plan, m, x: View, y: View, s=1, act=True, res: View | None = None):
+        w = m.conv.weight
+        self.m, self.x, self.y, self.res, self.act = m, x, y, res, int(act)
+        co, ci, k, _ = w.shape
+        assert ci == x.c and co == y.c, (m, ci, x.c, co, y.c)
+        self.k, self.s, self.co, self.ci = k, s, co, ci
+        oh, ow = (x.H + 2 * (k // 2) - k) // s + 1, (x.W + 2 * (k // 2) - k) // s + 1
+        assert (oh, ow) == (y.H, y.W), ((oh, ow), (y.H, y.W))
+        B = plan.B
+        self.M, self.HW = B * oh * ow, oh * ow
+        self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
+        self.wf, self.wt = plan.weights.add(w, need_t=x.act is not None)
+        self.G = lib().ym_conv_stat_blocks(self.M, co)
+        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
+        self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)      # scale, shift, mean, rstd
+        self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
+        d = ConvDesc()
+        d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout = B, x.H, x.W, ci, oh, ow, co
+        d.k, d.stride, d.pad = k, s, k // 2
+        d.x_bs, d.x_ld, d.y_bs, d.y_ld = x.bs, x.ld, self.HW * co, co
+        d.out_f32 = 2                                                   # fp16 pre-BN z
+        self.desc = d
+        self.wscratch = plan.wgrad_scratch(co * ci * k * k) if k > 1 else None
+
+    def flops(self):
+        return 2 * self.M * self.co * self.ci * self.k * self.k
+
+    def forward(self, plan, st):
+        bn = self.m.bn
+        ss, sq = self.ps[0], self.ps[1]
+        probe = plan.probe is self
+        if probe:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        call("ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
+             ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st)
+        if probe:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            plan.probe_events.append((ev0, ev1))
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        if plan.training:
+            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
+                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+        else:
+            call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
+                 float(bn.eps), sc, sh, st)
+        r = self.res
+        call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, self.act,
+             r.ptr() if r else None, r.bs if r else 0, r.ld if r else 0, self.y.ptr(), self.y.bs, self.y.ld,
+             _p(getattr(self, "out32", None)), st)
+
+    def backward(self, plan, st):
+        bn = self.m.bn
+        dy = self.y.grad_for_read(st)
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
+        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
+             self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+        dz = self.z  # reuse the z buffer? no: z is needed by nobody after this op -> in-place dz
+        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
+             self.act, self.coef.data_ptr(), dz.data_ptr(), st)
+        if self.res is not None:
+            acc = self.res.grad_for_write(st)
+            call("ym_view_axpy", dy, self.y.bs, self.y.ld, self.res.gptr(), self.res.bs, self.res.ld, self.M, self.co,
+                 self.HW, acc, 0, st)
+            self.res.mark()
+        # weight gradient
+        w = self.m.conv.weight
+        if self.k == 1:
+            call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), plan.gptr(w), st)
+        else:
+            call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), self.wscratch.data_ptr(), st)
+            call("ym_wgrad_to_oihw", self.wscratch.data_ptr(), plan.gptr(w), self.co, self.ci, self.k * self.k, 0, st)
+        # data gradient
+        if plan.needs_grad(self.x):
+            acc = self.x.grad_for_write(st)
+            self.desc.accumulate = acc
+            call("ym_conv_dgrad", ctypes.byref(self.desc), dz.data_ptr(), self.wt.data_ptr(), self.x.gptr(), st)
+            self.desc.accumulate = 0
+            self.x.mark()
+
+
+class StemConvBN(ConvBN):
+    """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
+
+    def __init__(self, plan, m, img_shape, y: View, s):
+        w = m.conv.weight
+        self.m, self.y, self.res, self.act, self.x = m, y, None, 1, None
+        co, ci, k, _ = w.shape
+        assert ci == 1 and k == 3
+        B, H, W = img_shape
+        self.H, self.W, self.k, self.s, self.co, self.ci = H, W, k, s, co, ci
+        oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+        assert (oh, ow) == (y.H, y.W)
+        self.M, self.HW, self.oh, self.ow = B * oh * ow, oh * ow, oh, ow
+        self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
+        self.G = 1024
+        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
+        self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)
+        self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
+
+    def forward(self, plan, st):
+        bn = self.m.bn
+        ss, sq = self.ps[0], self.ps[1]
+        B = plan.B
+        call("ym_conv_first_fwd", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(), ss.data_ptr(),
+             sq.data_ptr(), B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        if plan.training:
+            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
+                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+        else:
+            call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
+                 float(bn.eps), sc, sh, st)
+        call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, 1, None, 0, 0, self.y.ptr(),
+             self.y.bs, self.y.ld, None, st)
+
+    def backward(self, plan, st):
+        bn = self.m.bn
+        dy = self.y.grad_for_read(st)
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
+        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
+             1, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
+             1, self.coef.data_ptr(), self.z.data_ptr(), st)
+        call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight), plan.B,
+             self.H, self.W, self.oh, self.ow, self.co, self.s, 1, st)
+
+
+class DWConvBN(ConvBN):
+    """Attention.pe: depthwise 3x3 + BN (no act) on v, + the attention output as residual (:122, :134)."""
+
+    def __init__(self, plan, m, qkv: View, heads, kd, hd, y: View, res: View):
+        self.m, self.x, self.y, self.res, self.act = m, qkv, y, res, 0
+        C = heads * hd
+        self.C, self.map = C, (hd, 2 * kd + hd, 2 * kd)     # gsz, gstride, goff
+        self.k, self.co = 3, C
+        self.M, self.HW = y.M, y.H * y.W
+        self.z = torch.empty(self.M, C, dtype=BF16, device=plan.dev)
+        self.G = 256
+        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, C)), C, dtype=F32, device=plan.dev)
+        self.bnv = torch.empty(4, C, dtype=F32, device=plan.dev)
+        self.coef = torch.empty(3, C, dtype=F32, device=plan.dev)
+
+    def forward(self, plan, st):
+        bn = self.m.bn
+        ss, sq = self.ps[0], self.ps[1]
+        gsz, gstr, goff = self.map
+        call("ym_dw3x3_fwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
+             self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G, st)
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        if plan.training:
+            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.C, float(self.M), _p(bn.weight),
+                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+        else:
+            call("ym_bn_eval_coeff", self.C, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
+                 float(bn.eps), sc, sh, st)
+        r = self.res
+        call("ym_bn_apply", self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, 0, r.ptr(), r.bs, r.ld, self.y.ptr(),
+             self.y.bs, self.y.ld, None, st)
+
+    def backward(self, plan, st):
+        bn = self.m.bn
+        dy = self.y.grad_for_read(st)
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        Gb = lib().ym_bn_bwd_blocks(self.M, self.C)
+        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
+             0, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.C, float(self.M),
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
+             0, self.coef.data_ptr(), self.z.data_ptr(), st)
+        acc = self.res.grad_for_write(st)
+        call("ym_view_axpy", dy, self.y.bs, self.y.ld, self.res.gptr(), self.res.bs, self.res.ld, self.M, self.C,
+             self.HW, acc, 0, st)
+        self.res.mark()
+        # dx into the v channels of dqkv (accumulate if the attention core wrote them already)
+        hd, hs, goff = self.map
+        heads = self.C // hd
+        vch = np.zeros(self.x.act.C, bool)
+        for h in range(heads):
+            vch[self.x.c0 + h * hs + goff: self.x.c0 + h * hs + goff + hd] = True
+        acc = int(self.x.act.written[vch].all())
+        gsz, gstr, goff = self.map
+        call("ym_dw3x3_bwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
+             self.z.data_ptr(), self.x.gptr(), self.x.bs, self.x.ld, plan.gptr(self.m.conv.weight), plan.B, self.y.H,
+             self.y.W, self.C, acc, st)
+        self.x.act.written[vch] = True
+
+
+class AttnCore:
+    """softmax(q^T k * kd^-0.5) and v @ attn^T per head (Attention.forward :124-134)."""
+
+    def __init__(self, plan, qkv: View, heads, kd, hd, out: View):
+        self.qkv, self.out, self.heads, self.kd, self.hd = qkv, out, heads, kd, hd
+        self.N = qkv.H * qkv.W
+        self.scale = kd ** -0.5
+        self.lse = torch.empty(plan.B, heads, self.N, dtype=F32, device=plan.dev)
+        ws = lib().ym_attn_workspace_size(plan.B, heads, self.N)
+        self.ws = torch.empty(max(ws // 4, 1), dtype=F32, device=plan.dev)
+
+    def forward(self, plan, st):
+        call("ym_attn_fwd", self.qkv.ptr(), self.qkv.bs, self.qkv.ld, plan.B, self.heads, self.N, self.kd, self.hd,
+             self.scale, self.out.ptr(), self.out.bs, self.out.ld, self.lse.data_ptr(), st)
+
+    def backward(self, plan, st):
+        dout = self.out.grad_for_read(st)
+        q = self.qkv
+        hs = 2 * self.kd + self.hd
+        wr = q.act.written
+        idx = lambda off, n: np.concatenate([np.arange(q.c0 + h * hs + off, q.c0 + h * hs + off + n)
+                                             for h in range(self.heads)])
+        iq, ik, iv = idx(0, self.kd), idx(self.kd, self.kd), idx(2 * self.kd, self.hd)
+        acc = [int(wr[i].all()) for i in (iq, ik, iv)]
+        call("ym_attn_bwd", q.ptr(), q.bs, q.ld, self.out.ptr(), self.out.bs, self.out.ld, dout, self.out.bs,
+             self.out.ld, self.lse.data_ptr(), plan.B, self.heads, self.N, self.scale, self.ws.data_ptr(), q.gptr(),
+             q.bs, q.ld, acc[0], acc[1], acc[2], st)
+        for i in (iq, ik, iv):
+            wr[i] = True
+
+
+class SPPFPools:
+    """SPPF's three chained nn.MaxPool2d(5, 1, 2) (yolo11_modules.py:100-104) on fp32 values.
+
+    The chain is evaluated on the fp32 cv1 output (recomputed by its BN-apply) so the
+    first-maximum routing of the backward sees the same ties as the fp32 reference
+    (chained pools copy values, so exact ties are structural); the bf16 copies go to
+    the concat slices for cv2."""
+
+    def __init__(self, plan, cv1_op, slices):
+        self.slices = slices                      # [s0 (cv1 out), s1, s2, s3]
+        x = slices[0]
+        self.M, self.C, self.H, self.W = x.M, x.c, x.H, x.W
+        self.P = torch.empty(4, self.M, self.C, dtype=F32, device=plan.dev)   # fp32 chain values
+        self.G = torch.empty(2, self.M, self.C, dtype=F32, device=plan.dev)   # grad ping-pong
+        cv1_op.out32 = self.P[0]
+
+    def forward(self, plan, st):
+        for j in range(3):
+            y = self.slices[j + 1]
+            call("ym_maxpool5_f32_fwd", self.P[j].data_ptr(), self.P[j + 1].data_ptr(), y.ptr(), y.bs, y.ld, plan.B,
+                 self.H, self.W, self.C, st)
+
+    def backward(self, plan, st):
+        HW = self.H * self.W
+        cur = self.G[0]
+        s3 = self.slices[3]
+        call("ym_view_to_f32", s3.grad_for_read(st), s3.bs, s3.ld, cur.data_ptr(), self.M, self.C, HW, st)
+        for j in (2, 1, 0):
+            nxt = self.G[(3 - j) % 2]
+            sj = self.slices[j]
+            if j > 0:
+                call("ym_view_to_f32", sj.grad_for_read(st), sj.bs, sj.ld, nxt.data_ptr(), self.M, self.C, HW, st)
+            else:
+                nxt.zero_()
+            call("ym_maxpool5_f32_bwd", self.P[j].data_ptr(), cur.data_ptr(), nxt.data_ptr(), plan.B, self.H, self.W,
+                 self.C, st)
+            cur = nxt
+        s0 = self.slices[0]
+        acc = s0.grad_for_write(st)
+        call("ym_f32_to_view", cur.data_ptr(), s0.gptr(), s0.bs, s0.ld, self.M, self.C, HW, acc, st)
+        s0.mark()
+
+
+class Upsample2:
+    """nn.Upsample(scale_factor=2, mode='nearest') (yaml head rows 11, 14)."""
+
+    def __init__(self, plan, x: View, y: View):
+        self.x, self.y = x, y
+
+    def forward(self, plan, st):
+        x, y = self.x, self.y
+        call("ym_upsample2_fwd", x.ptr(), x.bs, x.ld, y.ptr(), y.bs, y.ld, plan.B, x.H, x.W, x.c, st)
+
+    def backward(self, plan, st):
+        x, y = self.x, self.y
+        dy = y.grad_for_read(st)
+        acc = x.grad_for_write(st)
+        call("ym_upsample2_bwd", dy, y.bs, y.ld, x.gptr(), x.bs, x.ld, plan.B, x.H, x.W, x.c, acc, st)
+        x.mark()
+
+
+class Copy:
+    """Channel-slice copy for the two concatenations whose halves live in different buffers (PSA / C2PSA)."""
+
+    def __init__(self, plan, x: View, y: View):
+        self.x, self.y = x, y
+
+    def forward(self, plan, st):
+        x, y = self.x, self.y
+        call("ym_view_axpy", x.ptr(), x.bs, x.ld, y.ptr(), y.bs, y.ld, x.M, x.c, x.H * x.W, 0, 1, st)
+
+    def backward(self, plan, st):
+        x, y = self.x, self.y
+        dy = y.grad_for_read(st)
+        acc = x.grad_for_write(st)
+        call("ym_view_axpy", dy, y.bs, y.ld, x.gptr(), x.bs, x.ld, x.M, x.c, x.H * x.W, acc, 0, st)
+        x.mark()
+
+
+class HeadLevel:
+    """Detect level i: the two bias 1x1 convs (cv2[i][2] -> 64 box logits, cv3[i][2] -> nc cls logits)
+    writing fp32 rows of the (B, A, 64+nc) head buffer (Detect.forward :237-246)."""
+
+    def __init__(self, plan, box_conv, cls_conv, xb: View, xc: View, head, a_off):
+        self.box, self.cls, self.xb, self.xc, self.head, self.a_off = box_conv, cls_conv, xb, xc, head, a_off
+        B, A, no = head.shape
+        self.nc = no - 64
+        self.HW, self.M = xb.H * xb.W, B * xb.H * xb.W
+        self.wb_f, self.wb_t = plan.weights.add(box_conv.weight, need_t=True)
+        self.wc_f, self.wc_t = plan.weights.add(cls_conv.weight, need_t=True, cout_t=8)
+        self.dzb = torch.empty(self.M, 64, dtype=BF16, device=plan.dev)
+        self.dzc = torch.empty(self.M, 8, dtype=BF16, device=plan.dev)
+        self.wsc = torch.empty(8, xc.c, dtype=F32, device=plan.dev)
+
+        def desc(x, cout, y_bs, y_ld, out_f32):
+            d = ConvDesc()
+            d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout = B, x.H, x.W, x.c, x.H, x.W, cout
+            d.k, d.stride, d.pad = 1, 1, 0
+            d.x_bs, d.x_ld, d.y_bs, d.y_ld, d.out_f32 = x.bs, x.ld, y_bs, y_ld, out_f32
+            return d
+        self.fb = desc(xb, 64, A * no, no, 1)
+        self.fc = desc(xc, self.nc, A * no, no, 1)
+        self.bb = desc(xb, 64, self.HW * 64, 64, 0)
+        self.bc = desc(xc, 8, self.HW * 8, 8, 0)
+
+    def forward(self, plan, st):
+        base = self.head.data_ptr() + self.a_off * self.head.shape[2] * 4
+        call("ym_conv_fwd", ctypes.byref(self.fb), self.xb.ptr(), self.wb_f.data_ptr(), base, _p(self.box.bias), None,
+             None, st)
+        call("ym_conv_fwd", ctypes.byref(self.fc), self.xc.ptr(), self.wc_f.data_ptr(), base + 64 * 4,
+             _p(self.cls.bias), None, None, st)
+
+    def backward(self, plan, st):
+        B, A, no = self.head.shape
+        call("ym_head_grad", plan.dhead.data_ptr(), A, self.a_off, self.HW, self.M, self.nc, self.dzb.data_ptr(),
+             self.dzc.data_ptr(), plan.gptr(self.box.bias), plan.gptr(self.cls.bias), st)
+        call("ym_conv_wgrad", ctypes.byref(self.bb), self.dzb.data_ptr(), self.xb.ptr(), plan.gptr(self.box.weight), st)
+        self.wsc.zero_()
+        call("ym_conv_wgrad", ctypes.byref(self.bc), self.dzc.data_ptr(), self.xc.ptr(), self.wsc.data_ptr(), st)
+        g = plan.grad_view(self.cls.weight).view(self.nc, -1)
+        g.copy_(self.wsc[: self.nc])
+        for d, dz, wt, x in ((self.bb, self.dzb, self.wb_t, self.xb), (self.bc, self.dzc, self.wc_t, self.xc)):
+            acc = x.grad_for_write(st)
+            d.accumulate = acc
+            call("ym_conv_dgrad", ctypes.byref(d), dz.data_ptr(), wt.data_ptr(), x.gptr(), st)
+            d.accumulate = 0
+            x.mark()
+
+
+# ----------------------------------------------------------------------------- plan
+class Plan:
+    def __init__(self, root, B, H, W, dev, training):
+        self.root, self.B, self.dev, self.training = root, B, dev, training
+        self.acts, self.ops = [], []
+        self.weights = WeightStore(self)
+        self.probe, self.probe_events = None, []   # bench: time one op's conv launch
+        self.input = None          # View for block plans
+        self.img = None            # fp32 image for the full model
+        self.head = None           # (B, A, 64+nc) fp32 for the full model
+        self.dhead = None
+        self._scratch = []
+        # flat parameter-gradient buffer; each .grad is a view of it
+        params = [p for p in root.parameters() if p.requires_grad]
+        self.params = params
+        sizes = [p.numel() for p in params]
+        self.grad_flat = torch.zeros(max(sum(sizes), 1), dtype=F32, device=dev)
+        self.grad_views, off = {}, 0
+        for p, n in zip(params, sizes):
+            self.grad_views[id(p)] = self.grad_flat[off:off + n].view(p.shape)
+            off += n
+
+    def act(self, C, H, W, name=""):
+        return View(Act(self, C, H, W, name=name))
+
+    def wgrad_scratch(self, n):
+        t = torch.empty(n, dtype=F32, device=self.dev)
+        self._scratch.append(t)
+        return t
+
+    def grad_view(self, p):
+        return self.grad_views[id(p)]
+
+    def gptr(self, p):
+        if p is None or not p.requires_grad:
+            return None
+        return self.grad_views[id(p)].data_ptr()
+
+    def needs_grad(self, v: View):
+        return v.act is not None and (v.act is not getattr(self.input, "act", None) or self.input_requires_grad)
+
+    # --------------------------------------------------------------- run
+    def forward(self):
+        st = stream_ptr(self.dev)
+        self.weights.refresh(st)
+        for op in self.ops:
+            op.forward(self, st)
+
+    def backward(self):
+        st = stream_ptr(self.dev)
+        for a in self.acts:
+            a.written[:] = False
+        self.grad_flat.zero_()
+        for t in self._scratch:
+            t.zero_()
+        for op in reversed(self.ops):
+            op.backward(self, st)
+
+    def install_grads(self):
+        """Expose the flat buffer as parameter .grad (accumulating if a grad already exists)."""
+        for p in self.params:
+            g = self.grad_views[id(p)]
+            if p.grad is None:
+                p.grad = g
+            elif p.grad.data_ptr() != g.data_ptr():
+                p.grad.add_(g)
+
+
+# ----------------------------------------------------------------------------- lowering
+def _conv(plan, m, x: View, out: View | None = None, res=None, act=None):
+    k, s = m.conv.kernel_size[0], m.conv.stride[0]
+    co = m.conv.out_channels
+    H, W = (x.H + 2 * (k // 2) - k) // s + 1, (x.W + 2 * (k // 2) - k) // s + 1
+    y = out if out is not None else plan.act(co, H, W)
+    if act is None:
+        act = not isinstance(m.act, torch.nn.Identity)
+    plan.ops.append(ConvBN(plan, m, x, y, s, act, res))
+    return y
+
+
+def _bottleneck(plan, m, x: View, out=None):
+    t = _conv(plan, m.cv1, x)
+    return _conv(plan, m.cv2, t, out, res=x if m.add else None)
+
+
+def _c3k(plan, m, x: View, out=None):
+    c_ = m.cv1.conv.out_channels
+    cat = plan.act(2 * c_, x.H, x.W)
+    a = _conv(plan, m.cv1, x)
+    blocks = list(m.m)
+    for j, b in enumerate(blocks):
+        a = _bottleneck(plan, b, a, cat.sub(0, c_) if j == len(blocks) - 1 else None)
+    _conv(plan, m.cv2, x, cat.sub(c_, c_))
+    return _conv(plan, m.cv3, cat, out)
+
+
+def _c2f(plan, m, x: View, out=None):
+    c, n = m.c, len(m.m)
+    cat = plan.act((2 + n) * c, x.H, x.W)
+    _conv(plan, m.cv1, x, cat.sub(0, 2 * c))
+    prev = cat.sub(c, c)
+    for j, b in enumerate(m.m):
+        dst = cat.sub((2 + j) * c, c)
+        if type(b).__name__ == "C3k":
+            prev = _c3k(plan, b, prev, dst)
+        else:
+            prev = _bottleneck(plan, b, prev, dst)
+    return _conv(plan, m.cv2, cat, out)
+
+
+def _sppf(plan, m, x: View, out=None):
+    c_ = m.cv1.conv.out_channels
+    cat = plan.act(4 * c_, x.H, x.W)
+    _conv(plan, m.cv1, x, cat.sub(0, c_))
+    plan.ops.append(SPPFPools(plan, plan.ops[-1], [cat.sub(j * c_, c_) for j in range(4)]))
+    return _conv(plan, m.cv2, cat, out)
+
+
+def _attention(plan, m, x: View, out: View, res: View):
+    heads, kd, hd = m.num_heads, m.key_dim, m.head_dim
+    qkv = _conv(plan, m.qkv, x, act=False)
+    o = plan.act(heads * hd, x.H, x.W)
+    plan.ops.append(AttnCore(plan, qkv, heads, kd, hd, o))
+    s = plan.act(heads * hd, x.H, x.W)
+    plan.ops.append(DWConvBN(plan, m.pe, qkv, heads, kd, hd, s, o))
+    return _conv(plan, m.proj, s, out, res=res, act=False)
+
+
+def _psa(plan, m, x: View, out=None):
+    c = m.c
+    y = _conv(plan, m.cv1, x)                      # [a | b]
+    a, b = y.sub(0, c), y.sub(c, c)
+    cat = plan.act(2 * c, x.H, x.W)
+    b2 = plan.act(c, x.H, x.W)
+    _attention(plan, m.attn, b, b2, res=b)         # b2 = b + attn(b)
+    f1 = _conv(plan, m.ffn[0], b2)
+    _conv(plan, m.ffn[1], f1, cat.sub(c, c), res=b2, act=False)   # b3 = b2 + ffn(b2)
+    plan.ops.append(Copy(plan, a, cat.sub(0, c)))
+    return _conv(plan, m.cv2, cat, out)
+
+
+def _c2psa(plan, m, x: View, out=None):
+    c = m.c
+    y = _conv(plan, m.cv1, x)
+    a, b = y.sub(0, c), y.sub(c, c)
+    cat = plan.act(2 * c, x.H, x.W)
+    blocks = list(m.m)
+    for j, blk in enumerate(blocks):
+        b = _psa(plan, blk, b, cat.sub(c, c) if j == len(blocks) - 1 else None)
+    plan.ops.append(Copy(plan, a, cat.sub(0, c)))
+    return _conv(plan, m.cv2, cat, out)
+
+
+def _detect(plan, m, xs, head):
+    a_off = 0
+    for i, x in enumerate(xs):
+        b = _conv(plan, m.cv2[i][1], _conv(plan, m.cv2[i][0], x))
+        c = _conv(plan, m.cv3[i][1], _conv(plan, m.cv3[i][0], x))
+        plan.ops.append(HeadLevel(plan, m.cv2[i][2], m.cv3[i][2], b, c, head, a_off))
+        a_off += x.H * x.W
+
+
+LOWER = {"Conv": _conv, "Bottleneck": _bottleneck, "C3k": _c3k, "C2f": _c2f, "C3k2": _c2f, "SPPF": _sppf,
+         "C2PSA": _c2psa, "PSA": _psa}
+
+
+def lower_block(plan, m, x: View):
+    t = type(m).__name__
+    if t not in LOWER:
+        raise YolomiError(f"no MI355X lowering for module type {t}")
+    return LOWER[t](plan, m, x)
+
+
+def lower_model(plan, model, img_shape):
+    """YOLOv11._forward_once (yolo11_model.py:60-71) over the layer list with concat-slice planning."""
+    layers = list(model.model)
+    B, H, W = img_shape
+    # output channels / spatial size of every layer
+    shapes = []
+    for i, L in enumerate(layers):
+        t = type(L).__name__
+        f = L.f
+        src = (i - 1 if f == -1 else f) if isinstance(f, int) else None
+        inp = (1, H, W) if (isinstance(f, int) and src < 0) else (shapes[src] if src is not None else None)
+        if t == "Conv":
+            k, s = L.conv.kernel_size[0], L.conv.stride[0]
+            shapes.append((L.conv.out_channels, (inp[1] + 2 * (k // 2) - k) // s + 1,
+                           (inp[2] + 2 * (k // 2) - k) // s + 1))
+        elif t in ("C3k2", "C2f", "SPPF", "C2PSA"):
+            shapes.append((L.cv2.conv.out_channels, inp[1], inp[2]))
+        elif t == "Upsample":
+            shapes.append((inp[0], inp[1] * 2, inp[2] * 2))
+        elif t == "Concat":
+            srcs = [shapes[i - 1 if j == -1 else j] for j in f]
+            assert all(s_[1:] == srcs[0][1:] for s_ in srcs), f"concat {i}: spatial mismatch {srcs}"
+            shapes.append((sum(s_[0] for s_ in srcs), srcs[0][1], srcs[0][2]))
+        elif t == "Detect":
+            shapes.append(None)
+        else:
+            raise YolomiError(f"no MI355X lowering for layer type {t}")
+    # concat buffers: producers write into their slice
+    dest = {}
+    for i, L in enumerate(layers):
+        if type(L).__name__ == "Concat":
+            C, hh, ww = shapes[i]
+            buf = plan.act(C, hh, ww, name=f"cat{i}")
+            c0 = 0
+            for j in L.f:
+                src = i - 1 if j == -1 else j
+                cj = shapes[src][0]
+                assert src not in dest, "a layer feeding two concats is not supported"
+                dest[src] = buf.sub(c0, cj)
+                c0 += cj
+            dest[i] = buf
+    outs = []
+    x = None
+    for i, L in enumerate(layers):
+        t = type(L).__name__
+        f = L.f
+        if f != -1:
+            xin = outs[f] if isinstance(f, int) else [x if j == -1 else outs[j] for j in f]
+        else:
+            xin = x
+        if t == "Conv":
+            if i == 0:
+                y = dest.get(i) or plan.act(*shapes[i])
+                plan.ops.append(StemConvBN(plan, L, img_shape, y, L.conv.stride[0]))
+                x = y
+            else:
+                x = _conv(plan, L, xin, dest.get(i))
+        elif t in ("C3k2", "C2f"):
+            x = _c2f(plan, L, xin, dest.get(i))
+        elif t == "SPPF":
+            x = _sppf(plan, L, xin, dest.get(i))
+        elif t == "C2PSA":
+            x = _c2psa(plan, L, xin, dest.get(i))
+        elif t == "Upsample":
+            y = dest.get(i) or plan.act(*shapes[i])
+            plan.ops.append(Upsample2(plan, xin, y))
+            x = y
+        elif t == "Concat":
+            x = dest[i]
+        elif t == "Detect":
+            nc = L.nc
+            A = sum(v.H * v.W for v in xin)
+            plan.head = torch.empty(B, A, 64 + nc, dtype=F32, device=plan.dev)
+            plan.dhead = torch.empty_like(plan.head)
+            _detect(plan, L, xin, plan.head)
+            plan.level_hw = [(v.H, v.W) for v in xin]
+            x = None
+        outs.append(x)
+    plan.layer_outs = outs
+    return plan
+
+
+# ----------------------------------------------------------------------------- autograd glue
+class _ModelFn(torch.autograd.Function):
+    """Whole-model forward/backward as one node; parameter grads are written into the plan's flat buffer."""
+
+    @staticmethod
+    def forward(ctx, img, anchor, plan):
+        plan.img = img.contiguous()
+        plan.forward()
+        ctx.plan = plan
+        return plan.head.detach()
+
+    @staticmethod
+    def backward(ctx, dhead):
+        plan = ctx.plan
+        plan.dhead = dhead.contiguous()
+        plan.backward()
+        plan.install_grads()
+        return None, None, None
+
+
+class _BlockFn(torch.autograd.Function):
+    """A single building block on NCHW fp32 tensors (per-block parity / module-level API)."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, plan):
+        if plan.stem:
+            plan.img = x.float().contiguous()
+        else:
+            plan.input.act.t.copy_(x.permute(0, 2, 3, 1))
+        plan.forward()
+        ctx.plan = plan
+        out = plan.output.act.t[..., plan.output.c0:plan.output.c0 + plan.output.c]
+        return out.permute(0, 3, 1, 2).float().contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        plan = ctx.plan
+        o = plan.output
+        g = o.act.grad()
+        g[..., o.c0:o.c0 + o.c].copy_(dy.permute(0, 2, 3, 1))
+        plan.backward_from_output()
+        plan.install_grads()
+        dx = plan.input.act.grad().permute(0, 3, 1, 2).float() if plan.input_requires_grad else None
+        return dx, None, None
+
+
+def run_block(module, x: torch.Tensor):
+    """Execute one building block on the GPU through the plan (training or eval per module.training)."""
+    if not x.is_cuda:
+        raise YolomiError("yolomi kernels run on the MI355X only (got a CPU tensor)")
+    B, C, H, W = x.shape
+    key = ("block", B, H, W, module.training, x.requires_grad)
+    cache = module.__dict__.setdefault("_ym_plans", {})
+    plan = cache.get(key)
+    if plan is None:
+        plan = Plan(module, B, H, W, x.device, module.training)
+        if type(module).__name__ == "Conv" and module.conv.in_channels == 1:
+            # stem conv reads the fp32 image directly (no input gradient)
+            plan.stem = True
+            plan.input = None
+            plan.input_requires_grad = False
+            k, s = module.conv.kernel_size[0], module.conv.stride[0]
+            plan.output = plan.act(module.conv.out_channels, (H + 2 * (k // 2) - k) // s + 1,
+                                   (W + 2 * (k // 2) - k) // s + 1)
+            plan.ops.append(StemConvBN(plan, module, (B, H, W), plan.output, s))
+        else:
+            plan.stem = False
+            plan.input = plan.act(C, H, W, name="input")
+            plan.input_requires_grad = x.requires_grad
+            plan.output = lower_block(plan, module, plan.input)
+
+        def backward_from_output():
+            st = stream_ptr(plan.dev)
+            for a in plan.acts:
+                a.written[:] = False
+            plan.output.mark()
+            plan.grad_flat.zero_()
+            for t in plan._scratch:
+                t.zero_()
+            for op in reversed(plan.ops):
+                op.backward(plan, st)
+        plan.backward_from_output = backward_from_output
+        cache[key] = plan
+    anchor = module.__dict__.setdefault("_ym_anchor", torch.zeros(1, requires_grad=True))
+    return _BlockFn.apply(x, anchor, plan)
+
+
+def run_model(model, img: torch.Tensor):
+    """Training-mode / eval-mode forward of the whole YOLOv11; returns the (B, A, 64+nc) fp32 head buffer."""
+    if not img.is_cuda:
+        raise YolomiError("yolomi kernels run on the MI355X only (got a CPU tensor)")
+    B, C, H, W = img.shape
+    if C != 1:
+        raise YolomiError(f"stem kernel supports ch=1 input (got {C})")
+    key = ("model", B, H, W, model.training)
+    cache = model.__dict__.setdefault("_ym_plans", {})
+    plan = cache.get(key)
+    if plan is None:
+        plan = Plan(model, B, H, W, img.device, model.training)
+        plan.input_requires_grad = False
+        lower_model(plan, model, (B, H, W))
+        cache[key] = plan
+    if model.training:
+        model.__dict__["_ym_last_plan"] = plan
+    anchor = model.__dict__.setdefault("_ym_anchor", torch.zeros(1, device=img.device, requires_grad=True))
+    img32 = img.float()
+    if torch.is_grad_enabled() and model.training:
+        head = _ModelFn.apply(img32, anchor, plan)
+    else:
+        plan.img = img32.contiguous()
+        plan.forward()
+        head = plan.head
+    return head, plan
