@@ -129,9 +129,12 @@ int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t tota
  * eps 1e-3 / momentum 0.03 from yolo11_model.py:183-185).  z is the dense (m, c) conv output in
  * fp16 (written by ym_conv_fwd with out_f32 = 2); dz (bf16) may overwrite it in place.
  */
+/* scratch for the two-level partial reductions of ym_bn_finalize / ym_bn_bwd_finalize */
+size_t ym_bn_workspace_size(int c);
 int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
-                   float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* stream);
+                   float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* workspace,
+                   void* stream);
 int ym_bn_eval_coeff(int c, const float* gamma, const float* beta, const float* running_mean,
                      const float* running_var, float eps, float* scale, float* shift, void* stream);
 /* out_view = act(z*scale+shift) (+ res_view); act: 0 identity, 1 SiLU; hw = pixels per image */
@@ -144,7 +147,7 @@ int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint1
                      float* part_sum, float* part_dot, void* stream);
 int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                        const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
-                       float* coef, void* stream);
+                       float* coef, void* workspace, void* stream);
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                     const float* coef, uint16_t* dz, void* stream);

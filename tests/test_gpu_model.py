@@ -200,3 +200,39 @@ def test_sppf_pool_chain_exact():
         call("ym_maxpool5_f32_bwd", P[j].data_ptr(), cur.data_ptr(), nxt.data_ptr(), B, H, W, C, st)
         cur = nxt
     torch.testing.assert_close(cur.cpu().view(B, H, W, C), xr.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
+
+
+def test_network_backward_fixed_head_grads_vs_oracle():
+    """Network backward: the same random head gradients through our plan and through CPU fp32
+    autograd of the oracle.  Gradients are bf16 and the error grows smoothly with backward depth
+    (measured: 2.7% at the first Detect convs, <= 9% at the stem, no block-level jump — every block
+    also passes its own 2e-2 check), so the per-parameter bound here is relative-L2 <= 1.2e-1;
+    near-zero true gradients are compared on the network's gradient scale."""
+    from oracle import model as om
+    from models import build_yolo11
+    cfg = om.load_cfg("n")
+    layers, save, P = om.build(cfg)
+    m = build_yolo11(cfg, ch=1, nc=5)
+    m.load_state_dict(P)
+    m = m.cuda().train()
+    g = torch.Generator().manual_seed(3)
+    img = torch.rand(2, 1, 256, 256, generator=g)
+    heads = m(img.cuda())
+    dh = [torch.randn(h.shape, generator=g) * 0.01 for h in heads]
+    torch.autograd.backward(heads, [t.cuda() for t in dh])
+    Q = {k: v.clone() for k, v in P.items()}
+    leaf = {k: v.requires_grad_(True) for k, v in Q.items()
+            if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")}
+    ref = om.forward(Q, layers, save, img, training=True)
+    torch.autograd.backward(ref, dh)
+    gmax = max(float(v.grad.norm()) for v in leaf.values())
+    worst = []
+    for k, p in m.named_parameters():
+        if not p.requires_grad:
+            continue
+        r = leaf[k].grad
+        err = float((p.grad.cpu().double() - r.double()).norm())
+        bound = 1.2e-1 * max(float(r.norm()), 1e-4 * gmax)
+        worst.append((err / max(float(r.norm()), 1e-4 * gmax), k))
+        assert err < bound, (k, err, float(r.norm()))
+    print("worst rel", sorted(worst)[-3:])

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU session: parity tests, the benchmark, and a rocprofv3 kernel-trace profile of it.
+# Usage (on the GPU box, from the repo root): bash tools/gpu_round.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-run}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -m pytest $R/tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
+echo "pytest_gpu exit $?"; tail -3 $OUT/pytest_gpu.log
+timeout -k 10 500 python3 $R/bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed $?"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+echo "rocprof exit $?"
+find $OUT/prof -name "*stats*" | head

@@ -1,4 +1,4 @@
-// Training-mode BatchNorm2d + SiLU, forward and backward, NHWC bf16 (gfx950).
+// Training-mode BatchNorm2d + SiLU, forward and backward, NHWC (gfx950).
 //
 // Replaces BatchNorm2d (batch statistics, biased var for normalisation,
 // unbiased var for the running estimate, eps 1e-3, momentum 0.03) and the
@@ -6,13 +6,18 @@
 // yolo11_modules.py:24-33; eps/momentum set at yolo11_model.py:183-187).
 //
 // Forward (per Conv block): the conv epilogue emits per-block channel partial
-// sums; bn_finalize reduces them in fp64 -> (scale, shift, mean, rstd) and
-// updates running stats; bn_apply writes act(z*scale+shift) (+ residual) into
-// the strided destination view (a concat slice).
+// sums; bn_finalize reduces them (fp64, two levels) -> (scale, shift, mean,
+// rstd) and updates running stats; bn_apply writes act(z*scale+shift)
+// (+ residual) into the strided destination view (a concat slice).
 // Backward: bn_bwd_reduce forms g = dy*act'(u) and per-block partials of
 // sum(g), sum(g*xhat); bn_bwd_finalize -> dgamma, dbeta and the three apply
 // coefficients; bn_bwd_apply writes dz = gamma*rstd*(g - mean(g) - xhat*mean(g*xhat)).
 // Dtypes: z fp16, activations (out, residual) fp16, gradients (dy, dz) bf16.
+//
+// Streaming kernels: a 256-thread block covers rows x (C/8) lanes, each thread
+// owns 8 consecutive channels (16-B loads/stores) of one pixel per iteration
+// and keeps its channels' parameters in registers; every activation view is a
+// whole (B, H, W, ld) buffer, so pixel m lives at m*ld (no integer division).
 #include <algorithm>
 
 #include "common.h"
@@ -48,44 +53,90 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
     for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
+__device__ __forceinline__ void load8(const float* p, float* v) {
+    float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ float dsilu(float u) {
+    float sg = 1.0f / (1.0f + __expf(-u));
+    return sg * (1.0f + u * (1.0f - sg));
+}
 
-// grid: ceil(C/64) blocks of 1024 = 64 channels x 16 row groups
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pq,
-                                                           int G, int C, double count, const float* __restrict__ gamma,
-                                                           const float* __restrict__ beta, float* running_mean,
-                                                           float* running_var, int64_t* nbt, float momentum, float eps,
-                                                           float* __restrict__ scale, float* __restrict__ shift,
-                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out) {
-    __shared__ double sh[2][16][64];
+// ---------------------------------------------------------------- two-level reduction of [G][C] partials
+// level 1: grid (ceil(C/64), R), 256 threads = 64 channels x 4 row groups -> out [R][2][C] fp64
+__global__ void __launch_bounds__(256) partials_reduce_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                              int G, int C, int R, double* __restrict__ out) {
+    __shared__ double sh[2][4][64];
     const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
+    const int per = (G + R - 1) / R;
+    const int g0 = blockIdx.y * per, g1 = min(G, g0 + per);
     double s = 0.0, q = 0.0;
-    if (c < C)
-        for (int g = rg; g < G; g += 16) {
-            s += ps[int64_t(g) * C + c];
-            q += pq[int64_t(g) * C + c];
+    if (c < C) {
+#pragma unroll 4
+        for (int g = g0 + rg; g < g1; g += 4) {
+            s += a[int64_t(g) * C + c];
+            q += b[int64_t(g) * C + c];
         }
+    }
     sh[0][rg][cl] = s;
     sh[1][rg][cl] = q;
     __syncthreads();
     if (rg == 0 && c < C) {
-        for (int r = 1; r < 16; ++r) { s += sh[0][r][cl]; q += sh[1][r][cl]; }
-        double mean = s / count;
-        double var = q / count - mean * mean;
-        if (var < 0) var = 0;
-        double rstd = 1.0 / sqrt(var + double(eps));
-        float sc = float(double(gamma[c]) * rstd);
-        scale[c] = sc;
-        shift[c] = float(double(beta[c]) - mean * double(sc));
-        mean_out[c] = float(mean);
-        rstd_out[c] = float(rstd);
-        if (running_mean) {
-            double unb = count > 1 ? var * count / (count - 1) : var;
-            running_mean[c] = float((1.0 - momentum) * running_mean[c] + momentum * mean);
-            running_var[c] = float((1.0 - momentum) * running_var[c] + momentum * unb);
-        }
+        s = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+        q = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+        out[(int64_t(blockIdx.y) * 2 + 0) * C + c] = s;
+        out[(int64_t(blockIdx.y) * 2 + 1) * C + c] = q;
     }
-    if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__device__ __forceinline__ void fold(const double* p, int R, int C, int c, double& s, double& q) {
+    s = 0.0;
+    q = 0.0;
+    for (int r = 0; r < R; ++r) {
+        s += p[(int64_t(r) * 2 + 0) * C + c];
+        q += p[(int64_t(r) * 2 + 1) * C + c];
+    }
+}
+
+__global__ void bn_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                                   float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
+                                   float* __restrict__ rstd_out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (nbt && c == 0) *nbt += 1;
+    if (c >= C) return;
+    double s, q;
+    fold(p2, R, C, c, s, q);
+    double mean = s / count;
+    double var = q / count - mean * mean;
+    if (var < 0) var = 0;
+    double rstd = 1.0 / sqrt(var + double(eps));
+    float sc = float(double(gamma[c]) * rstd);
+    scale[c] = sc;
+    shift[c] = float(double(beta[c]) - mean * double(sc));
+    mean_out[c] = float(mean);
+    rstd_out[c] = float(rstd);
+    if (running_mean) {
+        double unb = count > 1 ? var * count / (count - 1) : var;
+        running_mean[c] = float((1.0 - momentum) * running_mean[c] + momentum * mean);
+        running_var[c] = float((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+}
+
+__global__ void bn_bwd_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
+                                       float* dbeta, int accumulate, float* __restrict__ coef) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    double s, q;
+    fold(p2, R, C, c, s, q);
+    if (dgamma) dgamma[c] = float(accumulate ? dgamma[c] + q : q);
+    if (dbeta) dbeta[c] = float(accumulate ? dbeta[c] + s : s);
+    coef[c] = gamma[c] * rstd[c];               // k1
+    coef[C + c] = float(s / count);             // k2 = mean(g)
+    coef[2 * C + c] = float(q / count);         // k3 = mean(g * xhat)
 }
 
 // eval: scale/shift from running stats
@@ -99,148 +150,141 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
     shift[c] = beta[c] - rm[c] * sc;
 }
 
-// out[view] = act(z*scale + shift) (+ res[view]); z dense fp16 [M][C]; 8 channels per thread
-__global__ void bn_apply_kernel(const bf16_t* __restrict__ z, int64_t M, int C, int HW, const float* __restrict__ scale,
-                                const float* __restrict__ shift, int act, const bf16_t* __restrict__ res, int64_t r_bs,
-                                int64_t r_ld, bf16_t* __restrict__ out, int64_t o_bs, int64_t o_ld,
-                                float* __restrict__ out32) {
-    const int cg = C / 8;
-    const int64_t total = M * cg;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int g = int(i % cg);
-        int64_t m = i / cg;
-        int64_t n = m / HW, pix = m - n * HW;
+// ---------------------------------------------------------------- streaming kernels
+struct Lanes {
+    int g, r, rows;
+    bool on;
+};
+__device__ __forceinline__ Lanes lanes(int C) {
+    const int cg = C >> 3;
+    Lanes L;
+    L.rows = 256 / cg;
+    L.g = threadIdx.x % cg;
+    L.r = threadIdx.x / cg;
+    L.on = L.r < L.rows;
+    return L;
+}
+
+// out[m*o_ld + c] = act(z*scale + shift) (+ res[m*r_ld + c]);  optional fp32 dense copy
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ z, int64_t M, int C,
+                                                       const float* __restrict__ scale, const float* __restrict__ shift,
+                                                       int act, const bf16_t* __restrict__ res, int64_t r_ld,
+                                                       bf16_t* __restrict__ out, int64_t o_ld, float* __restrict__ out32) {
+    const Lanes L = lanes(C);
+    if (!L.on) return;
+    const int c0 = L.g * 8;
+    float sc[8], sf[8];
+    load8(scale + c0, sc);
+    load8(shift + c0, sf);
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
         float v[8];
-        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + g * 8), v);
+        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), v);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            float u = v[k] * scale[g * 8 + k] + shift[g * 8 + k];
+            float u = v[k] * sc[k] + sf[k];
             v[k] = act ? silu_f(u) : u;
         }
         if (res) {
             float r[8];
-            unpack8h(*reinterpret_cast<const uint4*>(res + n * r_bs + pix * r_ld + g * 8), r);
+            unpack8h(*reinterpret_cast<const uint4*>(res + m * r_ld + c0), r);
 #pragma unroll
             for (int k = 0; k < 8; ++k) v[k] += r[k];
         }
-        *reinterpret_cast<uint4*>(out + n * o_bs + pix * o_ld + g * 8) = pack8h(v);
+        *reinterpret_cast<uint4*>(out + m * o_ld + c0) = pack8h(v);
         if (out32) {
-            float4* o = reinterpret_cast<float4*>(out32 + m * C + g * 8);
+            float4* o = reinterpret_cast<float4*>(out32 + m * C + c0);
             o[0] = make_float4(v[0], v[1], v[2], v[3]);
             o[1] = make_float4(v[4], v[5], v[6], v[7]);
         }
     }
 }
 
-// per-block partials of sum(g) and sum(g*xhat); block = 256 threads = cg channel groups x rows
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld,
-                                                            const bf16_t* __restrict__ z, int64_t M, int C, int HW,
+// per-block partials of sum(g) and sum(g*xhat)
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __restrict__ dy, int64_t d_ld,
+                                                            const bf16_t* __restrict__ z, int64_t M, int C,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act,
                                                             float* __restrict__ ps, float* __restrict__ pg) {
-    extern __shared__ float red[];   // [2][C]
-    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) red[i] = 0.f;
-    __syncthreads();
-    const int cg = C / 8;
-    const int rows = blockDim.x / cg;
-    const int g = threadIdx.x % cg, r = threadIdx.x / cg;
-    float s[8] = {0}, sx[8] = {0};
-    if (r < rows) {
+    extern __shared__ float red[];   // [2][rows][C]
+    const Lanes L = lanes(C);
+    const int c0 = L.g * 8;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (L.on) {
         float sc[8], sf[8], mu[8], rs[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            sc[k] = scale[g * 8 + k]; sf[k] = shift[g * 8 + k];
-            mu[k] = mean[g * 8 + k]; rs[k] = rstd[g * 8 + k];
-        }
-        for (int64_t m = int64_t(blockIdx.x) * rows + r; m < M; m += int64_t(gridDim.x) * rows) {
-            int64_t n = m / HW, pix = m - n * HW;
+        load8(scale + c0, sc);
+        load8(shift + c0, sf);
+        load8(mean + c0, mu);
+        load8(rstd + c0, rs);
+        for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
             float zv[8], dv[8];
-            unpack8h(*reinterpret_cast<const uint4*>(z + m * C + g * 8), zv);
-            unpack8(*reinterpret_cast<const uint4*>(dy + n * d_bs + pix * d_ld + g * 8), dv);
+            unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), zv);
+            unpack8(*reinterpret_cast<const uint4*>(dy + m * d_ld + c0), dv);
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                float gg = dv[k];
-                if (act) {
-                    float u = zv[k] * sc[k] + sf[k];
-                    float sg = 1.0f / (1.0f + __expf(-u));
-                    gg *= sg * (1.0f + u * (1.0f - sg));
-                }
-                float xh = (zv[k] - mu[k]) * rs[k];
+                float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
                 s[k] += gg;
-                sx[k] += gg * xh;
+                sx[k] += gg * ((zv[k] - mu[k]) * rs[k]);
             }
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            atomicAdd(&red[g * 8 + k], s[k]);
-            atomicAdd(&red[C + g * 8 + k], sx[k]);
+            red[L.r * C + c0 + k] = s[k];
+            red[(L.rows + L.r) * C + c0 + k] = sx[k];
         }
     }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        ps[int64_t(blockIdx.x) * C + c] = red[c];
-        pg[int64_t(blockIdx.x) * C + c] = red[C + c];
-    }
-}
-
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ ps, const float* __restrict__ pg,
-                                                               int G, int C, double count,
-                                                               const float* __restrict__ gamma,
-                                                               const float* __restrict__ rstd, float* dgamma,
-                                                               float* dbeta, int accumulate, float* __restrict__ coef) {
-    __shared__ double sh[2][16][64];
-    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
-    double s = 0.0, q = 0.0;
-    if (c < C)
-        for (int g = rg; g < G; g += 16) {
-            s += ps[int64_t(g) * C + c];
-            q += pg[int64_t(g) * C + c];
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < L.rows; ++r) {
+            a += red[r * C + c];
+            b += red[(L.rows + r) * C + c];
         }
-    sh[0][rg][cl] = s;
-    sh[1][rg][cl] = q;
-    __syncthreads();
-    if (rg == 0 && c < C) {
-        for (int r = 1; r < 16; ++r) { s += sh[0][r][cl]; q += sh[1][r][cl]; }
-        if (dgamma) dgamma[c] = float(accumulate ? dgamma[c] + q : q);
-        if (dbeta) dbeta[c] = float(accumulate ? dbeta[c] + s : s);
-        coef[c] = gamma[c] * rstd[c];               // k1
-        coef[C + c] = float(s / count);             // k2 = mean(g)
-        coef[2 * C + c] = float(q / count);         // k3 = mean(g * xhat)
+        ps[int64_t(blockIdx.x) * C + c] = a;
+        pg[int64_t(blockIdx.x) * C + c] = b;
     }
 }
 
-// dz[m][c] = k1*(g - k2 - xhat*k3), dz dense [M][C]
-__global__ void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld,
-                                    const bf16_t* __restrict__ z, int64_t M, int C, int HW,
-                                    const float* __restrict__ scale, const float* __restrict__ shift,
-                                    const float* __restrict__ mean, const float* __restrict__ rstd, int act,
-                                    const float* __restrict__ coef, bf16_t* __restrict__ dz) {
-    const int cg = C / 8;
-    const int64_t total = M * cg;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int g = int(i % cg);
-        int64_t m = i / cg;
-        int64_t n = m / HW, pix = m - n * HW;
+// dz[m][c] = k1*(g - k2 - xhat*k3), dz dense [M][C] (may alias z)
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, int64_t d_ld,
+                                                           const bf16_t* z, int64_t M, int C,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, int act,
+                                                           const float* __restrict__ coef, bf16_t* dz) {
+    const Lanes L = lanes(C);
+    if (!L.on) return;
+    const int c0 = L.g * 8;
+    float sc[8], sf[8], mu[8], rs[8], k1[8], k2[8], k3[8];
+    load8(scale + c0, sc);
+    load8(shift + c0, sf);
+    load8(mean + c0, mu);
+    load8(rstd + c0, rs);
+    load8(coef + c0, k1);
+    load8(coef + C + c0, k2);
+    load8(coef + 2 * C + c0, k3);
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
         float zv[8], dv[8], o[8];
-        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + g * 8), zv);
-        unpack8(*reinterpret_cast<const uint4*>(dy + n * d_bs + pix * d_ld + g * 8), dv);
+        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), zv);
+        unpack8(*reinterpret_cast<const uint4*>(dy + m * d_ld + c0), dv);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            int c = g * 8 + k;
-            float gg = dv[k];
-            if (act) {
-                float u = zv[k] * scale[c] + shift[c];
-                float sg = 1.0f / (1.0f + __expf(-u));
-                gg *= sg * (1.0f + u * (1.0f - sg));
-            }
-            float xh = (zv[k] - mean[c]) * rstd[c];
-            o[k] = coef[c] * (gg - coef[C + c] - xh * coef[2 * C + c]);
+            float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
+            float xh = (zv[k] - mu[k]) * rs[k];
+            o[k] = k1[k] * (gg - k2[k] - xh * k3[k]);
         }
-        *reinterpret_cast<uint4*>(dz + m * C + g * 8) = pack8(o);
+        *reinterpret_cast<uint4*>(dz + m * C + c0) = pack8(o);
     }
+}
+
+constexpr int RED_R = 32;   // level-1 row splits of the partials reduction
+
+int stream_blocks(int64_t M, int C, int cap) {
+    int rows = 256 / (C / 8);
+    int64_t g = (M + rows - 1) / rows;
+    return int(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
 }
 
 }  // namespace
@@ -248,19 +292,23 @@ __global__ void bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, int64_t d_bs,
 
 using namespace ym;
 
-static int grid_for(int64_t work, int threads = 256, int cap = 4096) {
-    int64_t g = (work + threads - 1) / threads;
-    return int(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
-}
+#define CHECK_C(c) YM_CHECK_ARG((c) % 8 == 0 && (c) / 8 <= 256, "BN: C=%d must be a multiple of 8 and <= 2048", (c))
+#define CHECK_VIEW(bs, ld, hw) YM_CHECK_ARG((bs) == int64_t(hw) * (ld) && (ld) % 8 == 0, \
+                                            "BN: views must be whole-image buffers with 16-B aligned rows")
+
+extern "C" size_t ym_bn_workspace_size(int c) { return size_t(RED_R) * 2 * c * sizeof(double); }
 
 extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count,
                               const float* gamma, const float* beta, float* running_mean, float* running_var,
                               int64_t* num_batches_tracked, float momentum, float eps, float* scale, float* shift,
-                              float* mean, float* rstd, void* stream) {
-    YM_CHECK_ARG(count > 0, "ym_bn_finalize: count must be > 0");
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 63) / 64), dim3(1024), 0, as_stream(stream), part_sum, part_sq,
-                       parts, c, count, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
-                       scale, shift, mean, rstd);
+                              float* mean, float* rstd, void* workspace, void* stream) {
+    YM_CHECK_ARG(count > 0 && workspace, "ym_bn_finalize: count must be > 0, workspace required");
+    hipStream_t st = as_stream(stream);
+    double* p2 = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_sq, parts,
+                       c, RED_R, p2);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, st, p2, RED_R, c, count, gamma, beta,
+                       running_mean, running_var, num_batches_tracked, momentum, eps, scale, shift, mean, rstd);
     YM_LAUNCH_CHECK("ym_bn_finalize");
     return YM_OK;
 }
@@ -276,37 +324,41 @@ extern "C" int ym_bn_eval_coeff(int c, const float* gamma, const float* beta, co
 extern "C" int ym_bn_apply(const uint16_t* z, int64_t m, int c, int hw, const float* scale, const float* shift,
                            int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* out, int64_t o_bs,
                            int64_t o_ld, float* out32, void* stream) {
-    YM_CHECK_ARG(c % 8 == 0, "ym_bn_apply: C %% 8 != 0");
-    YM_CHECK_ARG(o_ld % 8 == 0 && o_bs % 8 == 0 && (!res || (r_ld % 8 == 0 && r_bs % 8 == 0)),
-                 "ym_bn_apply: views must be 16-byte aligned");
+    CHECK_C(c);
+    CHECK_VIEW(o_bs, o_ld, hw);
+    if (res) CHECK_VIEW(r_bs, r_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(grid_for(m * (c / 8))), dim3(256), 0, as_stream(stream), z, m, c, hw,
-                       scale, shift, act, res, r_bs, r_ld, out, o_bs, o_ld, out32);
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(m, c, 4096)), dim3(256), 0, as_stream(stream), z, m, c,
+                       scale, shift, act, res, r_ld, out, o_ld, out32);
     YM_LAUNCH_CHECK("ym_bn_apply");
     return YM_OK;
 }
 
-extern "C" int ym_bn_bwd_blocks(int64_t m, int c) {
-    int rows = 256 / (c / 8);
-    return grid_for((m + rows - 1) / rows, 1, 2048);
-}
+extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, 1024); }
 
 extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
                                 int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
                                 int act, float* part_sum, float* part_dot, void* stream) {
-    YM_CHECK_ARG(c % 8 == 0 && c / 8 <= 256, "ym_bn_bwd_reduce: C=%d unsupported", c);
+    CHECK_C(c);
+    CHECK_VIEW(d_bs, d_ld, hw);
     int blocks = ym_bn_bwd_blocks(m, c);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2 * c) * sizeof(float), as_stream(stream),
-                       dy, d_bs, d_ld, z, m, c, hw, scale, shift, mean, rstd, act, part_sum, part_dot);
+    int rows = 256 / (c / 8);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2) * rows * c * sizeof(float),
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot);
     YM_LAUNCH_CHECK("ym_bn_bwd_reduce");
     return YM_OK;
 }
 
 extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                                   const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
-                                  float* coef, void* stream) {
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 63) / 64), dim3(1024), 0, as_stream(stream), part_sum,
-                       part_dot, parts, c, count, gamma, rstd, dgamma, dbeta, accumulate, coef);
+                                  float* coef, void* workspace, void* stream) {
+    YM_CHECK_ARG(workspace, "ym_bn_bwd_finalize: workspace required");
+    hipStream_t st = as_stream(stream);
+    double* p2 = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_dot, parts,
+                       c, RED_R, p2);
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, st, p2, RED_R, c, count, gamma,
+                       rstd, dgamma, dbeta, accumulate, coef);
     YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
     return YM_OK;
 }
@@ -314,9 +366,11 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
 extern "C" int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
                                int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
                                int act, const float* coef, uint16_t* dz, void* stream) {
+    CHECK_C(c);
+    CHECK_VIEW(d_bs, d_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(m * (c / 8))), dim3(256), 0, as_stream(stream), dy, d_bs,
-                       d_ld, z, m, c, hw, scale, shift, mean, rstd, act, coef, dz);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(m, c, 4096)), dim3(256), 0, as_stream(stream), dy, d_ld,
+                       z, m, c, scale, shift, mean, rstd, act, coef, dz);
     YM_LAUNCH_CHECK("ym_bn_bwd_apply");
     return YM_OK;
 }

@@ -92,11 +92,11 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
             int row = id / NCH;
             int64_t m = m0 + row;
             b_ok[it] = (id < BM * NCH) && (m < a.M);
-            int64_t n = b_ok[it] ? m / OHW : 0;
-            int64_t pix = b_ok[it] ? m - n * OHW : 0;
-            b_img[it] = n * a.x_bs;
-            b_oh[it] = int(pix / a.OW);
-            b_ow[it] = int(pix - int64_t(b_oh[it]) * a.OW);
+            const uint32_t um = b_ok[it] ? uint32_t(m) : 0u;
+            const uint32_t n = um / uint32_t(OHW), pix = um - n * uint32_t(OHW);
+            b_img[it] = int64_t(n) * a.x_bs;
+            b_oh[it] = int(pix / uint32_t(a.OW));
+            b_ow[it] = int(pix - uint32_t(b_oh[it]) * uint32_t(a.OW));
         }
         uint4 ra[A_ITEMS], rb[B_ITEMS];
         auto load = [&](int k) {
@@ -200,8 +200,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
         for (int j = 0; j < TN; ++j) {
             const int64_t m = m0 + wc * (BM / 2) + j * 16 + fr;
             if (m >= a.M) continue;
-            const int64_t n = m / OHW, pix = m - n * OHW;
-            const int64_t obase = n * a.y_bs + pix * a.y_ld;
+            const uint32_t n = uint32_t(m) / uint32_t(OHW), pix = uint32_t(m) - n * uint32_t(OHW);
+            const int64_t obase = int64_t(n) * a.y_bs + int64_t(pix) * a.y_ld;
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int cb = n0 + wr * (BN / 2) + i * 16 + fc * 4;
@@ -320,19 +320,21 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     uint4 ra, rb;
+    const uint32_t uOHW = uint32_t(OHW), uOW = uint32_t(a.OW);
     auto load = [&](int64_t p0) {
         int64_t p = p0 + srow;
         ra = make_uint4(0, 0, 0, 0);
         rb = make_uint4(0, 0, 0, 0);
         if (p < p_end) {
-            int64_t n = p / OHW, pix = p - n * OHW;
-            int oh = int(pix / a.OW), ow = int(pix - int64_t(oh) * a.OW);
+            const uint32_t up = uint32_t(p);                  // M < 2^31 (checked on the host)
+            const uint32_t n = up / uOHW, pix = up - n * uOHW;
+            const int oh = int(pix / uOW), ow = int(pix - uint32_t(oh) * uOW);
             int co = co0 + sc * 8;
-            if (co < a.Cout) ra = *reinterpret_cast<const uint4*>(a.dz + n * a.dz_bs + pix * a.dz_ld + co);
+            if (co < a.Cout) ra = *reinterpret_cast<const uint4*>(a.dz + int64_t(n) * a.dz_bs + int64_t(pix) * a.dz_ld + co);
             int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
             int ci = ci0 + sc * 8;
             if (ci < a.Cin && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW) {
-                uint4 h = *reinterpret_cast<const uint4*>(a.x + n * a.x_bs + (int64_t(ih) * a.IW + iw) * a.x_ld + ci);
+                uint4 h = *reinterpret_cast<const uint4*>(a.x + int64_t(n) * a.x_bs + (int64_t(ih) * a.IW + iw) * a.x_ld + ci);
                 uint32_t w4[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)   // fp16 activation -> bf16 MFMA operand
@@ -661,6 +663,7 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
     a.M = int64_t(d->n) * d->oh * d->ow;
     a.out_f32 = d->out_f32; a.accumulate = d->accumulate;
     if (a.M == 0) return YM_OK;
+    YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
     pick_and_launch(a, MODE_FWD, 2048, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
@@ -682,6 +685,7 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     a.M = int64_t(d->n) * d->h * d->w;
     a.accumulate = d->accumulate;
     if (a.M == 0) return YM_OK;
+    YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
     pick_and_launch(a, MODE_DGRAD, 4096, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_dgrad");
     return YM_OK;
@@ -701,6 +705,7 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
     a.M = int64_t(d->n) * d->oh * d->ow;
     if (a.M == 0) return YM_OK;
+    YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_wgrad: too many pixels");
     int co_t = (a.Cout + WG_T - 1) / WG_T;
     a.ci_tiles = (a.Cin + WG_T - 1) / WG_T;
     int cols = a.ci_tiles * a.KH * a.KW;

@@ -114,7 +114,7 @@ struct AssignWs {
     int* fg;             // [B][A] foreground flag
     unsigned long long* amax;   // [B][M] packed (iou bits << 32 | ~a)   (zeroed)
     int* gcnt;           // [B][M] in-box positives per gt           (zeroed)
-    double* part;        // [nblk][4] loss partials
+    double* part;        // [nblk][5] loss partials (cls, box, dfl, tss, num_fg)
     float* out;          // [8] loss, items[3], tss, num_fg ...
 };
 
@@ -332,10 +332,10 @@ __device__ __forceinline__ float bce(float x, float t) {
 __global__ void __launch_bounds__(256) loss_partial_kernel(const float* __restrict__ head, int64_t A, int no, int nc,
                                                            Levels L, const float4* __restrict__ gt_box,
                                                            const float* __restrict__ gt_lab, int M, AssignWs w) {
-    __shared__ double red[4][256];
+    __shared__ double red[5][256];
     const int b = blockIdx.y;
     const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    double lc = 0, lb = 0, ld = 0, ts = 0;
+    double lc = 0, lb = 0, ld = 0, ts = 0, nf = 0;
     if (a < A) {
         const int64_t i = int64_t(b) * A + a;
         const float* x = head + i * no;
@@ -349,6 +349,7 @@ __global__ void __launch_bounds__(256) loss_partial_kernel(const float* __restri
         }
         if (f) {
             ts = nm;
+            nf = 1;
             float ax, ay, s;
             anchor_of(L, a, ax, ay, s);
             float4 pb = w.pbox[i];
@@ -379,24 +380,23 @@ __global__ void __launch_bounds__(256) loss_partial_kernel(const float* __restri
     red[1][threadIdx.x] = lb;
     red[2][threadIdx.x] = ld;
     red[3][threadIdx.x] = ts;
+    red[4][threadIdx.x] = nf;
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if (threadIdx.x < o)
-            for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+            for (int k = 0; k < 5; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
         __syncthreads();
     }
-    if (threadIdx.x < 4) w.part[(int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = red[threadIdx.x][0];
+    if (threadIdx.x < 5) w.part[(int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 5 + threadIdx.x] = red[threadIdx.x][0];
 }
 
 // out: [0] loss, [1..3] items (box, cls, dfl with gains), [4] tss, [5] num_fg
-__global__ void loss_final_kernel(int nparts, int B, const int* __restrict__ fg, int64_t BA, AssignWs w) {
+__global__ void loss_final_kernel(int nparts, int B, AssignWs w) {
     __shared__ double red[5][256];
-    double s[4] = {0, 0, 0, 0}, nf = 0;
+    double s[5] = {0, 0, 0, 0, 0};
     for (int p = threadIdx.x; p < nparts; p += blockDim.x)
-        for (int k = 0; k < 4; ++k) s[k] += w.part[int64_t(p) * 4 + k];
-    for (int64_t i = threadIdx.x; i < BA; i += blockDim.x) nf += fg[i];
-    for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = s[k];
-    red[4][threadIdx.x] = nf;
+        for (int k = 0; k < 5; ++k) s[k] += w.part[int64_t(p) * 5 + k];
+    for (int k = 0; k < 5; ++k) red[k][threadIdx.x] = s[k];
     __syncthreads();
     for (int o = 128; o > 0; o >>= 1) {
         if (threadIdx.x < o)
@@ -517,7 +517,7 @@ Carve carve(void* base, int64_t B, int64_t A, int M, int64_t nparts) {
     c.w.tgi = reinterpret_cast<int*>(take(BA * 4));
     c.w.norm = reinterpret_cast<float*>(take(BA * 4));
     c.w.fg = reinterpret_cast<int*>(take(BA * 4));
-    c.w.part = reinterpret_cast<double*>(take(size_t(nparts) * 4 * 8));
+    c.w.part = reinterpret_cast<double*>(take(size_t(nparts) * 5 * 8));
     c.bytes = off;
     return c;
 }
@@ -585,7 +585,7 @@ extern "C" int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int 
     }
     hipLaunchKernelGGL(loss_partial_kernel, ga, dim3(256), 0, st, head, A, no, nc, L,
                        reinterpret_cast<const float4*>(gt_box), gt_lab, M, w);
-    hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, int(nparts), int(B), w.fg, B * A, w);
+    hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, int(nparts), int(B), w);
     YM_LAUNCH_CHECK("ym_loss_fwd");
     return YM_OK;
 }

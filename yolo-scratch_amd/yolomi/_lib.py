@@ -52,12 +52,13 @@ SIGNATURES = {
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
-    "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P]),
+    "ym_bn_workspace_size": (SZ, [INT]),
+    "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
     "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
     "ym_bn_apply": (R, [P, I64, INT, INT, P, P, INT, P, I64, I64, P, I64, I64, P, P]),
     "ym_bn_bwd_blocks": (R, [I64, INT]),
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
-    "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P]),
+    "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_maxpool5_fwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, P]),
     "ym_maxpool5_bwd": (R, [P, I64, I64, P, P, INT, INT, INT, INT, P]),

@@ -208,7 +208,7 @@ class ConvBN:
         if plan.training:
             call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
                  _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
         else:
             call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
                  float(bn.eps), sc, sh, st)
@@ -225,7 +225,7 @@ class ConvBN:
         call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
              self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
         call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
         dz = self.z  # reuse the z buffer? no: z is needed by nobody after this op -> in-place dz
         call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
              self.act, self.coef.data_ptr(), dz.data_ptr(), st)
@@ -279,7 +279,7 @@ class StemConvBN(ConvBN):
         if plan.training:
             call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
                  _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
         else:
             call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
                  float(bn.eps), sc, sh, st)
@@ -294,7 +294,7 @@ class StemConvBN(ConvBN):
         call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
              1, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
         call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
         call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
              1, self.coef.data_ptr(), self.z.data_ptr(), st)
         call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight), plan.B,
@@ -326,7 +326,7 @@ class DWConvBN(ConvBN):
         if plan.training:
             call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.C, float(self.M), _p(bn.weight),
                  _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, st)
+                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
         else:
             call("ym_bn_eval_coeff", self.C, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
                  float(bn.eps), sc, sh, st)
@@ -342,7 +342,7 @@ class DWConvBN(ConvBN):
         call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
              0, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
         call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.C, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), st)
+             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
         call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
              0, self.coef.data_ptr(), self.z.data_ptr(), st)
         acc = self.res.grad_for_write(st)
@@ -530,6 +530,7 @@ class Plan:
         self.acts, self.ops = [], []
         self.weights = WeightStore(self)
         self.probe, self.probe_events = None, []   # bench: time one op's conv launch
+        self.bn_ws = torch.empty(lib().ym_bn_workspace_size(2048) // 4, dtype=F32, device=dev)
         self.input = None          # View for block plans
         self.img = None            # fp32 image for the full model
         self.head = None           # (B, A, 64+nc) fp32 for the full model
