@@ -90,7 +90,7 @@ typedef struct {
 
 typedef struct {
     const float* src;          /* fp32 OIHW master weight */
-    uint16_t* dst_fwd;         /* bf16 [cout][kh][kw][cin] or NULL */
+    uint16_t* dst_fwd;         /* fp16 [cout][kh][kw][cin] (forward) or NULL */
     uint16_t* dst_t;           /* bf16 [cin][kh][kw][cout] (dgrad) or NULL */
     int64_t elem_offset;       /* running element offset of this entry */
     int32_t cout, cin, kh, kw;
@@ -99,7 +99,7 @@ typedef struct {
 
 /* Number of grid-x blocks (= rows of the BN statistics partials) ym_conv_fwd uses. */
 int ym_conv_stat_blocks(int64_t m, int cout);
-/* y = conv(x, w) (+bias); optional per-block channel sum / sum-of-squares partials
+/* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
  * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                 float* stat_sum, float* stat_sq, void* stream);

@@ -1,0 +1,115 @@
+"""Implicit-GEMM conv kernels (fwd / dgrad / wgrad) vs a PyTorch fp32 reference of the same op.
+
+The operands are rounded to the kernel's input dtypes first (fp16 activations and forward
+weights, bf16 gradients and dgrad weights), so the reference differs from the kernel only
+by fp32 accumulation order and the output rounding:
+  fwd  fp32 out: rel 1e-3 of max|y|
+  dgrad bf16 out: rel 1e-2 of max|dx| (one bf16 rounding = 2^-8)
+  wgrad fp32 out: rel 1e-3 of max|dw| (x is converted fp16 -> bf16 at staging, mirrored here)
+Shapes cover odd spatial sizes, both strides, k = 1 and 3, channel counts that are not
+multiples of the tile sizes, and the 4-parity-class stride-2 dgrad (a 1x1 stride-2 conv
+leaves three of the classes with no tap: their gradient must be exactly zero).
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [
+    # n, h, w, cin, cout, k, stride, pad
+    (2, 9, 11, 64, 96, 3, 2, 1),
+    (2, 8, 8, 32, 64, 3, 1, 1),
+    (1, 7, 5, 48, 40, 1, 2, 0),
+    (2, 13, 13, 128, 136, 3, 2, 1),
+    (1, 6, 6, 16, 24, 1, 1, 0),
+    (3, 20, 20, 256, 128, 3, 2, 1),
+    (1, 5, 7, 520, 264, 3, 1, 1),
+]
+
+
+def _desc(n, h, w, cin, cout, k, s, p):
+    from yolomi._lib import ConvDesc
+    oh = (h + 2 * p - k) // s + 1
+    ow = (w + 2 * p - k) // s + 1
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, oh, ow, cout, k, s, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * cin, cin, oh * ow * cout, cout
+    d.out_f32, d.accumulate = 1, 0
+    return d, oh, ow
+
+
+@pytest.mark.parametrize("shape", SHAPES, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in SHAPES])
+def test_conv_kernels_vs_torch(shape):
+    from yolomi._lib import call
+    n, h, w, cin, cout, k, s, p = shape
+    d, oh, ow = _desc(*shape)
+    g = torch.Generator().manual_seed(hash(shape) & 0xFFFF)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, generator=g).half()
+    wt = (torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5)
+    dz = torch.randn(n, oh, ow, cout, generator=g).bfloat16()
+
+    w16 = wt.half()                                   # forward copy [cout][kh][kw][cin] fp16
+    wbf = wt.bfloat16()                               # dgrad copy [cin][kh][kw][cout] bf16
+    xd = x.to(dev)
+    w_fwd = w16.permute(0, 2, 3, 1).contiguous().to(dev)
+    w_t = wbf.permute(1, 2, 3, 0).contiguous().to(dev)
+    dzd = dz.to(dev)
+    st = torch.cuda.current_stream().cuda_stream
+
+    # forward, fp32 output
+    y = torch.empty(n, oh, ow, cout, dtype=torch.float32, device=dev)
+    call("ym_conv_fwd", ctypes.byref(d), xd.data_ptr(), w_fwd.data_ptr(), y.data_ptr(), None, None, None, st)
+    x_nchw = x.float().permute(0, 3, 1, 2)
+    y_ref = F.conv2d(x_nchw, w16.float(), stride=s, padding=p).permute(0, 2, 3, 1)
+    # dgrad, bf16 output; prefill with garbage: every pixel must be written
+    dx = torch.full((n, h, w, cin), float("nan"), dtype=torch.bfloat16, device=dev)
+    call("ym_conv_dgrad", ctypes.byref(d), dzd.data_ptr(), w_t.data_ptr(), dx.data_ptr(), st)
+    dz_nchw = dz.float().permute(0, 3, 1, 2)
+    dx_ref = torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz_nchw, stride=s, padding=p).permute(0, 2, 3, 1)
+    # wgrad into [cout][taps][cin] fp32
+    dw = torch.zeros(cout, k * k, cin, dtype=torch.float32, device=dev)
+    call("ym_conv_wgrad", ctypes.byref(d), dzd.data_ptr(), xd.data_ptr(), dw.data_ptr(), st)
+    dw_ref = torch.nn.grad.conv2d_weight(x.bfloat16().float().permute(0, 3, 1, 2), (cout, cin, k, k), dz_nchw,
+                                         stride=s, padding=p)
+    dw_ref = dw_ref.permute(0, 2, 3, 1).reshape(cout, k * k, cin)
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        return float((a.float().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+    assert rel(y, y_ref) < 1e-3
+    assert torch.isfinite(dx.float()).all()
+    assert rel(dx, dx_ref) < 1e-2
+    assert rel(dw, dw_ref) < 1e-3
+    if k == 1 and s == 2:
+        # pixels at odd rows or odd columns receive no tap
+        dxc = dx.float().cpu()
+        assert (dxc[:, 1::2] == 0).all() and (dxc[:, :, 1::2] == 0).all()
+
+
+def test_dgrad_accumulate_stride2():
+    """accumulate=1 adds the transposed conv into an existing gradient (concat/residual fan-in)."""
+    from yolomi._lib import call
+    shape = (2, 10, 12, 64, 64, 3, 2, 1)
+    n, h, w, cin, cout, k, s, p = shape
+    d, oh, ow = _desc(*shape)
+    d.accumulate = 1
+    g = torch.Generator().manual_seed(7)
+    dev = torch.device("cuda", 0)
+    wt = torch.randn(cout, cin, k, k, generator=g) * 0.05
+    wbf = wt.bfloat16()
+    dz = torch.randn(n, oh, ow, cout, generator=g).bfloat16()
+    base = torch.randn(n, h, w, cin, generator=g).bfloat16()
+    dx = base.to(dev)
+    w_t = wbf.permute(1, 2, 3, 0).contiguous().to(dev)
+    call("ym_conv_dgrad", ctypes.byref(d), dz.to(dev).data_ptr(), w_t.data_ptr(), dx.data_ptr(),
+         torch.cuda.current_stream().cuda_stream)
+    ref = base.float() + torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz.float().permute(0, 3, 1, 2),
+                                                    stride=s, padding=p).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    err = float((dx.float().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < 1e-2

@@ -3,9 +3,11 @@
 Tolerances (BASELINE.json north_star: 1e-2 for 16-bit tensors): activations are fp16 and
 gradients bf16, so single blocks are held to relative-L2 <= 1e-2 (outputs) / 2e-2 (input and
 parameter gradients); the full n@320 network's head maps to <= 1e-2; loss items <= 1e-2;
-per-parameter gradient norms within 10% (P5-branch gradients hinge on a handful of stride-32
-anchors whose assignment follows the predicted boxes) — stated per assert.  The loss on fp32 head maps is an fp32 path: assignment decisions
-(fg mask, target_gt_idx) are bit-exact and loss values / head gradients within 1e-4.
+per-parameter gradients within 10%, or within 2x the distance of the oracle run under the
+HIP storage-rounding model (oracle/precision.py) where that is larger: backbone gradients are
+discontinuous in the activations through SPPF's max-pool routing — stated per assert.  The loss
+on fp32 head maps is an fp32 path: assignment decisions (fg mask, target_gt_idx) are bit-exact
+and loss values / head gradients within 1e-4.
 """
 import numpy as np
 import pytest
@@ -98,6 +100,12 @@ def test_model_n320_train_step_vs_reference(golden):
     assert abs(float(loss) - float(d["loss"][0])) / float(d["loss"][0]) < 1e-2
     assert rel(items, d["items"]) < 1e-2, (items.tolist(), d["items"].tolist())
     loss.backward()
+    # backbone gradients of this network are discontinuous in the activations (SPPF max-pool
+    # routing, oracle/precision.py): each gradient is held to 10%, or to 2x the distance of the
+    # oracle run under the HIP storage-rounding model from the fp32 reference, whichever is larger
+    from oracle import loss as ol
+    cpu_batch = {k: v.cpu() for k, v in batch.items() if k != "img"}
+    emu = _emulated_oracle_grads("n", torch.from_numpy(d["img"]), lambda h: ol.v8_loss(h, cpu_batch)[0])
     names = list(d["grad_names"])
     ref = dict(zip(names, d["grad_norm"]))
     bad = []
@@ -106,12 +114,14 @@ def test_model_n320_train_step_vs_reference(golden):
         if not p.requires_grad or ref[k] < 1e-6 * gmax:      # true gradient ~0 (BN-invariant biases)
             continue
         g = float(p.grad.norm())
-        if abs(g - ref[k]) > 0.1 * ref[k] + 1e-6:
+        tol = max(0.1, 2.0 * abs(float(emu[k].norm()) - ref[k]) / ref[k])
+        if abs(g - ref[k]) > tol * ref[k] + 1e-6:
             bad.append((k, g, ref[k]))
     assert len(bad) <= len(names) // 20, bad[:10]
     for k in [n for n in d.files if n.startswith("grad:")]:
         p = dict(m.named_parameters())[k[5:]]
-        assert rel(p.grad, d[k]) < 1e-1, (k, rel(p.grad, d[k]))
+        tol = max(1e-1, 2.0 * rel(emu[k[5:]], d[k]))
+        assert rel(p.grad, d[k]) < tol, (k, rel(p.grad, d[k]), tol)
     sd = m.state_dict()
     for k in [n for n in d.files if n.startswith("state:")]:
         assert rel(sd[k[6:]], d[k]) < 2e-2, (k, rel(sd[k[6:]], d[k]))
@@ -202,12 +212,26 @@ def test_sppf_pool_chain_exact():
     torch.testing.assert_close(cur.cpu().view(B, H, W, C), xr.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
 
 
+def _emulated_oracle_grads(scale, img, loss_fn):
+    """Parameter gradients of the CPU oracle under the HIP storage-rounding model."""
+    from oracle import model as om
+    from oracle.precision import hip_storage_rounding
+    layers, save, P = om.build(om.load_cfg(scale))
+    leaf = {k: v.requires_grad_(True) for k, v in P.items()
+            if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")}
+    with hip_storage_rounding():
+        out = om.forward(P, layers, save, torch.as_tensor(img), training=True)
+        loss_fn(out).backward() if callable(loss_fn) else torch.autograd.backward(out, loss_fn)
+    return {k: v.grad for k, v in leaf.items()}
+
+
 def test_network_backward_fixed_head_grads_vs_oracle():
     """Network backward: the same random head gradients through our plan and through CPU fp32
-    autograd of the oracle.  Gradients are bf16 and the error grows smoothly with backward depth
-    (measured: 2.7% at the first Detect convs, <= 9% at the stem, no block-level jump — every block
-    also passes its own 2e-2 check), so the per-parameter bound here is relative-L2 <= 1.2e-1;
-    near-zero true gradients are compared on the network's gradient scale."""
+    autograd of the oracle.  The backbone is discontinuous in its activations (SPPF max-pool
+    routing, oracle/precision.py), so each parameter's relative-L2 error is bounded by
+    max(3e-2, 2 x the error of the oracle under the HIP storage-rounding model: both round at
+    the same points but differ in accumulation order, so near-tie argmax flips land elsewhere); near-zero true
+    gradients are compared on the network's gradient scale."""
     from oracle import model as om
     from models import build_yolo11
     cfg = om.load_cfg("n")
@@ -225,14 +249,17 @@ def test_network_backward_fixed_head_grads_vs_oracle():
             if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")}
     ref = om.forward(Q, layers, save, img, training=True)
     torch.autograd.backward(ref, dh)
+    emu = _emulated_oracle_grads("n", img, dh)
     gmax = max(float(v.grad.norm()) for v in leaf.values())
     worst = []
     for k, p in m.named_parameters():
         if not p.requires_grad:
             continue
         r = leaf[k].grad
-        err = float((p.grad.cpu().double() - r.double()).norm())
-        bound = 1.2e-1 * max(float(r.norm()), 1e-4 * gmax)
-        worst.append((err / max(float(r.norm()), 1e-4 * gmax), k))
-        assert err < bound, (k, err, float(r.norm()))
-    print("worst rel", sorted(worst)[-3:])
+        scale = max(float(r.norm()), 1e-4 * gmax)
+        err = float((p.grad.cpu().double() - r.double()).norm()) / scale
+        err_emu = float((emu[k].double() - r.double()).norm()) / scale
+        bound = max(3e-2, 2.0 * err_emu)
+        worst.append((err / bound, k, err, err_emu))
+        assert err < bound, (k, err, err_emu)
+    print("worst err/bound", sorted(worst)[-3:])

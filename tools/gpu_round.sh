@@ -8,7 +8,10 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python3 -m pytest $R/tests -m gpu -q > $OUT/pytest_gpu.log 2>&1
-echo "pytest_gpu exit $?"; tail -3 $OUT/pytest_gpu.log
+rc=$?
+echo "pytest_gpu exit $rc"; tail -3 $OUT/pytest_gpu.log
+# 0 = pass, 1 = test failures; anything else (fault, abort, timeout) ends the GPU session here
+if [ $rc -gt 1 ]; then tail -30 $OUT/pytest_gpu.log; exit $rc; fi
 timeout -k 10 500 python3 $R/bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed $?"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \

@@ -35,12 +35,14 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
-// round-to-nearest-even f32 -> bf16 (NaN kept as a quiet NaN)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-    uint32_t u = __float_as_uint(f);
-    if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16_t)((u >> 16) | 0x40);
-    u += 0x7fffu + ((u >> 16) & 1u);
-    return (bf16_t)(u >> 16);
+// round-to-nearest-even f32 -> bf16 (v_cvt_pk_bf16_f32; NaN stays a quiet NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+// two floats -> packed bf16 pair (lo in bits 0..15): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pk2bf(float lo, float hi) {
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    typedef __bf16 b2_t __attribute__((ext_vector_type(2)));
+    f2_t v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b2_t));
 }
 
 // fp16 bits <-> f32 (pre-BatchNorm conv outputs are kept in fp16: 3 more mantissa bits than

@@ -36,7 +36,7 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
-constexpr int BK = 32;   // k per LDS stage = one MFMA k-step
+constexpr int BK = 64;   // k per LDS stage = two MFMA k-steps
 constexpr int NCH = BK / 8;
 
 struct GemmArgs {
@@ -51,16 +51,31 @@ struct GemmArgs {
     int64_t M;                               // N*OH*OW
     int mtiles;
     int out_f32, accumulate;
+    int N;                                   // images
+    int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
 };
 
-__device__ __forceinline__ int swz(int row, int c) { return row ^ (c << 2); }
+// LDS row slot of (row, chunk): row ^ g(c), g = {0,1,2,3,12,13,14,15}.  A staging write group
+// (8 lanes = one row, chunks 0..7) hits 8 distinct 16-B slots mod 16, and a ds_read_b128 lane
+// group (chunk 2j: rows {0-3,12-15}, chunk 2j+1: rows {4-11}, or the converse) stays a
+// permutation of the 16 slots because every g keeps bit2 == bit3.
+__device__ __forceinline__ int swz(int row, int c) { return row ^ (c + ((c & 4) << 1)); }
+
+constexpr uint32_t OOB = 0x80000000u;          // buffer offset past num_records: loads return 0
+constexpr int RSRC_FLAGS = 0x00020000;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                             int(bytes < 0x7fffffff ? bytes : 0x7fffffff), RSRC_FLAGS);
+}
 
 template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
+__global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
     constexpr int TM = BN / 32;          // 16-channel subtiles per wave
     constexpr int TN = BM / 32;          // 16-pixel subtiles per wave
-    constexpr int A_ITEMS = (BN * NCH + 255) / 256;
-    constexpr int B_ITEMS = (BM * NCH + 255) / 256;
+    constexpr int A_ITEMS = BN * NCH / 256;
+    constexpr int B_ITEMS = BM * NCH / 256;
+    static_assert(A_ITEMS >= 1 && B_ITEMS >= 1, "tile too small for the staging map");
     __shared__ uint4 As[2][NCH][BN];
     __shared__ uint4 Bs[2][NCH][BM];
     __shared__ float red[2][2][BN];      // [sum|sq][wave pixel half][channel]
@@ -68,11 +83,33 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int fc = lane >> 4, fr = lane & 15;
+    const int sc = tid & (NCH - 1);      // 16-B chunk this thread stages (fixed)
+    const int srow = tid / NCH;          // first staged row; item it adds 256/NCH*it
+    constexpr int RSTEP = 256 / NCH;
     const int n0 = blockIdx.y * BN;
     const int kc = (a.Kin + BK - 1) / BK;
-    const int nk = a.KH * a.KW * kc;
-    const int64_t OHW = int64_t(a.OH) * a.OW;
-    const int64_t wrow = int64_t(a.KH) * a.KW * a.Kin;
+    // output pixel mapping: oh = i*os + py, ow = j*os + px over a class grid OHc x OWc;
+    // for the stride-2 data gradient only the taps kh = kh0 + 2i, kw = kw0 + 2j reach whole pixels
+    const int os = a.ostep;
+    const int py = os == 2 ? int(blockIdx.z >> 1) : 0, px = os == 2 ? int(blockIdx.z & 1) : 0;
+    const int OHc = (a.OH - py + os - 1) / os, OWc = (a.OW - px + os - 1) / os;
+    const int kh0 = os == 2 ? ((py + a.pad) & 1) : 0, kw0 = os == 2 ? ((px + a.pad) & 1) : 0;
+    const int nkw = (a.KW - kw0 + os - 1) / os;
+    const int ntap = ((a.KH - kh0 + os - 1) / os) * nkw;
+    const int nk = ntap * kc;
+    const uint32_t OHW = uint32_t(OHc) * uint32_t(OWc);
+    const int64_t Mc = int64_t(a.N) * OHW;
+    const int mtiles = int((Mc + BM - 1) / BM);
+    const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
+    const uint32_t xld_b = uint32_t(a.x_ld) * 2u;
+
+    const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
+    uint32_t a_off[A_ITEMS];
+#pragma unroll
+    for (int it = 0; it < A_ITEMS; ++it) {
+        const int ch = n0 + srow + RSTEP * it;
+        a_off[it] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t(sc) * 16u : OOB;
+    }
 
     float ssum[TM][4], ssq[TM][4];
 #pragma unroll
@@ -80,79 +117,74 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
 
-    for (int mt = blockIdx.x; mt < a.mtiles; mt += gridDim.x) {
+    // m-tiles grouped per XCD (workgroups go to XCDs round-robin by linear id; gridDim.x % 8 == 0):
+    // neighbouring tiles share input halo rows in that XCD's L2
+    const int xcd = blockIdx.x & 7, lstride = gridDim.x >> 3;
+    const int per_xcd = (mtiles + 7) >> 3;
+    const int mt_end = min((xcd + 1) * per_xcd, mtiles);
+    for (int mt = xcd * per_xcd + (blockIdx.x >> 3); mt < mt_end; mt += lstride) {
         const int64_t m0 = int64_t(mt) * BM;
-        // per-item pixel decomposition of the B tile rows this thread stages
-        int64_t b_img[B_ITEMS];
+        const uint32_t nfirst = uint32_t(m0 / OHW);
+        const __amdgpu_buffer_rsrc_t xres =
+            make_rsrc(a.x + int64_t(nfirst) * a.x_bs, (int64_t(a.N) - nfirst) * a.x_bs * 2);
         int b_oh[B_ITEMS], b_ow[B_ITEMS];
-        bool b_ok[B_ITEMS];
+        uint32_t b_img[B_ITEMS], b_off[B_ITEMS];
 #pragma unroll
         for (int it = 0; it < B_ITEMS; ++it) {
-            int id = tid + it * 256;
-            int row = id / NCH;
-            int64_t m = m0 + row;
-            b_ok[it] = (id < BM * NCH) && (m < a.M);
-            const uint32_t um = b_ok[it] ? uint32_t(m) : 0u;
-            const uint32_t n = um / uint32_t(OHW), pix = um - n * uint32_t(OHW);
-            b_img[it] = int64_t(n) * a.x_bs;
-            b_oh[it] = int(pix / uint32_t(a.OW));
-            b_ow[it] = int(pix - uint32_t(b_oh[it]) * uint32_t(a.OW));
+            const int64_t m = m0 + srow + RSTEP * it;
+            const uint32_t um = m < Mc ? uint32_t(m) : 0u;
+            const uint32_t n = um / OHW, pix = um - n * OHW;
+            const uint32_t i = pix / uint32_t(OWc);
+            b_img[it] = m < Mc ? (n - nfirst) * uint32_t(a.x_bs) * 2u + uint32_t(sc) * 16u : OOB;
+            b_oh[it] = int(i) * os + py;
+            b_ow[it] = int(pix - i * uint32_t(OWc)) * os + px;
         }
-        uint4 ra[A_ITEMS], rb[B_ITEMS];
-        auto load = [&](int k) {
-            const int tap = k / kc, k0 = (k - tap * kc) * BK;
-            const int kh = tap / a.KW, kw = tap - kh * a.KW;
-#pragma unroll
-            for (int it = 0; it < A_ITEMS; ++it) {
-                int id = tid + it * 256;
-                int row = id / NCH, c = id % NCH;
-                int ch = n0 + row, kk = k0 + 8 * c;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (id < BN * NCH && ch < a.Nout && kk < a.Kin)
-                    v = *reinterpret_cast<const uint4*>(a.w + int64_t(ch) * wrow + int64_t(tap) * a.Kin + kk);
-                ra[it] = v;
-            }
+        auto tap_setup = [&](int t) {
+            const int ti = t / nkw;
+            const int kh = kh0 + ti * os, kw = kw0 + (t - ti * nkw) * os;
 #pragma unroll
             for (int it = 0; it < B_ITEMS; ++it) {
-                int id = tid + it * 256;
-                int c = id % NCH, kk = k0 + 8 * c;
-                uint4 v = make_uint4(0, 0, 0, 0);
-                if (b_ok[it] && kk < a.Kin) {
-                    int gh, gw;
-                    bool ok;
-                    if (MODE == MODE_FWD) {
-                        gh = b_oh[it] * a.stride - a.pad + kh;
-                        gw = b_ow[it] * a.stride - a.pad + kw;
-                        ok = gh >= 0 && gh < a.GH && gw >= 0 && gw < a.GW;
-                    } else {
-                        int th = b_oh[it] + a.pad - kh, tw = b_ow[it] + a.pad - kw;
-                        ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
-                        gh = th / a.stride;
-                        gw = tw / a.stride;
-                        ok = ok && gh < a.GH && gw < a.GW;
-                    }
-                    if (ok)
-                        v = *reinterpret_cast<const uint4*>(a.x + b_img[it] + (int64_t(gh) * a.GW + gw) * a.x_ld + kk);
+                int gh, gw;
+                if (MODE == MODE_FWD) {
+                    gh = b_oh[it] * a.stride - a.pad + kh;
+                    gw = b_ow[it] * a.stride - a.pad + kw;
+                } else {                       // th, tw are multiples of the stride here
+                    gh = (b_oh[it] + a.pad - kh) >> (a.stride - 1);
+                    gw = (b_ow[it] + a.pad - kw) >> (a.stride - 1);
                 }
-                rb[it] = v;
+                const bool ok = b_img[it] != OOB && gh >= 0 && gh < a.GH && gw >= 0 && gw < a.GW;
+                b_off[it] = ok ? b_img[it] + uint32_t(gh * a.GW + gw) * xld_b : OOB;
             }
+            return uint32_t((kh * a.KW + kw) * a.Kin) * 2u;
+        };
+        uint4 ra[A_ITEMS], rb[B_ITEMS];
+        int t_next = 0, c_next = 0;
+        uint32_t a_tap = 0;
+        auto load = [&]() {
+            if (c_next == 0) a_tap = tap_setup(t_next);
+            const int k0 = c_next * BK;
+            const bool in_k = k0 + 8 * sc < a.Kin;
+            const uint32_t kb = uint32_t(k0) * 2u;
+#pragma unroll
+            for (int it = 0; it < A_ITEMS; ++it)
+                ra[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       wres, in_k && a_off[it] != OOB ? a_off[it] + a_tap + kb : OOB, 0, 0));
+#pragma unroll
+            for (int it = 0; it < B_ITEMS; ++it)
+                rb[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       xres, in_k && b_off[it] != OOB ? b_off[it] + kb : OOB, 0, 0));
+            if (++c_next == kc) { c_next = 0; ++t_next; }
         };
         auto store = [&](int buf) {
 #pragma unroll
             for (int it = 0; it < A_ITEMS; ++it) {
-                int id = tid + it * 256;
-                if (id < BN * NCH) {
-                    int row = id / NCH, c = id % NCH;
-                    As[buf][c][swz(row, c)] = ra[it];
-                }
+                const int row = srow + RSTEP * it;
+                As[buf][sc][swz(row, sc)] = ra[it];
             }
 #pragma unroll
             for (int it = 0; it < B_ITEMS; ++it) {
-                int id = tid + it * 256;
-                if (id < BM * NCH) {
-                    int row = id / NCH, c = id % NCH;
-                    Bs[buf][c][swz(row, c)] = rb[it];
-                }
+                const int row = srow + RSTEP * it;
+                Bs[buf][sc][swz(row, sc)] = rb[it];
             }
         };
 
@@ -162,35 +194,36 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-        load(0);
+        // nk == 0: a parity class no tap reaches (1x1 stride-2): zero gradient
+        if (nk > 0) load();
         __syncthreads();     // previous tile's readers are done with both buffers
-        store(0);
+        if (nk > 0) store(0);
         __syncthreads();
         for (int k = 0; k < nk; ++k) {
             const int buf = k & 1;
-            if (k + 1 < nk) load(k + 1);
-            bf16x8 af[TM], bfr[TN];
+            if (k + 1 < nk) load();
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                int row = wr * (BN / 2) + i * 16 + fr;
-                af[i] = __builtin_bit_cast(bf16x8, As[buf][fc][swz(row, fc)]);
+            for (int kk = 0; kk < BK / 32; ++kk) {
+                const int cch = kk * 4 + fc;
+                bf16x8 af[TM], bfr[TN];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    af[i] = __builtin_bit_cast(bf16x8, As[buf][cch][swz(wr * (BN / 2) + i * 16 + fr, cch)]);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    bfr[j] = __builtin_bit_cast(bf16x8, Bs[buf][cch][swz(wc * (BM / 2) + j * 16 + fr, cch)]);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) {
+                        if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
+                                                                               __builtin_bit_cast(f16x8, bfr[j]),
+                                                                               acc[i][j], 0, 0, 0);
+                        else                              // bf16 gradients x bf16 weights
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                    }
             }
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                int row = wc * (BM / 2) + j * 16 + fr;
-                bfr[j] = __builtin_bit_cast(bf16x8, Bs[buf][fc][swz(row, fc)]);
-            }
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
-                                                                           __builtin_bit_cast(f16x8, bfr[j]),
-                                                                           acc[i][j], 0, 0, 0);
-                    else                              // bf16 gradients x bf16 weights
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-                }
             if (k + 1 < nk) store(buf ^ 1);
             __syncthreads();
         }
@@ -199,9 +232,11 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             const int64_t m = m0 + wc * (BM / 2) + j * 16 + fr;
-            if (m >= a.M) continue;
-            const uint32_t n = uint32_t(m) / uint32_t(OHW), pix = uint32_t(m) - n * uint32_t(OHW);
-            const int64_t obase = int64_t(n) * a.y_bs + int64_t(pix) * a.y_ld;
+            if (m >= Mc) continue;
+            const uint32_t n = uint32_t(m) / OHW, pix = uint32_t(m) - n * OHW;
+            const uint32_t ci_ = pix / uint32_t(OWc);
+            const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(pix - ci_ * uint32_t(OWc)) * os + px;
+            const int64_t obase = int64_t(n) * a.y_bs + opix * a.y_ld;
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int cb = n0 + wr * (BN / 2) + i * 16 + fc * 4;
@@ -242,8 +277,8 @@ __global__ void __launch_bounds__(256) conv_gemm_kernel(GemmArgs a) {
                             v[2] += bf2f(bf16_t(o.y & 0xffff)); v[3] += bf2f(bf16_t(o.y >> 16));
                         }
                         uint2 o;
-                        o.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
-                        o.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+                        o.x = pk2bf(v[0], v[1]);
+                        o.y = pk2bf(v[2], v[3]);
                         *reinterpret_cast<uint2*>(yp) = o;
                     } else {
 #pragma unroll
@@ -295,69 +330,80 @@ struct WgradArgs {
     int ci_tiles;
 };
 
-constexpr int WG_T = 64;                      // tile: 64 co x 64 ci
-constexpr int WG_RS = WG_T * 2 + 32;          // LDS row stride in bytes (bank-conflict-free tr reads)
-
+// tile: T co x T ci, 32 pixels per k-step; LDS rows padded by 32 B so the 8 rows a 32-lane half
+// reads with ds_read_b64_tr_b16 start on 8 distinct 8-bank groups (conflict-free)
+template <int T>
 __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
-    __shared__ __attribute__((aligned(16))) char As[2][32 * WG_RS];   // dz rows (pixels) x 64 co
-    __shared__ __attribute__((aligned(16))) char Bs[2][32 * WG_RS];   // x rows (pixels) x 64 ci
+    constexpr int RS = T * 2 + 32;                 // LDS row stride (bytes)
+    constexpr int CPR = T / 8;                     // 16-B chunks per row
+    constexpr int ITEMS = 32 * CPR / 256;          // staging chunks per thread per operand
+    constexpr int TS = T / 32;                     // 16-wide subtiles per wave (per dim)
+    __shared__ __attribute__((aligned(16))) char As[2][32 * RS];   // dz rows (pixels) x T co
+    __shared__ __attribute__((aligned(16))) char Bs[2][32 * RS];   // x rows (pixels) x T ci
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int co0 = blockIdx.x * WG_T;
+    const int co0 = blockIdx.x * T;
     const int tap = blockIdx.y / a.ci_tiles;
-    const int ci0 = (blockIdx.y - tap * a.ci_tiles) * WG_T;
+    const int ci0 = (blockIdx.y - tap * a.ci_tiles) * T;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
     const int64_t p_begin = int64_t(blockIdx.z) * a.chunk;
     const int64_t p_end = min(a.M, p_begin + a.chunk);
     if (p_begin >= p_end) return;
     const int64_t OHW = int64_t(a.OH) * a.OW;
-    const int srow = tid >> 3, sc = tid & 7;      // staging: one 16-B chunk per thread per tile
 
-    f32x4 acc[2][2];
+    f32x4 acc[TS][TS];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TS; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TS; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 ra, rb;
+    uint4 ra[ITEMS], rb[ITEMS];
     const uint32_t uOHW = uint32_t(OHW), uOW = uint32_t(a.OW);
     auto load = [&](int64_t p0) {
-        int64_t p = p0 + srow;
-        ra = make_uint4(0, 0, 0, 0);
-        rb = make_uint4(0, 0, 0, 0);
-        if (p < p_end) {
-            const uint32_t up = uint32_t(p);                  // M < 2^31 (checked on the host)
-            const uint32_t n = up / uOHW, pix = up - n * uOHW;
-            const int oh = int(pix / uOW), ow = int(pix - uint32_t(oh) * uOW);
-            int co = co0 + sc * 8;
-            if (co < a.Cout) ra = *reinterpret_cast<const uint4*>(a.dz + int64_t(n) * a.dz_bs + int64_t(pix) * a.dz_ld + co);
-            int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-            int ci = ci0 + sc * 8;
-            if (ci < a.Cin && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW) {
-                uint4 h = *reinterpret_cast<const uint4*>(a.x + int64_t(n) * a.x_bs + (int64_t(ih) * a.IW + iw) * a.x_ld + ci);
-                uint32_t w4[4] = {h.x, h.y, h.z, h.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e)   // fp16 activation -> bf16 MFMA operand
-                    w4[e] = uint32_t(f2bf(h2f(uint16_t(w4[e] & 0xffff)))) | (uint32_t(f2bf(h2f(uint16_t(w4[e] >> 16)))) << 16);
-                rb = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+        for (int it = 0; it < ITEMS; ++it) {
+            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
+            int64_t p = p0 + srow;
+            ra[it] = make_uint4(0, 0, 0, 0);
+            rb[it] = make_uint4(0, 0, 0, 0);
+            if (p < p_end) {
+                const uint32_t up = uint32_t(p);                  // M < 2^31 (checked on the host)
+                const uint32_t n = up / uOHW, pix = up - n * uOHW;
+                const int oh = int(pix / uOW), ow = int(pix - uint32_t(oh) * uOW);
+                int co = co0 + sc * 8;
+                if (co < a.Cout)
+                    ra[it] = *reinterpret_cast<const uint4*>(a.dz + int64_t(n) * a.dz_bs + int64_t(pix) * a.dz_ld + co);
+                int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                int ci = ci0 + sc * 8;
+                if (ci < a.Cin && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW) {
+                    uint4 h = *reinterpret_cast<const uint4*>(a.x + int64_t(n) * a.x_bs + (int64_t(ih) * a.IW + iw) * a.x_ld + ci);
+                    uint32_t w4[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)   // fp16 activation -> bf16 MFMA operand
+                        w4[e] = uint32_t(f2bf(h2f(uint16_t(w4[e] & 0xffff)))) |
+                                (uint32_t(f2bf(h2f(uint16_t(w4[e] >> 16)))) << 16);
+                    rb[it] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                }
             }
         }
     };
     auto store = [&](int buf) {
-        *reinterpret_cast<uint4*>(&As[buf][srow * WG_RS + sc * 16]) = ra;
-        *reinterpret_cast<uint4*>(&Bs[buf][srow * WG_RS + sc * 16]) = rb;
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
+            *reinterpret_cast<uint4*>(&As[buf][srow * RS + sc * 16]) = ra[it];
+            *reinterpret_cast<uint4*>(&Bs[buf][srow * RS + sc * 16]) = rb[it];
+        }
     };
 
     // transposed fragment read: group g = lane>>4 owns k rows {4g..4g+3} and {16+4g..16+4g+3};
     // lane 4q+p of the group addresses row (4g+q [+16]), columns col0 + 4p .. +3
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     auto frag = [&](const char* base, int col0) -> bf16x8 {
-        const char* p1 = base + (4 * g + q) * WG_RS + (col0 + 4 * pp) * 2;
-        const char* p2 = p1 + 16 * WG_RS;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4*)(p1));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (__attribute__((address_space(3))) s16x4*)(p2));
+        const char* p1 = base + (4 * g + q) * RS + (col0 + 4 * pp) * 2;
+        const char* p2 = p1 + 16 * RS;
+        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p2));
         typedef short s16x8 __attribute__((ext_vector_type(8)));
         s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, v);
@@ -370,15 +416,16 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
     for (int64_t p0 = p_begin; p0 < p_end; p0 += 32) {
         const bool more = p0 + 32 < p_end;
         if (more) load(p0 + 32);
-        bf16x8 af[2], bf[2];
+        bf16x8 af[TS], bf[TS];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = frag(As[buf], wr * 32 + i * 16);
+        for (int i = 0; i < TS; ++i) af[i] = frag(As[buf], wr * (T / 2) + i * 16);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = frag(Bs[buf], wc * 32 + j * 16);
+        for (int j = 0; j < TS; ++j) bf[j] = frag(Bs[buf], wc * (T / 2) + j * 16);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TS; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TS; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
         if (more) store(buf ^ 1);
         __syncthreads();
         buf ^= 1;
@@ -386,14 +433,14 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
     // D[co][ci]: lane holds co rows (lane>>4)*4 + r, ci column lane&15
     const int64_t trow = int64_t(a.KH) * a.KW * a.Cin;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TS; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            int ci = ci0 + wc * 32 + j * 16 + (lane & 15);
+        for (int j = 0; j < TS; ++j) {
+            int ci = ci0 + wc * (T / 2) + j * 16 + (lane & 15);
             if (ci >= a.Cin) continue;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                int co = co0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+                int co = co0 + wr * (T / 2) + i * 16 + (lane >> 4) * 4 + r;
                 if (co < a.Cout) atomicAdd(a.dw + co * trow + int64_t(tap) * a.Cin + ci, acc[i][j][r]);
             }
         }
@@ -604,18 +651,29 @@ __global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int 
     if (t.dst_t) t.dst_t[(int64_t(ci) * T + tap) * t.cout_t + co] = f2bf(v);     // bf16 (dgrad operand)
 }
 
+// grid x: a multiple of 8 (the kernel groups m-tiles per XCD); with BatchNorm statistics the
+// partials are one row per grid-x block, so the grid is bounded and blocks loop over tiles
+static int grid_x(int mtiles, int ntiles, bool stats, int max_blocks) {
+    int gx = (mtiles + 7) & ~7;
+    if (stats) gx = std::min(gx, std::max(8, (max_blocks / ntiles) & ~7));
+    return gx;
+}
+
+// the kernel's buffer offsets are 32-bit, relative to the first image of a tile
+static bool offsets_fit(int64_t bs, int64_t class_pixels) {
+    const int64_t images = 128 / std::max<int64_t>(class_pixels, 1) + 2;
+    return bs * 2 * images < (int64_t(1) << 31);
+}
+
 template <int BM, int BN, int MODE>
 int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     GemmArgs a = a0;
-    a.mtiles = int((a.M + BM - 1) / BM);
+    const int os = a.ostep;
+    const int64_t Mc = int64_t(a.N) * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);   // largest class
+    a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
-    int gx = a.mtiles;
-    if (a.st_sum) {
-        // stats partials are per grid-x block: bound the grid, keep it a multiple of 8 (XCD grouping)
-        int cap = max(8, (max_blocks / ntiles) & ~7);
-        gx = min(gx, cap);
-    }
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE>), dim3(gx, ntiles), dim3(256), 0, st, a);
+    int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1), dim3(256), 0, st, a);
     return gx;
 }
 
@@ -641,14 +699,14 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     int BN = Cout >= 128 ? 128 : (Cout >= 64 ? 64 : 32);
     int ntiles = (Cout + BN - 1) / BN;
     int mtiles = int((M + 127) / 128);
-    int cap = std::max(8, (2048 / ntiles) & ~7);
-    return std::min(mtiles, cap);
+    return grid_x(mtiles, ntiles, true, 2048);
 }
 
 extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                            float* stat_sum, float* stat_sq, void* stream) {
     YM_CHECK_ARG(d && x && w && y, "ym_conv_fwd: null argument");
     YM_CHECK_ARG(d->cin % 8 == 0, "ym_conv_fwd: Cin %% 8 != 0 (Cin=%d)", d->cin);
+    YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_fwd: kernel size %d unsupported (1..3)", d->k);
     YM_CHECK_ARG(d->x_ld % 8 == 0 && d->x_bs % 8 == 0, "ym_conv_fwd: input view not 16-byte aligned");
     YM_CHECK_ARG(d->out_f32 == 1 || (d->y_ld % 4 == 0 && d->y_bs % 4 == 0), "ym_conv_fwd: output view not 8-byte aligned");
     YM_CHECK_ARG((stat_sum == nullptr) == (stat_sq == nullptr), "ym_conv_fwd: stats pointers");
@@ -662,8 +720,11 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
     a.M = int64_t(d->n) * d->oh * d->ow;
     a.out_f32 = d->out_f32; a.accumulate = d->accumulate;
+    a.N = d->n;
+    a.ostep = 1;
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
+    YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
     pick_and_launch(a, MODE_FWD, 2048, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
@@ -684,8 +745,15 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
     a.M = int64_t(d->n) * d->h * d->w;
     a.accumulate = d->accumulate;
+    a.N = d->n;
+    // stride-2: one launch over the 4 output parity classes, each with only its valid taps
+    YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_dgrad: kernel size %d unsupported (1..3)", d->k);
+    YM_CHECK_ARG(d->stride == 1 || d->stride == 2, "ym_conv_dgrad: stride %d unsupported (1, 2)", d->stride);
+    a.ostep = d->stride;
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
+    YM_CHECK_ARG(offsets_fit(d->y_bs, int64_t(d->h / d->stride) * (d->w / d->stride)),
+                 "ym_conv_dgrad: gradient image stride too large");
     pick_and_launch(a, MODE_DGRAD, 4096, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_dgrad");
     return YM_OK;
@@ -706,15 +774,20 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     a.M = int64_t(d->n) * d->oh * d->ow;
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_wgrad: too many pixels");
-    int co_t = (a.Cout + WG_T - 1) / WG_T;
-    a.ci_tiles = (a.Cin + WG_T - 1) / WG_T;
+    // 128x128 tiles when both channel counts fill them, else 64x64
+    const int T = (a.Cout >= 128 && a.Cin >= 128) ? 128 : 64;
+    int co_t = (a.Cout + T - 1) / T;
+    a.ci_tiles = (a.Cin + T - 1) / T;
     int cols = a.ci_tiles * a.KH * a.KW;
     int64_t steps = (a.M + 31) / 32;
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(2048 / (co_t * cols), steps / 8));
     splits = std::min<int64_t>(splits, 65535);
     a.chunk = ((steps + splits - 1) / splits) * 32;
     splits = (a.M + a.chunk - 1) / a.chunk;
-    hipLaunchKernelGGL(wgrad_kernel, dim3(co_t, cols, unsigned(splits)), dim3(256), 0, as_stream(stream), a);
+    if (T == 128)
+        hipLaunchKernelGGL(wgrad_kernel<128>, dim3(co_t, cols, unsigned(splits)), dim3(256), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL(wgrad_kernel<64>, dim3(co_t, cols, unsigned(splits)), dim3(256), 0, as_stream(stream), a);
     YM_LAUNCH_CHECK("ym_conv_wgrad");
     return YM_OK;
 }
