@@ -99,3 +99,20 @@ def test_assigner_and_loss_oracle(golden):
     le.backward()
     for i in range(3):
         torch.testing.assert_close(fe[i].grad, torch.from_numpy(d[f"empty_dfeat{i}"]), rtol=1e-5, atol=1e-7)
+
+
+def test_precision_model_restores_and_rounds():
+    """oracle/precision.py: rounding applies only inside the context and stays close to fp32."""
+    from oracle.precision import hip_storage_rounding
+    layers, save, P = om.build(om.load_cfg("n"))
+    x = torch.rand(2, 1, 160, 160, generator=torch.Generator().manual_seed(0))
+    conv0 = om.conv
+    with torch.no_grad():
+        ref = om.forward({k: v.clone() for k, v in P.items()}, layers, save, x, training=True)
+        with hip_storage_rounding():
+            assert om.conv is not conv0
+            emu = om.forward({k: v.clone() for k, v in P.items()}, layers, save, x, training=True)
+    assert om.conv is conv0
+    for r, e in zip(ref, emu):
+        err = float((r - e).norm() / r.norm())
+        assert 0 < err < 2e-2

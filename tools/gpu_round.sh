@@ -12,6 +12,8 @@ rc=$?
 echo "pytest_gpu exit $rc"; tail -3 $OUT/pytest_gpu.log
 # 0 = pass, 1 = test failures; anything else (fault, abort, timeout) ends the GPU session here
 if [ $rc -gt 1 ]; then tail -30 $OUT/pytest_gpu.log; exit $rc; fi
+timeout -k 10 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo "smoke failed $?"; tail -20 $OUT/smoke.log; exit 1; }
+tail -2 $OUT/smoke.log
 timeout -k 10 500 python3 $R/bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed $?"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
