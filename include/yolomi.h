@@ -105,10 +105,13 @@ int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, voi
                 float* stat_sum, float* stat_sq, void* stream);
 /* dx (+)= conv_transpose(dz, w) using the [cin][kh][kw][cout] weight copy. */
 int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream);
-/* dw_ohwi[cout][k*k][cin] += sum over pixels (fp32 atomics; caller zeroes). */
-int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, float* dw_ohwi, void* stream);
-/* [cout][taps][cin] -> [cout][cin][taps] (PyTorch OIHW grad layout). */
-int ym_wgrad_to_oihw(const float* src, float* dst, int cout, int cin, int taps, int accumulate, void* stream);
+/* Weight gradient dW (fp32 OIHW) = sum over output pixels of dz (x) x, overwriting dw_oihw or adding
+ * into it (accumulate = 1).  The K (pixel) axis is split over workgroups; the fp32 partials go to
+ * `workspace` (ym_conv_wgrad_workspace_size bytes) and are reduced by the library: no atomics
+ * into, and no zero-fill of, dw_oihw.  dz bf16 with the y_* view, x fp16 with the x_* view. */
+size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d);
+int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, void* workspace,
+                  size_t workspace_bytes, float* dw_oihw, int accumulate, void* stream);
 /* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0). */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
@@ -121,7 +124,7 @@ int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gst
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
                  int c, int accumulate, void* stream);
-/* All conv weights fp32 OIHW -> bf16 fwd / dgrad layouts in one launch (table in device memory). */
+/* All conv weights fp32 OIHW -> fp16 forward / bf16 dgrad layouts in one launch (table in device memory). */
 int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream);
 
 /* ------------------------------------------------------------------ BatchNorm2d (train) + SiLU

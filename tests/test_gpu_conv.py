@@ -5,7 +5,9 @@ weights, bf16 gradients and dgrad weights), so the reference differs from the ke
 by fp32 accumulation order and the output rounding:
   fwd  fp32 out: rel 1e-3 of max|y|
   dgrad bf16 out: rel 1e-2 of max|dx| (one bf16 rounding = 2^-8)
-  wgrad fp32 out: rel 1e-3 of max|dw| (x is converted fp16 -> bf16 at staging, mirrored here)
+  wgrad fp32 out: rel 1e-3 of max|dw| (x is converted fp16 -> bf16 at staging, mirrored here),
+    OIHW, overwrite and accumulate; the 3x3 (all taps per block), 1x1 (flat pixels) and generic
+    (here: 1x1 stride 2) kernels are all covered
 Shapes cover odd spatial sizes, both strides, k = 1 and 3, channel counts that are not
 multiples of the tile sizes, and the 4-parity-class stride-2 dgrad (a 1x1 stride-2 conv
 leaves three of the classes with no tap: their gradient must be exactly zero).
@@ -27,6 +29,8 @@ SHAPES = [
     (1, 6, 6, 16, 24, 1, 1, 0),
     (3, 20, 20, 256, 128, 3, 2, 1),
     (1, 5, 7, 520, 264, 3, 1, 1),
+    (2, 9, 9, 256, 136, 1, 1, 0),
+    (2, 33, 17, 64, 64, 3, 1, 1),
 ]
 
 
@@ -70,12 +74,17 @@ def test_conv_kernels_vs_torch(shape):
     call("ym_conv_dgrad", ctypes.byref(d), dzd.data_ptr(), w_t.data_ptr(), dx.data_ptr(), st)
     dz_nchw = dz.float().permute(0, 3, 1, 2)
     dx_ref = torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz_nchw, stride=s, padding=p).permute(0, 2, 3, 1)
-    # wgrad into [cout][taps][cin] fp32
-    dw = torch.zeros(cout, k * k, cin, dtype=torch.float32, device=dev)
-    call("ym_conv_wgrad", ctypes.byref(d), dzd.data_ptr(), xd.data_ptr(), dw.data_ptr(), st)
+    # wgrad: OIHW fp32, split-K partials in the workspace; then accumulate=1 adds a second copy
+    from yolomi._lib import lib
+    ws = torch.empty(max(lib().ym_conv_wgrad_workspace_size(ctypes.byref(d)) // 4, 1), dtype=torch.float32, device=dev)
+    dw = torch.full((cout, cin, k, k), float("nan"), dtype=torch.float32, device=dev)
+    call("ym_conv_wgrad", ctypes.byref(d), dzd.data_ptr(), xd.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+         dw.data_ptr(), 0, st)
+    dw2 = dw.clone()
+    call("ym_conv_wgrad", ctypes.byref(d), dzd.data_ptr(), xd.data_ptr(), ws.data_ptr(), ws.numel() * 4,
+         dw2.data_ptr(), 1, st)
     dw_ref = torch.nn.grad.conv2d_weight(x.bfloat16().float().permute(0, 3, 1, 2), (cout, cin, k, k), dz_nchw,
                                          stride=s, padding=p)
-    dw_ref = dw_ref.permute(0, 2, 3, 1).reshape(cout, k * k, cin)
     torch.cuda.synchronize()
 
     def rel(a, b):
@@ -85,6 +94,7 @@ def test_conv_kernels_vs_torch(shape):
     assert torch.isfinite(dx.float()).all()
     assert rel(dx, dx_ref) < 1e-2
     assert rel(dw, dw_ref) < 1e-3
+    assert rel(dw2, 2 * dw_ref) < 1e-3
     if k == 1 and s == 2:
         # pixels at odd rows or odd columns receive no tap
         dxc = dx.float().cpu()

@@ -1,6 +1,6 @@
 // NHWC convolutions on CDNA4 MFMA, fp32 accumulate: forward fp16 x fp16
-// (v_mfma_f32_16x16x32_f16; activations are fp16), data/weight gradients bf16
-// (v_mfma_f32_16x16x32_bf16; gradients are bf16, activations converted while staging).
+// (v_mfma_f32_16x16x32_f16; activations are fp16), data gradients bf16
+// (v_mfma_f32_16x16x32_bf16; gradients are bf16).
 //
 // Replaces the reference's nn.Conv2d calls (and their autograd) inside
 // Conv / Bottleneck / C2f / C3k / SPPF / PSA / Detect
@@ -8,31 +8,29 @@
 //
 // conv_gemm_kernel<MODE>  implicit GEMM, one kernel for forward (MODE_FWD) and
 //   data-gradient (MODE_DGRAD).  GEMM rows = output pixels, cols = output
-//   channels, K = taps x input channels.  Tiles BM pixels x BN channels x 32,
-//   256 threads = 2x2 waves, register-staged double-buffered LDS.  LDS tiles
-//   are stored chunk-major ([k-chunk of 8][row] x 16 B) with the row index
-//   XOR-swizzled by 4*chunk, so both the 16-B fragment reads (one per lane per
-//   MFMA operand) and the 16-B staging writes are bank-conflict free.
+//   channels, K = taps x input channels.  Tiles BM pixels x BN channels x 64,
+//   256 threads = 2x2 waves, register-staged double-buffered LDS, operands
+//   fetched with raw buffer loads (out-of-image taps and channel tails read as
+//   zero through an out-of-range offset, no branches).  LDS tiles are stored
+//   chunk-major ([k-chunk of 8][row] x 16 B) with swizzled rows (swz below) so
+//   the 16-B fragment reads and the 16-B staging writes are conflict free.
+//   The K loop runs tap-major: per-row source offsets are set up once per tap.
+//   m-tiles are grouped per XCD.  The stride-2 data gradient runs as four
+//   output-parity classes (blockIdx.z), each with only the taps that land.
 //   Epilogue: optional bias, bf16 or fp32 store into a strided NHWC view
 //   (concat slices are free), optional accumulate (grad fan-in), and per-block
 //   per-channel sum / sum-of-squares partials for training-mode BatchNorm.
-// wgrad_kernel  dW[co][tap][ci] = sum_p dz[p][co] * x[src(p,tap)][ci]: K =
-//   pixels, staged row-major and read TRANSPOSED with ds_read_b64_tr_b16 so the
-//   pixel (reduction) axis lands in each lane's fragment; split-K over pixels
-//   with fp32 atomics.
+// (weight gradients: wgrad.hip)
 // conv_first_*  Cin = 1 stem (K = 9): direct fp32 VALU kernels.
 // dw3x3_*       depthwise 3x3 (Attention.pe, yolo11_modules.py:122): direct.
 #include <algorithm>
 
 #include "common.h"
+#include "tile.h"
 
 namespace ym {
 namespace {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
@@ -60,14 +58,6 @@ struct GemmArgs {
 // group (chunk 2j: rows {0-3,12-15}, chunk 2j+1: rows {4-11}, or the converse) stays a
 // permutation of the 16 slots because every g keeps bit2 == bit3.
 __device__ __forceinline__ int swz(int row, int c) { return row ^ (c + ((c & 4) << 1)); }
-
-constexpr uint32_t OOB = 0x80000000u;          // buffer offset past num_records: loads return 0
-constexpr int RSRC_FLAGS = 0x00020000;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, int64_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
-                                             int(bytes < 0x7fffffff ? bytes : 0x7fffffff), RSRC_FLAGS);
-}
 
 template <int BM, int BN, int MODE>
 __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
@@ -317,147 +307,6 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
             }
         }
     }
-}
-
-// ------------------------------------------------------------------ wgrad
-struct WgradArgs {
-    const bf16_t* dz; int64_t dz_bs, dz_ld;  // (N, OH, OW, Cout) view
-    const bf16_t* x; int64_t x_bs, x_ld;     // (N, IH, IW, Cin) view
-    float* dw;                               // [Cout][KH*KW][Cin] fp32, accumulated atomically
-    int IH, IW, Cin, OH, OW, Cout, KH, KW, stride, pad;
-    int64_t M;                               // N*OH*OW
-    int64_t chunk;                           // pixels per split (multiple of 32)
-    int ci_tiles;
-};
-
-// tile: T co x T ci, 32 pixels per k-step; LDS rows padded by 32 B so the 8 rows a 32-lane half
-// reads with ds_read_b64_tr_b16 start on 8 distinct 8-bank groups (conflict-free)
-template <int T>
-__global__ void __launch_bounds__(256) wgrad_kernel(WgradArgs a) {
-    constexpr int RS = T * 2 + 32;                 // LDS row stride (bytes)
-    constexpr int CPR = T / 8;                     // 16-B chunks per row
-    constexpr int ITEMS = 32 * CPR / 256;          // staging chunks per thread per operand
-    constexpr int TS = T / 32;                     // 16-wide subtiles per wave (per dim)
-    __shared__ __attribute__((aligned(16))) char As[2][32 * RS];   // dz rows (pixels) x T co
-    __shared__ __attribute__((aligned(16))) char Bs[2][32 * RS];   // x rows (pixels) x T ci
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
-    const int co0 = blockIdx.x * T;
-    const int tap = blockIdx.y / a.ci_tiles;
-    const int ci0 = (blockIdx.y - tap * a.ci_tiles) * T;
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const int64_t p_begin = int64_t(blockIdx.z) * a.chunk;
-    const int64_t p_end = min(a.M, p_begin + a.chunk);
-    if (p_begin >= p_end) return;
-    const int64_t OHW = int64_t(a.OH) * a.OW;
-
-    f32x4 acc[TS][TS];
-#pragma unroll
-    for (int i = 0; i < TS; ++i)
-#pragma unroll
-        for (int j = 0; j < TS; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    uint4 ra[ITEMS], rb[ITEMS];
-    const uint32_t uOHW = uint32_t(OHW), uOW = uint32_t(a.OW);
-    auto load = [&](int64_t p0) {
-#pragma unroll
-        for (int it = 0; it < ITEMS; ++it) {
-            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
-            int64_t p = p0 + srow;
-            ra[it] = make_uint4(0, 0, 0, 0);
-            rb[it] = make_uint4(0, 0, 0, 0);
-            if (p < p_end) {
-                const uint32_t up = uint32_t(p);                  // M < 2^31 (checked on the host)
-                const uint32_t n = up / uOHW, pix = up - n * uOHW;
-                const int oh = int(pix / uOW), ow = int(pix - uint32_t(oh) * uOW);
-                int co = co0 + sc * 8;
-                if (co < a.Cout)
-                    ra[it] = *reinterpret_cast<const uint4*>(a.dz + int64_t(n) * a.dz_bs + int64_t(pix) * a.dz_ld + co);
-                int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-                int ci = ci0 + sc * 8;
-                if (ci < a.Cin && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW) {
-                    uint4 h = *reinterpret_cast<const uint4*>(a.x + int64_t(n) * a.x_bs + (int64_t(ih) * a.IW + iw) * a.x_ld + ci);
-                    uint32_t w4[4] = {h.x, h.y, h.z, h.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)   // fp16 activation -> bf16 MFMA operand
-                        w4[e] = uint32_t(f2bf(h2f(uint16_t(w4[e] & 0xffff)))) |
-                                (uint32_t(f2bf(h2f(uint16_t(w4[e] >> 16)))) << 16);
-                    rb[it] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                }
-            }
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int it = 0; it < ITEMS; ++it) {
-            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
-            *reinterpret_cast<uint4*>(&As[buf][srow * RS + sc * 16]) = ra[it];
-            *reinterpret_cast<uint4*>(&Bs[buf][srow * RS + sc * 16]) = rb[it];
-        }
-    };
-
-    // transposed fragment read: group g = lane>>4 owns k rows {4g..4g+3} and {16+4g..16+4g+3};
-    // lane 4q+p of the group addresses row (4g+q [+16]), columns col0 + 4p .. +3
-    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-    auto frag = [&](const char* base, int col0) -> bf16x8 {
-        const char* p1 = base + (4 * g + q) * RS + (col0 + 4 * pp) * 2;
-        const char* p2 = p1 + 16 * RS;
-        s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
-        s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p2));
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, v);
-    };
-
-    load(p_begin);
-    store(0);
-    __syncthreads();
-    int buf = 0;
-    for (int64_t p0 = p_begin; p0 < p_end; p0 += 32) {
-        const bool more = p0 + 32 < p_end;
-        if (more) load(p0 + 32);
-        bf16x8 af[TS], bf[TS];
-#pragma unroll
-        for (int i = 0; i < TS; ++i) af[i] = frag(As[buf], wr * (T / 2) + i * 16);
-#pragma unroll
-        for (int j = 0; j < TS; ++j) bf[j] = frag(Bs[buf], wc * (T / 2) + j * 16);
-#pragma unroll
-        for (int i = 0; i < TS; ++i)
-#pragma unroll
-            for (int j = 0; j < TS; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-        if (more) store(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
-    }
-    // D[co][ci]: lane holds co rows (lane>>4)*4 + r, ci column lane&15
-    const int64_t trow = int64_t(a.KH) * a.KW * a.Cin;
-#pragma unroll
-    for (int i = 0; i < TS; ++i)
-#pragma unroll
-        for (int j = 0; j < TS; ++j) {
-            int ci = ci0 + wc * (T / 2) + j * 16 + (lane & 15);
-            if (ci >= a.Cin) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                int co = co0 + wr * (T / 2) + i * 16 + (lane >> 4) * 4 + r;
-                if (co < a.Cout) atomicAdd(a.dw + co * trow + int64_t(tap) * a.Cin + ci, acc[i][j][r]);
-            }
-        }
-}
-
-// [Cout][KH*KW][Cin] fp32 -> [Cout][Cin][KH][KW] fp32 (PyTorch OIHW), optionally accumulating
-__global__ void ohwi_to_oihw_kernel(const float* __restrict__ src, float* __restrict__ dst, int Cout, int Cin,
-                                    int T, int accumulate) {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    int64_t total = int64_t(Cout) * Cin * T;
-    if (i >= total) return;
-    int t = int(i % T);
-    int64_t r = i / T;
-    int ci = int(r % Cin);
-    int co = int(r / Cin);
-    float v = src[(int64_t(co) * T + t) * Cin + ci];
-    dst[i] = accumulate ? dst[i] + v : v;
 }
 
 // ------------------------------------------------------------------ stem conv (Cin = 1), fp32 image input
@@ -756,48 +605,6 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
                  "ym_conv_dgrad: gradient image stride too large");
     pick_and_launch(a, MODE_DGRAD, 4096, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_dgrad");
-    return YM_OK;
-}
-
-extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, float* dw_ohwi, void* stream) {
-    // dw_ohwi [cout][k*k][cin] fp32 must be zeroed (or hold a partial sum) by the caller
-    YM_CHECK_ARG(d && dz && x && dw_ohwi, "ym_conv_wgrad: null argument");
-    YM_CHECK_ARG(d->cin % 8 == 0 && d->cout % 8 == 0, "ym_conv_wgrad: channels %% 8 != 0");
-    YM_CHECK_ARG(d->x_ld % 8 == 0 && d->y_ld % 8 == 0 && d->x_bs % 8 == 0 && d->y_bs % 8 == 0,
-                 "ym_conv_wgrad: views not 16-byte aligned");
-    WgradArgs a{};
-    a.dz = dz; a.dz_bs = d->y_bs; a.dz_ld = d->y_ld;
-    a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
-    a.dw = dw_ohwi;
-    a.IH = d->h; a.IW = d->w; a.Cin = d->cin; a.OH = d->oh; a.OW = d->ow; a.Cout = d->cout;
-    a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
-    a.M = int64_t(d->n) * d->oh * d->ow;
-    if (a.M == 0) return YM_OK;
-    YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_wgrad: too many pixels");
-    // 128x128 tiles when both channel counts fill them, else 64x64
-    const int T = (a.Cout >= 128 && a.Cin >= 128) ? 128 : 64;
-    int co_t = (a.Cout + T - 1) / T;
-    a.ci_tiles = (a.Cin + T - 1) / T;
-    int cols = a.ci_tiles * a.KH * a.KW;
-    int64_t steps = (a.M + 31) / 32;
-    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(2048 / (co_t * cols), steps / 8));
-    splits = std::min<int64_t>(splits, 65535);
-    a.chunk = ((steps + splits - 1) / splits) * 32;
-    splits = (a.M + a.chunk - 1) / a.chunk;
-    if (T == 128)
-        hipLaunchKernelGGL(wgrad_kernel<128>, dim3(co_t, cols, unsigned(splits)), dim3(256), 0, as_stream(stream), a);
-    else
-        hipLaunchKernelGGL(wgrad_kernel<64>, dim3(co_t, cols, unsigned(splits)), dim3(256), 0, as_stream(stream), a);
-    YM_LAUNCH_CHECK("ym_conv_wgrad");
-    return YM_OK;
-}
-
-extern "C" int ym_wgrad_to_oihw(const float* src, float* dst, int cout, int cin, int taps, int accumulate, void* stream) {
-    int64_t total = int64_t(cout) * cin * taps;
-    if (total == 0) return YM_OK;
-    hipLaunchKernelGGL(ohwi_to_oihw_kernel, dim3(unsigned((total + 255) / 256)), dim3(256), 0, as_stream(stream), src,
-                       dst, cout, cin, taps, accumulate);
-    YM_LAUNCH_CHECK("ym_wgrad_to_oihw");
     return YM_OK;
 }
 

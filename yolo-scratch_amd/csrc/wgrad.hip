@@ -1,0 +1,535 @@
+// Convolution weight gradients on CDNA4 MFMA (bf16 x bf16, fp32 accumulate).
+//
+// Replaces the weight half of nn.Conv2d's autograd inside Conv / Detect
+// (/root/reference/yolo_scratch_cuda/models/yolo11_modules.py:21-33, 221-234):
+// dW[co][ci][kh][kw] = sum over output pixels p of dz[p][co] * x[src(p, kh, kw)][ci].
+// K of this GEMM is the pixel axis (N*OH*OW, up to 1.6 M at s@640 bs64), so every kernel
+// splits it over grid.z and writes fp32 partials [split][Cout][taps][Cin]; wgrad_reduce_kernel
+// sums the splits and writes the PyTorch OIHW gradient (overwrite or accumulate) — no atomics,
+// no zero-fill by the caller.
+//
+// wgrad3_kernel<S>  3x3, pad 1, stride S in {1, 2}: one workgroup owns a 64co x 64ci tile for
+//   ALL nine taps (144 fp32 accumulators per lane).  Per 8x8 block of output pixels it stages
+//   dz (64 pixels x 64 co) and the input halo ((7S+3)^2 pixels x 64 ci) once — fp16
+//   activations converted to bf16 once — and every tap reads its shifted window out of the same
+//   halo with transposed LDS reads (ds_read_b64_tr_b16) whose tap offsets are immediates.
+// wgrad1_kernel<T>  1x1 stride 1 over whole-image views: pixels are a flat axis, so each lane's
+//   staging offsets are fixed for the whole K loop; T x T tiles, 64 pixels per stage.
+// wgrad_generic_kernel<T>  any other geometry (per-tap columns, fp32 atomics into split 0).
+#include <algorithm>
+
+#include "common.h"
+#include "tile.h"
+
+namespace ym {
+namespace {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+struct WgArgs {
+    const bf16_t* dz; int64_t dz_bs, dz_ld;   // (N, OH, OW, Cout) bf16 view
+    const uint16_t* x; int64_t x_bs, x_ld;    // (N, IH, IW, Cin) fp16 view
+    float* part;                              // [splits][Cout][taps][Cin] fp32
+    int N, IH, IW, Cin, OH, OW, Cout, KH, KW, stride, pad;
+    int64_t M;                                // N*OH*OW
+    int64_t units;                            // K units: 64-pixel stages (1x1), 8x8 tiles (3x3), 32-pixel steps
+    int64_t chunk;                            // units per split
+    int ci_tiles;                             // generic kernel: channel tiles per tap column
+};
+
+// transposed 16x(32 k) fragment: two ds_read_b64_tr_b16, k rows {4g..4g+3} from p_lo and
+// {16+4g..} from p_hi (g = lane>>4); the same k permutation on both operands cancels
+__device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p_lo));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p_hi));
+    s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, v);
+}
+
+// ------------------------------------------------------------------ 3x3
+template <int S>
+__global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
+    constexpr int TC = 64;                    // co and ci tile
+    constexpr int RSD = TC * 2 + 32;          // dz rows: consecutive-row tr reads conflict free
+    constexpr int RSX = S == 1 ? 160 : 144;   // halo rows: reads step S rows (S=2 needs 36-dword rows)
+    constexpr int HD = 7 * S + 3;             // halo side
+    constexpr int HR = HD * HD;
+    constexpr int XI = (HR * 8 + 255) / 256;  // 16-B halo chunks per thread
+    __shared__ __attribute__((aligned(16))) char Dz[64 * RSD];
+    __shared__ __attribute__((aligned(16))) char Xh[HR * RSX];
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int co0 = blockIdx.x * TC, ci0 = blockIdx.y * TC;
+    const int sc = tid & 7, srow = tid >> 3;  // staging: chunk sc of rows srow + 32*it
+    const bool co_ok = co0 + sc * 8 < a.Cout, ci_ok = ci0 + sc * 8 < a.Cin;
+    int x_hy[XI], x_hx[XI];
+#pragma unroll
+    for (int it = 0; it < XI; ++it) {
+        const int r = srow + 32 * it;
+        x_hy[it] = r / HD;
+        x_hx[it] = r - x_hy[it] * HD;
+    }
+    const int ntw = (a.OW + 7) >> 3, nth = (a.OH + 7) >> 3;
+    const int64_t t_begin = int64_t(blockIdx.z) * a.chunk;
+    const int64_t t_end = std::min<int64_t>(a.units, t_begin + a.chunk);
+
+    // fragment-read geometry: lane's k rows (pixels of the 8x8 tile) for the two 32-pixel halves
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    int hb_lo[2], hb_hi[2];                   // halo row of (pixel, tap 0,0)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int plo = kk * 32 + 4 * g + q, phi = plo + 16;
+        hb_lo[kk] = (plo >> 3) * S * HD + (plo & 7) * S;
+        hb_hi[kk] = (phi >> 3) * S * HD + (phi & 7) * S;
+    }
+
+    f32x4 acc[9][2][2];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 rdz[2], rx[XI];
+    auto load = [&](int64_t t) {
+        const int tw = int(t % ntw);
+        const int64_t r = t / ntw;
+        const int th = int(r % nth), n = int(r / nth);
+        const int oh0 = th * 8, ow0 = tw * 8;
+        const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + int64_t(n) * a.dz_bs, a.dz_bs * 2);
+        const __amdgpu_buffer_rsrc_t rxs = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            const int p = srow + 32 * it;
+            const int oh = oh0 + (p >> 3), ow = ow0 + (p & 7);
+            const bool ok = co_ok && oh < a.OH && ow < a.OW;
+            rdz[it] = buf_load16(rd, ok ? uint32_t(((oh * a.OW + ow) * int(a.dz_ld) + co0 + sc * 8) * 2) : OOB);
+        }
+        const int ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
+#pragma unroll
+        for (int it = 0; it < XI; ++it) {
+            const int ih = ih0 + x_hy[it], iw = iw0 + x_hx[it];
+            const bool ok = ci_ok && srow + 32 * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
+            rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + sc * 8) * 2) : OOB);
+        }
+    };
+    auto store = [&]() {
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+            *reinterpret_cast<uint4*>(Dz + (srow + 32 * it) * RSD + sc * 16) = rdz[it];
+#pragma unroll
+        for (int it = 0; it < XI; ++it)
+            if (srow + 32 * it < HR)
+                *reinterpret_cast<uint4*>(Xh + (srow + 32 * it) * RSX + sc * 16) = h8_to_bf8(rx[it]);
+    };
+
+    if (t_begin < t_end) {
+        load(t_begin);
+        store();
+        __syncthreads();
+    }
+    for (int64_t t = t_begin; t < t_end; ++t) {
+        const bool more = t + 1 < t_end;
+        if (more) load(t + 1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            bf16x8 af[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int col = (wr * 32 + i * 16 + 4 * pp) * 2;
+                af[i] = tr_frag(Dz + (kk * 32 + 4 * g + q) * RSD + col, Dz + (kk * 32 + 16 + 4 * g + q) * RSD + col);
+            }
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int toff = kh * HD + kw;
+                    bf16x8 bfr[2];
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) {
+                        const int col = (wc * 32 + j * 16 + 4 * pp) * 2;
+                        bfr[j] = tr_frag(Xh + (hb_lo[kk] + toff) * RSX + col, Xh + (hb_hi[kk] + toff) * RSX + col);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[kh * 3 + kw][i][j] =
+                                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[kh * 3 + kw][i][j], 0, 0, 0);
+                }
+        }
+        __syncthreads();
+        if (more) {
+            store();
+            __syncthreads();
+        }
+    }
+
+    // partials: D[co][ci], lane holds co rows (lane>>4)*4 + r, ci column lane&15
+    float* base = a.part + int64_t(blockIdx.z) * a.Cout * 9 * a.Cin;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int ci = ci0 + wc * 32 + j * 16 + (lane & 15);
+                if (ci >= a.Cin) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int co = co0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+                    if (co < a.Cout) base[(int64_t(co) * 9 + t) * a.Cin + ci] = acc[t][i][j][r];
+                }
+            }
+}
+
+// ------------------------------------------------------------------ 1x1, whole-image views
+template <int T>
+__global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
+    constexpr int KP = 64;                    // pixels per stage (2 MFMA k-steps)
+    constexpr int RS = T * 2 + 32;
+    constexpr int CPR = T / 8;                // 16-B chunks per row
+    constexpr int RPP = 256 / CPR;            // rows staged per pass
+    constexpr int ITEMS = KP / RPP;
+    constexpr int TS = T / 32;
+    __shared__ __attribute__((aligned(16))) char As[2][KP * RS];   // dz rows x T co
+    __shared__ __attribute__((aligned(16))) char Bs[2][KP * RS];   // x rows x T ci (bf16)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int co0 = blockIdx.x * T, ci0 = blockIdx.y * T;
+    const int sc = tid % CPR, srow = tid / CPR;
+    const int64_t p_begin = (int64_t(blockIdx.z) * a.chunk) * KP;
+    const int64_t p_end = std::min<int64_t>(a.M, p_begin + a.chunk * KP);
+    uint32_t dz_off[ITEMS], x_off[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const int r = srow + RPP * it;
+        dz_off[it] = co0 + sc * 8 < a.Cout ? uint32_t((r * int(a.dz_ld) + co0 + sc * 8) * 2) : OOB;
+        x_off[it] = ci0 + sc * 8 < a.Cin ? uint32_t((r * int(a.x_ld) + ci0 + sc * 8) * 2) : OOB;
+    }
+
+    f32x4 acc[TS][TS];
+#pragma unroll
+    for (int i = 0; i < TS; ++i)
+#pragma unroll
+        for (int j = 0; j < TS; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    uint4 ra[ITEMS], rb[ITEMS];
+    auto load = [&](int64_t p0) {
+        // records end at p_end: rows past it read as zero
+        const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + p0 * a.dz_ld, (p_end - p0) * a.dz_ld * 2);
+        const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + p0 * a.x_ld, (p_end - p0) * a.x_ld * 2);
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            ra[it] = buf_load16(rd, dz_off[it]);
+            rb[it] = buf_load16(rx, x_off[it]);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const int r = srow + RPP * it;
+            *reinterpret_cast<uint4*>(&As[buf][r * RS + sc * 16]) = ra[it];
+            *reinterpret_cast<uint4*>(&Bs[buf][r * RS + sc * 16]) = h8_to_bf8(rb[it]);
+        }
+    };
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+
+    int buf = 0;
+    if (p_begin < p_end) {
+        load(p_begin);
+        store(0);
+        __syncthreads();
+    }
+    for (int64_t p0 = p_begin; p0 < p_end; p0 += KP) {
+        const bool more = p0 + KP < p_end;
+        if (more) load(p0 + KP);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const char* A0 = As[buf] + (kk * 32 + 4 * g + q) * RS;
+            const char* B0 = Bs[buf] + (kk * 32 + 4 * g + q) * RS;
+            bf16x8 af[TS], bfr[TS];
+#pragma unroll
+            for (int i = 0; i < TS; ++i) {
+                const int col = (wr * (T / 2) + i * 16 + 4 * pp) * 2;
+                af[i] = tr_frag(A0 + col, A0 + 16 * RS + col);
+            }
+#pragma unroll
+            for (int j = 0; j < TS; ++j) {
+                const int col = (wc * (T / 2) + j * 16 + 4 * pp) * 2;
+                bfr[j] = tr_frag(B0 + col, B0 + 16 * RS + col);
+            }
+#pragma unroll
+            for (int i = 0; i < TS; ++i)
+#pragma unroll
+                for (int j = 0; j < TS; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    float* base = a.part + int64_t(blockIdx.z) * a.Cout * a.Cin;
+#pragma unroll
+    for (int i = 0; i < TS; ++i)
+#pragma unroll
+        for (int j = 0; j < TS; ++j) {
+            const int ci = ci0 + wc * (T / 2) + j * 16 + (lane & 15);
+            if (ci >= a.Cin) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + wr * (T / 2) + i * 16 + (lane >> 4) * 4 + r;
+                if (co < a.Cout) base[int64_t(co) * a.Cin + ci] = acc[i][j][r];
+            }
+        }
+}
+
+// ------------------------------------------------------------------ generic (any k, stride, pad, view)
+// one (co tile, tap, ci tile) per block, 32 pixels per step, fp32 atomics into split 0
+template <int T>
+__global__ void __launch_bounds__(256) wgrad_generic_kernel(WgArgs a) {
+    constexpr int RS = T * 2 + 32;
+    constexpr int CPR = T / 8;
+    constexpr int ITEMS = 32 * CPR / 256;
+    constexpr int TS = T / 32;
+    __shared__ __attribute__((aligned(16))) char As[2][32 * RS];
+    __shared__ __attribute__((aligned(16))) char Bs[2][32 * RS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int co0 = blockIdx.x * T;
+    const int tap = blockIdx.y / a.ci_tiles;
+    const int ci0 = (blockIdx.y - tap * a.ci_tiles) * T;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const int64_t p_begin = int64_t(blockIdx.z) * a.chunk * 32;
+    const int64_t p_end = std::min<int64_t>(a.M, p_begin + a.chunk * 32);
+    if (p_begin >= p_end) return;
+    const uint32_t uOHW = uint32_t(a.OH) * uint32_t(a.OW), uOW = uint32_t(a.OW);
+
+    f32x4 acc[TS][TS];
+#pragma unroll
+    for (int i = 0; i < TS; ++i)
+#pragma unroll
+        for (int j = 0; j < TS; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint4 ra[ITEMS], rb[ITEMS];
+    auto load = [&](int64_t p0) {
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
+            const int64_t p = p0 + srow;
+            ra[it] = make_uint4(0, 0, 0, 0);
+            rb[it] = make_uint4(0, 0, 0, 0);
+            if (p < p_end) {
+                const uint32_t up = uint32_t(p);
+                const uint32_t n = up / uOHW, pix = up - n * uOHW;
+                const int oh = int(pix / uOW), ow = int(pix - uint32_t(oh) * uOW);
+                const int co = co0 + sc * 8;
+                if (co < a.Cout)
+                    ra[it] = *reinterpret_cast<const uint4*>(a.dz + int64_t(n) * a.dz_bs + int64_t(pix) * a.dz_ld + co);
+                const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+                const int ci = ci0 + sc * 8;
+                if (ci < a.Cin && ih >= 0 && ih < a.IH && iw >= 0 && iw < a.IW)
+                    rb[it] = h8_to_bf8(*reinterpret_cast<const uint4*>(a.x + int64_t(n) * a.x_bs +
+                                                                       (int64_t(ih) * a.IW + iw) * a.x_ld + ci));
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int it = 0; it < ITEMS; ++it) {
+            const int id = tid + it * 256, srow = id / CPR, sc = id % CPR;
+            *reinterpret_cast<uint4*>(&As[buf][srow * RS + sc * 16]) = ra[it];
+            *reinterpret_cast<uint4*>(&Bs[buf][srow * RS + sc * 16]) = rb[it];
+        }
+    };
+    const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    load(p_begin);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t p0 = p_begin; p0 < p_end; p0 += 32) {
+        const bool more = p0 + 32 < p_end;
+        if (more) load(p0 + 32);
+        const char* A0 = As[buf] + (4 * g + q) * RS;
+        const char* B0 = Bs[buf] + (4 * g + q) * RS;
+        bf16x8 af[TS], bfr[TS];
+#pragma unroll
+        for (int i = 0; i < TS; ++i) {
+            const int col = (wr * (T / 2) + i * 16 + 4 * pp) * 2;
+            af[i] = tr_frag(A0 + col, A0 + 16 * RS + col);
+        }
+#pragma unroll
+        for (int j = 0; j < TS; ++j) {
+            const int col = (wc * (T / 2) + j * 16 + 4 * pp) * 2;
+            bfr[j] = tr_frag(B0 + col, B0 + 16 * RS + col);
+        }
+#pragma unroll
+        for (int i = 0; i < TS; ++i)
+#pragma unroll
+            for (int j = 0; j < TS; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    const int taps = a.KH * a.KW;
+#pragma unroll
+    for (int i = 0; i < TS; ++i)
+#pragma unroll
+        for (int j = 0; j < TS; ++j) {
+            const int ci = ci0 + wc * (T / 2) + j * 16 + (lane & 15);
+            if (ci >= a.Cin) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = co0 + wr * (T / 2) + i * 16 + (lane >> 4) * 4 + r;
+                if (co < a.Cout) atomicAdd(a.part + (int64_t(co) * taps + tap) * a.Cin + ci, acc[i][j][r]);
+            }
+        }
+}
+
+// ------------------------------------------------------------------ split reduction -> OIHW
+// block: 64 consecutive (co, tap, ci) elements x 4 split lanes; dst[co][ci][tap] (+)= sum
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t splits,
+                                                           int Cout, int taps, int Cin, float* __restrict__ dst,
+                                                           int accumulate) {
+    __shared__ float red[4][64];
+    const int64_t E = int64_t(Cout) * taps * Cin;
+    const int64_t e = int64_t(blockIdx.x) * 64 + (threadIdx.x & 63);
+    const int zl = threadIdx.x >> 6;
+    float s = 0.f;
+    if (e < E) {
+        int64_t z = zl;
+        for (; z + 12 < splits; z += 16) {
+            const float v0 = part[z * E + e], v1 = part[(z + 4) * E + e];
+            const float v2 = part[(z + 8) * E + e], v3 = part[(z + 12) * E + e];
+            s += (v0 + v1) + (v2 + v3);
+        }
+        for (; z < splits; z += 4) s += part[z * E + e];
+    }
+    red[zl][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (zl == 0 && e < E) {
+        const float v = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+        const int ci = int(e % Cin);
+        const int64_t r = e / Cin;
+        const int t = int(r % taps), co = int(r / taps);
+        float* d = dst + (int64_t(co) * Cin + ci) * taps + t;
+        *d = accumulate ? *d + v : v;
+    }
+}
+
+// ------------------------------------------------------------------ launch plan
+struct WgPlan {
+    int kind;          // 3: wgrad3, 1: wgrad1, 0: generic
+    int T;
+    int co_t, ci_t;
+    int64_t units, chunk, splits;
+};
+
+WgPlan wg_plan(const ym_conv_desc* d) {
+    WgPlan p{};
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    const bool whole = d->x_bs == int64_t(d->h) * d->w * d->x_ld && d->y_bs == int64_t(d->oh) * d->ow * d->y_ld;
+    if (d->k == 3 && d->pad == 1 && (d->stride == 1 || d->stride == 2)) {
+        p.kind = 3;
+        p.T = 64;
+        p.units = int64_t(d->n) * ((d->oh + 7) / 8) * ((d->ow + 7) / 8);
+    } else if (d->k == 1 && d->stride == 1 && d->pad == 0 && whole) {
+        p.kind = 1;
+        p.T = (d->cout >= 128 && d->cin >= 128) ? 128 : 64;
+        p.units = (M + 63) / 64;
+    } else {
+        p.kind = 0;
+        p.T = (d->cout >= 128 && d->cin >= 128) ? 128 : 64;
+        p.units = (M + 31) / 32;
+    }
+    p.co_t = (d->cout + p.T - 1) / p.T;
+    p.ci_t = (d->cin + p.T - 1) / p.T;
+    const int64_t cols = int64_t(p.co_t) * p.ci_t * (p.kind == 0 ? d->k * d->k : 1);
+    // about two workgroups per CU, each with at least 4 K units; partials bounded at 256 splits
+    const int64_t min_units = p.kind == 3 ? 4 : 8;
+    int64_t splits = std::max<int64_t>(1, std::min<int64_t>(512 / cols, p.units / min_units));
+    splits = std::min<int64_t>(splits, p.kind == 0 ? 65535 : 256);
+    p.chunk = (p.units + splits - 1) / splits;
+    p.splits = std::max<int64_t>(1, (p.units + p.chunk - 1) / p.chunk);
+    return p;
+}
+
+}  // namespace
+}  // namespace ym
+
+using namespace ym;
+
+extern "C" size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d) {
+    if (!d) return 0;
+    const WgPlan p = wg_plan(d);
+    const int64_t E = int64_t(d->cout) * d->k * d->k * d->cin;
+    return size_t((p.kind == 0 ? 1 : p.splits) * E) * sizeof(float);
+}
+
+extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, void* workspace,
+                             size_t workspace_bytes, float* dw_oihw, int accumulate, void* stream) {
+    YM_CHECK_ARG(d && dz && x && dw_oihw, "ym_conv_wgrad: null argument");
+    YM_CHECK_ARG(d->cin % 8 == 0 && d->cout % 8 == 0, "ym_conv_wgrad: channels %% 8 != 0");
+    YM_CHECK_ARG(d->x_ld % 8 == 0 && d->y_ld % 8 == 0 && d->x_bs % 8 == 0 && d->y_bs % 8 == 0,
+                 "ym_conv_wgrad: views not 16-byte aligned");
+    const WgPlan p = wg_plan(d);
+    const int taps = d->k * d->k;
+    const int64_t E = int64_t(d->cout) * taps * d->cin;
+    const size_t need = size_t((p.kind == 0 ? 1 : p.splits) * E) * sizeof(float);
+    YM_CHECK_ARG(workspace && workspace_bytes >= need, "ym_conv_wgrad: workspace %zu < %zu bytes", workspace_bytes,
+                 need);
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    YM_CHECK_ARG(M < (int64_t(1) << 31), "ym_conv_wgrad: too many pixels");
+    YM_CHECK_ARG(d->x_bs * 2 < (int64_t(1) << 31) && d->y_bs * 2 < (int64_t(1) << 31),
+                 "ym_conv_wgrad: image stride too large");
+    hipStream_t st = as_stream(stream);
+    WgArgs a{};
+    a.dz = dz; a.dz_bs = d->y_bs; a.dz_ld = d->y_ld;
+    a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
+    a.part = static_cast<float*>(workspace);
+    a.N = d->n; a.IH = d->h; a.IW = d->w; a.Cin = d->cin; a.OH = d->oh; a.OW = d->ow; a.Cout = d->cout;
+    a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
+    a.M = M; a.units = p.units; a.chunk = p.chunk;
+    int64_t splits = p.splits;
+    if (M == 0) {
+        // no pixels: the gradient is zero
+        splits = 0;
+    } else if (p.kind == 3) {
+        YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
+        if (d->stride == 1)
+            hipLaunchKernelGGL(wgrad3_kernel<1>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(wgrad3_kernel<2>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+    } else if (p.kind == 1) {
+        if (p.T == 128)
+            hipLaunchKernelGGL(wgrad1_kernel<128>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(wgrad1_kernel<64>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+    } else {
+        if (hipMemsetAsync(workspace, 0, size_t(E) * sizeof(float), st) != hipSuccess) {
+            set_error("ym_conv_wgrad: memset failed");
+            return YM_ERR_HIP;
+        }
+        a.ci_tiles = p.ci_t;
+        const dim3 grid(p.co_t, p.ci_t * taps, unsigned(splits));
+        if (p.T == 128)
+            hipLaunchKernelGGL(wgrad_generic_kernel<128>, grid, dim3(256), 0, st, a);
+        else
+            hipLaunchKernelGGL(wgrad_generic_kernel<64>, grid, dim3(256), 0, st, a);
+        splits = 1;
+    }
+    YM_LAUNCH_CHECK("ym_conv_wgrad");
+    if (splits == 0) {
+        if (!accumulate && hipMemsetAsync(dw_oihw, 0, size_t(E) * sizeof(float), st) != hipSuccess) {
+            set_error("ym_conv_wgrad: memset failed");
+            return YM_ERR_HIP;
+        }
+        return YM_OK;
+    }
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(unsigned((E + 63) / 64)), dim3(256), 0, st,
+                       static_cast<const float*>(workspace), splits, d->cout, taps, d->cin, dw_oihw, accumulate);
+    YM_LAUNCH_CHECK("ym_conv_wgrad(reduce)");
+    return YM_OK;
+}

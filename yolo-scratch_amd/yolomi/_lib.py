@@ -45,8 +45,8 @@ SIGNATURES = {
     "ym_conv_stat_blocks": (R, [I64, INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
-    "ym_conv_wgrad": (R, [P, P, P, P, P]),
-    "ym_wgrad_to_oihw": (R, [P, P, INT, INT, INT, INT, P]),
+    "ym_conv_wgrad_workspace_size": (SZ, [P]),
+    "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),

@@ -186,7 +186,7 @@ class ConvBN:
         d.x_bs, d.x_ld, d.y_bs, d.y_ld = x.bs, x.ld, self.HW * co, co
         d.out_f32 = 2                                                   # fp16 pre-BN z
         self.desc = d
-        self.wscratch = plan.wgrad_scratch(co * ci * k * k) if k > 1 else None
+        plan.need_wgrad_ws(d)
 
     def flops(self):
         return 2 * self.M * self.co * self.ci * self.k * self.k
@@ -235,12 +235,9 @@ class ConvBN:
                  self.HW, acc, 0, st)
             self.res.mark()
         # weight gradient
-        w = self.m.conv.weight
-        if self.k == 1:
-            call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), plan.gptr(w), st)
-        else:
-            call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), self.wscratch.data_ptr(), st)
-            call("ym_wgrad_to_oihw", self.wscratch.data_ptr(), plan.gptr(w), self.co, self.ci, self.k * self.k, 0, st)
+        ws = plan.wgrad_ws()
+        call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
+             plan.gptr(self.m.conv.weight), 0, st)
         # data gradient
         if plan.needs_grad(self.x):
             acc = self.x.grad_for_write(st)
@@ -498,6 +495,8 @@ class HeadLevel:
         self.fc = desc(xc, self.nc, A * no, no, 1)
         self.bb = desc(xb, 64, self.HW * 64, 64, 0)
         self.bc = desc(xc, 8, self.HW * 8, 8, 0)
+        plan.need_wgrad_ws(self.bb)
+        plan.need_wgrad_ws(self.bc)
 
     def forward(self, plan, st):
         base = self.head.data_ptr() + self.a_off * self.head.shape[2] * 4
@@ -510,9 +509,11 @@ class HeadLevel:
         B, A, no = self.head.shape
         call("ym_head_grad", plan.dhead.data_ptr(), A, self.a_off, self.HW, self.M, self.nc, self.dzb.data_ptr(),
              self.dzc.data_ptr(), plan.gptr(self.box.bias), plan.gptr(self.cls.bias), st)
-        call("ym_conv_wgrad", ctypes.byref(self.bb), self.dzb.data_ptr(), self.xb.ptr(), plan.gptr(self.box.weight), st)
-        self.wsc.zero_()
-        call("ym_conv_wgrad", ctypes.byref(self.bc), self.dzc.data_ptr(), self.xc.ptr(), self.wsc.data_ptr(), st)
+        ws = plan.wgrad_ws()
+        call("ym_conv_wgrad", ctypes.byref(self.bb), self.dzb.data_ptr(), self.xb.ptr(), ws.data_ptr(), ws.numel() * 4,
+             plan.gptr(self.box.weight), 0, st)
+        call("ym_conv_wgrad", ctypes.byref(self.bc), self.dzc.data_ptr(), self.xc.ptr(), ws.data_ptr(), ws.numel() * 4,
+             self.wsc.data_ptr(), 0, st)
         g = plan.grad_view(self.cls.weight).view(self.nc, -1)
         g.copy_(self.wsc[: self.nc])
         for d, dz, wt, x in ((self.bb, self.dzb, self.wb_t, self.xb), (self.bc, self.dzc, self.wc_t, self.xc)):
@@ -549,10 +550,15 @@ class Plan:
     def act(self, C, H, W, name=""):
         return View(Act(self, C, H, W, name=name))
 
-    def wgrad_scratch(self, n):
-        t = torch.empty(n, dtype=F32, device=self.dev)
-        self._scratch.append(t)
-        return t
+    def need_wgrad_ws(self, desc):
+        """Size the shared split-K workspace of ym_conv_wgrad (ops run in order on one stream)."""
+        self._wg_bytes = max(getattr(self, "_wg_bytes", 0), int(lib().ym_conv_wgrad_workspace_size(ctypes.byref(desc))))
+
+    def wgrad_ws(self):
+        ws = getattr(self, "_wg_ws", None)
+        if ws is None:
+            ws = self._wg_ws = torch.empty(max(self._wg_bytes // 4, 1), dtype=F32, device=self.dev)
+        return ws
 
     def grad_view(self, p):
         return self.grad_views[id(p)]
