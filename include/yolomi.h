@@ -159,15 +159,16 @@ int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16
  * SPPF max-pool (yolo11_modules.py:92-105), nearest 2x upsample (yaml head rows 11, 14),
  * C2PSA attention core (yolo11_modules.py:124-136), view conversions, Detect grad split.
  */
-int ym_maxpool5_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int n,
-                    int h, int w, int c, void* stream);
-/* dx_f32 (dense, +=) from dy_f32 (dense) through the argmax of each 5x5 window of x */
-int ym_maxpool5_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, const float* dy, float* dx, int n, int h, int w,
-                    int c, void* stream);
-/* SPPF's three chained pools on fp32 values (tie semantics of the fp32 reference): y32 and a bf16 view copy */
-int ym_maxpool5_f32_fwd(const float* x, float* y, uint16_t* yb, int64_t y_bs, int64_t y_ld, int n, int h, int w,
+/* SPPF's chained 5x5 / stride 1 / pad 2 pools on fp32 values (first-max tie semantics of the fp32
+ * reference).  Forward: y (dense fp32), code (dense uint8 window argmax kh*5+kw) and an fp16 copy
+ * into the view yv.  Backward (gather over the argmax codes, no atomics):
+ * out = init_view (bf16, optional) + sum of dy over the windows whose argmax is the pixel, written
+ * to dx (dense fp32, optional) and/or the bf16 view dxv (added to it when accumulate). */
+int ym_maxpool5_f32_fwd(const float* x, float* y, uint8_t* code, uint16_t* yv, int64_t y_bs, int64_t y_ld, int n,
+                        int h, int w, int c, void* stream);
+int ym_maxpool5_f32_bwd(const uint8_t* code, const float* dy, const uint16_t* init, int64_t i_bs, int64_t i_ld,
+                        float* dx, uint16_t* dxv, int64_t v_bs, int64_t v_ld, int accumulate, int n, int h, int w,
                         int c, void* stream);
-int ym_maxpool5_f32_bwd(const float* x, const float* dy, float* dx, int n, int h, int w, int c, void* stream);
 int ym_upsample2_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int n,
                      int h, int w, int c, void* stream);
 int ym_upsample2_bwd(const uint16_t* dy, int64_t d_bs, int64_t d_ld, uint16_t* dx, int64_t x_bs, int64_t x_ld, int n,

@@ -191,10 +191,12 @@ def test_sppf_pool_chain_exact():
     dys = [torch.randn(B, H, W, C, generator=g) for _ in range(3)]
     P = torch.zeros(4, B * H * W, C, device="cuda")
     P[0] = x.reshape(-1, C).cuda()
-    yb = torch.zeros(B, H, W, C, dtype=torch.bfloat16, device="cuda")
+    code = torch.zeros(3, B * H * W, C, dtype=torch.uint8, device="cuda")
+    yv = torch.zeros(B, H, W, C, dtype=torch.float16, device="cuda")
     st = stream_ptr()
     for j in range(3):
-        call("ym_maxpool5_f32_fwd", P[j].data_ptr(), P[j + 1].data_ptr(), yb.data_ptr(), H * W * C, C, B, H, W, C, st)
+        call("ym_maxpool5_f32_fwd", P[j].data_ptr(), P[j + 1].data_ptr(), code[j].data_ptr(), yv.data_ptr(),
+             H * W * C, C, B, H, W, C, st)
     xr = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
     ys, t = [], xr
     for j in range(3):
@@ -202,14 +204,39 @@ def test_sppf_pool_chain_exact():
         ys.append(t)
     for j in range(3):
         torch.testing.assert_close(P[j + 1].cpu().view(B, H, W, C), ys[j].detach().permute(0, 2, 3, 1), rtol=0, atol=0)
+    torch.testing.assert_close(yv.float().cpu(), ys[2].detach().permute(0, 2, 3, 1), rtol=0, atol=0)
     torch.autograd.backward(ys, [dy.permute(0, 3, 1, 2) for dy in dys])
-    # chain backward with the kernels: g3 -> +dy2 -> g2 -> +dy1 -> g1 -> dx
-    cur = dys[2].reshape(-1, C).cuda().contiguous()
-    for j in (2, 1, 0):
-        nxt = dys[j - 1].reshape(-1, C).cuda().clone() if j > 0 else torch.zeros(B * H * W, C, device="cuda")
-        call("ym_maxpool5_f32_bwd", P[j].data_ptr(), cur.data_ptr(), nxt.data_ptr(), B, H, W, C, st)
+    # chain backward with the kernels: g3 -> +dy2 -> g2 -> +dy1 -> g1 -> dx (bf16 view, accumulated
+    # onto a known base); the bf16 init views carry exactly representable values
+    dys_b = [d.bfloat16() for d in dys]
+    ref_dys = [d.float() for d in dys_b]
+    xr2 = x.permute(0, 3, 1, 2).clone().requires_grad_(True)
+    ys2, t = [], xr2
+    for j in range(3):
+        t = torch.nn.functional.max_pool2d(t, 5, 1, 2)
+        ys2.append(t)
+    torch.autograd.backward(ys2, [d.permute(0, 3, 1, 2) for d in ref_dys])
+    cur = ref_dys[2].reshape(-1, C).cuda().contiguous()
+    for j in (2, 1):
+        nxt = torch.empty(B * H * W, C, device="cuda")
+        init = dys_b[j - 1].cuda().contiguous()
+        call("ym_maxpool5_f32_bwd", code[j].data_ptr(), cur.data_ptr(), init.data_ptr(), H * W * C, C,
+             nxt.data_ptr(), None, 0, 0, 0, B, H, W, C, st)
         cur = nxt
-    torch.testing.assert_close(cur.cpu().view(B, H, W, C), xr.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
+    base = torch.full((B, H, W, C), 0.5, dtype=torch.bfloat16, device="cuda")
+    call("ym_maxpool5_f32_bwd", code[0].data_ptr(), cur.data_ptr(), None, 0, 0, None, base.data_ptr(), H * W * C, C,
+         1, B, H, W, C, st)
+    want = (xr2.grad.permute(0, 2, 3, 1) + 0.5).bfloat16().float()
+    torch.testing.assert_close(base.float().cpu(), want, rtol=1e-2, atol=1e-2)
+    # routing is exact: the fp32 chain result before the final bf16 rounding
+    cur_chk = ref_dys[2].reshape(-1, C).cuda().contiguous()
+    for j in (2, 1, 0):
+        nxt = torch.empty(B * H * W, C, device="cuda")
+        init = dys_b[j - 1].cuda().contiguous() if j > 0 else None
+        call("ym_maxpool5_f32_bwd", code[j].data_ptr(), cur_chk.data_ptr(), init.data_ptr() if init is not None else None,
+             H * W * C, C, nxt.data_ptr(), None, 0, 0, 0, B, H, W, C, st)
+        cur_chk = nxt
+    torch.testing.assert_close(cur_chk.cpu().view(B, H, W, C), xr2.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
 
 
 def _emulated_oracle_grads(scale, img, loss_fn):

@@ -1,0 +1,86 @@
+"""Per-layer timing of the conv kernels (fwd / dgrad / wgrad) of a YOLOv11 plan on the GPU.
+
+Builds the model at the bench configuration, runs one training step to populate every buffer,
+then replays each ConvBN's three conv launches in isolation (HIP events on the plan's stream)
+and prints achieved TFLOP/s per layer against the 2.5 PFLOP/s dense 16-bit MFMA peak.
+
+usage: python tools/layer_bench.py [--scale s --imgsz 640 --batch 64 --reps 10]
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (str(ROOT), str(ROOT / "yolo-scratch_amd")):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", default="s")
+    ap.add_argument("--imgsz", type=int, default=640)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=10)
+    args = ap.parse_args()
+    import torch
+    import yaml
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    from yolomi._lib import call, stream_ptr
+    from yolomi.graph import ConvBN
+
+    dev = torch.device("cuda", 0)
+    cfg = yaml.safe_load((ROOT / "yolo-scratch_amd" / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = args.scale
+    model = build_yolo11(cfg, ch=1, nc=5).to(dev).train()
+    crit = v8DetectionLoss(model)
+    b = {k: v.to(dev) for k, v in synth_batch(args.batch, args.imgsz, seed=1).items()}
+    loss, _ = crit(model(b["img"]), b)
+    loss.backward()
+    torch.cuda.synchronize()
+    plan = model.__dict__["_ym_last_plan"]
+    st = stream_ptr(dev)
+    ws = plan.wgrad_ws()
+    rows = []
+    tot = [0.0, 0.0, 0.0]
+    for i, op in enumerate(plan.ops):
+        if type(op) is not ConvBN:
+            continue
+        d = op.desc
+        fl = op.flops()
+        ms = []
+        for kind in ("fwd", "dgrad", "wgrad"):
+            if kind == "dgrad" and not plan.needs_grad(op.x):
+                ms.append(0.0)
+                continue
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for r in range(args.reps + 2):
+                if r == 2:
+                    e0.record()
+                if kind == "fwd":
+                    call("ym_conv_fwd", ctypes.byref(d), op.x.ptr(), op.wf.data_ptr(), op.z.data_ptr(), None,
+                         op.ps[0].data_ptr(), op.ps[1].data_ptr(), st)
+                elif kind == "dgrad":
+                    call("ym_conv_dgrad", ctypes.byref(d), op.z.data_ptr(), op.wt.data_ptr(), op.x.gptr(), st)
+                else:
+                    call("ym_conv_wgrad", ctypes.byref(d), op.z.data_ptr(), op.x.ptr(), ws.data_ptr(),
+                         ws.numel() * 4, plan.gptr(op.m.conv.weight), 0, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1) / args.reps)
+        for j in range(3):
+            tot[j] += ms[j]
+        tf = [fl / (m * 1e-3) / 1e12 if m > 0 else 0.0 for m in ms]
+        rows.append((i, d.cin, d.cout, d.k, d.stride, d.oh, d.ow, fl / 1e9, ms, tf))
+    print(f"{'op':>4} {'cin':>4} {'cout':>4} k s {'out':>7} {'GFLOP':>7} | {'fwd ms':>7} {'TF/s':>5} | "
+          f"{'dgrad':>7} {'TF/s':>5} | {'wgrad':>7} {'TF/s':>5}")
+    for i, ci, co, k, s, oh, ow, gf, ms, tf in rows:
+        print(f"{i:4d} {ci:4d} {co:4d} {k} {s} {oh:3d}x{ow:<3d} {gf:7.1f} | {ms[0]:7.3f} {tf[0]:5.0f} | "
+              f"{ms[1]:7.3f} {tf[1]:5.0f} | {ms[2]:7.3f} {tf[2]:5.0f}")
+    print(f"total ms: fwd {tot[0]:.3f}  dgrad {tot[1]:.3f}  wgrad {tot[2]:.3f}")
+
+
+if __name__ == "__main__":
+    main()

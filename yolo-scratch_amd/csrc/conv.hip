@@ -310,60 +310,72 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
 }
 
 // ------------------------------------------------------------------ stem conv (Cin = 1), fp32 image input
-// y[n,oh,ow,co] = sum_t w[co][t] * img[n, oh*s-p+kh, ow*s-p+kw]; stats partials per block
+// one thread per (output pixel, 8 channels), the 8x9 weights in registers, 32-bit index math
+// (N*OH*OW and N*H*W < 2^31, checked on the host).  HBM-bound: writes the fp16 z (2 B/elem).
 __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __restrict__ img, const float* __restrict__ w,
-                                                             bf16_t* __restrict__ y, float* __restrict__ st_sum,
+                                                             uint16_t* __restrict__ y, float* __restrict__ st_sum,
                                                              float* __restrict__ st_sq, int N, int H, int W, int OH,
-                                                             int OW, int Cout, int K, int stride, int pad) {
-    // block: 256 threads = 8 channel-groups of 4... generic: thread -> (pixel, 4 channels)
-    extern __shared__ float smem[];
-    float* ws = smem;                        // Cout*K
-    float* red = smem + Cout * K;            // 2 * Cout
-    for (int i = threadIdx.x; i < Cout * K; i += blockDim.x) ws[i] = w[i];
-    for (int i = threadIdx.x; i < 2 * Cout; i += blockDim.x) red[i] = 0.f;
-    __syncthreads();
-    const int cg = Cout / 4;                 // channel groups per pixel
-    const int64_t M = int64_t(N) * OH * OW;
-    const int64_t total = M * cg;
-    float ls[4] = {0, 0, 0, 0}, lq[4] = {0, 0, 0, 0};
-    int my_cg = -1;
-    for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
-         idx += int64_t(gridDim.x) * blockDim.x) {
-        int g4 = int(idx % cg);
-        int64_t m = idx / cg;
-        my_cg = g4;   // blockDim multiple of cg keeps g4 fixed per thread
-        int64_t n = m / (int64_t(OH) * OW);
-        int64_t pix = m - n * OH * OW;
-        int oh = int(pix / OW), ow = int(pix % OW);
+                                                             int OW, int Cout, int stride, int pad) {
+    __shared__ float red[2][512];
+    const int G = Cout >> 3;                 // channel groups (divides 64)
+    const int g = threadIdx.x % G;
+    for (int i = threadIdx.x; i < 2 * Cout; i += 256) red[i / Cout][i % Cout] = 0.f;
+    float wr[8][9];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[r][t] = w[(g * 8 + r) * 9 + t];
+    float ls[8], lq[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) ls[r] = lq[r] = 0.f;
+    const int M = N * OH * OW, OHW = OH * OW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
         float patch[9];
-        for (int kh = 0, t = 0; kh < 3; ++kh)
-            for (int kw = 0; kw < 3; ++kw, ++t) {
-                int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                patch[t] = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[(n * H + ih) * W + iw] : 0.f;
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+                patch[kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
+                                         ? img[(n * H + ih) * W + iw] : 0.f;
             }
-        uint2 o;
-        float v[4];
-        for (int r = 0; r < 4; ++r) {
-            const float* wr_ = ws + (g4 * 4 + r) * K;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
             float s = 0.f;
-            for (int t = 0; t < K; ++t) s += wr_[t] * patch[t];
+#pragma unroll
+            for (int t = 0; t < 9; ++t) s += wr[r][t] * patch[t];
             v[r] = s;
             ls[r] += s;
             lq[r] += s * s;
         }
+        uint4 o;
         o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
         o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
-        *reinterpret_cast<uint2*>(y + m * Cout + g4 * 4) = o;
+        o.z = uint32_t(f2h(v[4])) | (uint32_t(f2h(v[5])) << 16);
+        o.w = uint32_t(f2h(v[6])) | (uint32_t(f2h(v[7])) << 16);
+        *reinterpret_cast<uint4*>(y + size_t(m) * Cout + g * 8) = o;
     }
-    if (my_cg >= 0)
-        for (int r = 0; r < 4; ++r) {
-            atomicAdd(&red[my_cg * 4 + r], ls[r]);
-            atomicAdd(&red[Cout + my_cg * 4 + r], lq[r]);
+    // lanes with the same channel group: xor-reduce over the other lane bits, then across waves
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+        for (int o = G; o < 64; o <<= 1) {
+            ls[r] += __shfl_xor(ls[r], o, 64);
+            lq[r] += __shfl_xor(lq[r], o, 64);
         }
     __syncthreads();
-    for (int c = threadIdx.x; c < Cout; c += blockDim.x) {
-        st_sum[int64_t(blockIdx.x) * Cout + c] = red[c];
-        st_sq[int64_t(blockIdx.x) * Cout + c] = red[Cout + c];
+    if ((threadIdx.x & 63) < G)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            atomicAdd(&red[0][g * 8 + r], ls[r]);
+            atomicAdd(&red[1][g * 8 + r], lq[r]);
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < Cout; c += 256) {
+        st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
     }
 }
 
@@ -371,39 +383,51 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
 __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __restrict__ dz, const float* __restrict__ img,
                                                                float* __restrict__ dw, int N, int H, int W, int OH,
                                                                int OW, int Cout, int stride, int pad) {
-    extern __shared__ float sred[];          // Cout*9
-    for (int i = threadIdx.x; i < Cout * 9; i += blockDim.x) sred[i] = 0.f;
-    __syncthreads();
-    const int cg = Cout / 4;
-    const int64_t M = int64_t(N) * OH * OW;
-    const int64_t total = M * cg;
-    float acc[4][9];
-    for (int r = 0; r < 4; ++r)
+    __shared__ float red[512 * 9];
+    const int G = Cout >> 3;
+    const int g = threadIdx.x % G;
+    for (int i = threadIdx.x; i < Cout * 9; i += 256) red[i] = 0.f;
+    float acc[8][9];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
         for (int t = 0; t < 9; ++t) acc[r][t] = 0.f;
-    int my_cg = -1;
-    for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < total;
-         idx += int64_t(gridDim.x) * blockDim.x) {
-        int g4 = int(idx % cg);
-        int64_t m = idx / cg;
-        my_cg = g4;
-        int64_t n = m / (int64_t(OH) * OW);
-        int64_t pix = m - n * OH * OW;
-        int oh = int(pix / OW), ow = int(pix % OW);
-        uint2 d = *reinterpret_cast<const uint2*>(dz + m * Cout + g4 * 4);
-        float g[4] = {bf2f(bf16_t(d.x & 0xffff)), bf2f(bf16_t(d.x >> 16)), bf2f(bf16_t(d.y & 0xffff)),
-                      bf2f(bf16_t(d.y >> 16))};
-        for (int kh = 0, t = 0; kh < 3; ++kh)
-            for (int kw = 0; kw < 3; ++kw, ++t) {
-                int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                float xv = (ih >= 0 && ih < H && iw >= 0 && iw < W) ? img[(n * H + ih) * W + iw] : 0.f;
-                for (int r = 0; r < 4; ++r) acc[r][t] += g[r] * xv;
+    const int M = N * OH * OW, OHW = OH * OW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
+        const uint4 d = *reinterpret_cast<const uint4*>(dz + size_t(m) * Cout + g * 8);
+        const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
+        float gv[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            gv[2 * e] = bf2f(bf16_t(dd[e] & 0xffff));
+            gv[2 * e + 1] = bf2f(bf16_t(dd[e] >> 16));
+        }
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+                const float xv = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
+                                     ? img[(n * H + ih) * W + iw] : 0.f;
+#pragma unroll
+                for (int r = 0; r < 8; ++r) acc[r][kh * 3 + kw] += gv[r] * xv;
             }
     }
-    if (my_cg >= 0)
-        for (int r = 0; r < 4; ++r)
-            for (int t = 0; t < 9; ++t) atomicAdd(&sred[(my_cg * 4 + r) * 9 + t], acc[r][t]);
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
     __syncthreads();
-    for (int i = threadIdx.x; i < Cout * 9; i += blockDim.x) atomicAdd(&dw[i], sred[i]);
+    if ((threadIdx.x & 63) < G)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) atomicAdd(&red[(g * 8 + r) * 9 + t], acc[r][t]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < Cout * 9; i += 256) atomicAdd(&dw[i], red[i]);
 }
 
 // ------------------------------------------------------------------ depthwise 3x3, stride 1, pad 1
@@ -417,68 +441,144 @@ struct DwArgs {
     int N, H, W, C;
 };
 
-__global__ void dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
-    // one thread per (pixel, channel); block = 256 channels-major threads
-    extern __shared__ float sh[];           // 2*C partials
-    for (int i = threadIdx.x; i < 2 * a.C; i += blockDim.x) sh[i] = 0.f;
-    __syncthreads();
-    const int64_t total = int64_t(a.N) * a.H * a.W * a.C;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int c = int(i % a.C);
-        int64_t m = i / a.C;
-        int64_t n = m / (int64_t(a.H) * a.W);
-        int64_t pix = m - n * a.H * a.W;
-        int h = int(pix / a.W), wcol = int(pix % a.W);
-        int sc = (c / a.gsz) * a.gstride + a.goff + c % a.gsz;
-        float s = 0.f;
-        for (int kh = 0; kh < 3; ++kh)
-            for (int kw = 0; kw < 3; ++kw) {
-                int ih = h - 1 + kh, iw = wcol - 1 + kw;
-                if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-                    s += a.w[c * 9 + kh * 3 + kw] * h2f(a.x[n * a.x_bs + (int64_t(ih) * a.W + iw) * a.x_ld + sc]);
-            }
-        a.y[m * a.C + c] = f2h(s);
-        atomicAdd(&sh[c], s);
-        atomicAdd(&sh[a.C + c], s * s);
-    }
-    __syncthreads();
-    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
-        st_sum[int64_t(blockIdx.x) * a.C + c] = sh[c];
-        st_sq[int64_t(blockIdx.x) * a.C + c] = sh[a.C + c];
+// one thread per (pixel, 8 channels): 16-B loads, the 8x9 weights in registers, statistics and
+// weight-gradient partials in registers, reduced once per thread (xor shuffles over the lanes
+// with the same channel group, then LDS) — no per-element atomics.  C/8 divides 256.
+__device__ __forceinline__ void unpack8(uint4 u, float* f, bool half) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        f[2 * e] = half ? h2f(uint16_t(w[e] & 0xffff)) : bf2f(bf16_t(w[e] & 0xffff));
+        f[2 * e + 1] = half ? h2f(uint16_t(w[e] >> 16)) : bf2f(bf16_t(w[e] >> 16));
     }
 }
 
-// dx (mapped channels, accumulate into view) and dW (atomic) from dense dz (N,H,W,C)
-__global__ void dw3x3_bwd_kernel(DwArgs a, const bf16_t* __restrict__ dz, float* __restrict__ dw, int accumulate) {
-    extern __shared__ float sh[];           // 9*C
-    for (int i = threadIdx.x; i < 9 * a.C; i += blockDim.x) sh[i] = 0.f;
-    __syncthreads();
-    const int64_t total = int64_t(a.N) * a.H * a.W * a.C;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int c = int(i % a.C);
-        int64_t m = i / a.C;
-        int64_t n = m / (int64_t(a.H) * a.W);
-        int64_t pix = m - n * a.H * a.W;
-        int h = int(pix / a.W), wcol = int(pix % a.W);
-        int sc = (c / a.gsz) * a.gstride + a.goff + c % a.gsz;
-        float gx = 0.f;
+__global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
+    __shared__ float red[2][512];
+    const int G = a.C >> 3, g = threadIdx.x % G;
+    for (int i = threadIdx.x; i < 2 * a.C; i += 256) red[i / a.C][i % a.C] = 0.f;
+    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    float wr[8][9];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[r][t] = a.w[(c0 + r) * 9 + t];
+    float ls[8], lq[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) ls[r] = lq[r] = 0.f;
+    const int HW = a.H * a.W, M = a.N * HW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / HW, pix = m - n * HW, h = pix / a.W, wc = pix - h * a.W;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
         for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = h - 1 + kh, iw = wc - 1 + kw;
+                if (unsigned(ih) < unsigned(a.H) && unsigned(iw) < unsigned(a.W)) {
+                    float xv[8];
+                    unpack8(*reinterpret_cast<const uint4*>(a.x + n * a.x_bs + int64_t(ih * a.W + iw) * a.x_ld + sc0),
+                            xv, true);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) s[r] += wr[r][kh * 3 + kw] * xv[r];
+                }
+            }
+        uint4 o;
+        o.x = uint32_t(f2h(s[0])) | (uint32_t(f2h(s[1])) << 16);
+        o.y = uint32_t(f2h(s[2])) | (uint32_t(f2h(s[3])) << 16);
+        o.z = uint32_t(f2h(s[4])) | (uint32_t(f2h(s[5])) << 16);
+        o.w = uint32_t(f2h(s[6])) | (uint32_t(f2h(s[7])) << 16);
+        *reinterpret_cast<uint4*>(a.y + size_t(m) * a.C + c0) = o;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) { ls[r] += s[r]; lq[r] += s[r] * s[r]; }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+        for (int o = G; o < 64; o <<= 1) {
+            ls[r] += __shfl_xor(ls[r], o, 64);
+            lq[r] += __shfl_xor(lq[r], o, 64);
+        }
+    __syncthreads();
+    if ((threadIdx.x & 63) < G)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            atomicAdd(&red[0][c0 + r], ls[r]);
+            atomicAdd(&red[1][c0 + r], lq[r]);
+        }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.C; c += 256) {
+        st_sum[int64_t(blockIdx.x) * a.C + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * a.C + c] = red[1][c];
+    }
+}
+
+// dx (mapped channels, overwrite or accumulate into the view) and dW (+=) from dense dz (N,H,W,C)
+__global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* __restrict__ dz, float* __restrict__ dw,
+                                                        int accumulate) {
+    __shared__ float red[512 * 9];
+    const int G = a.C >> 3, g = threadIdx.x % G;
+    for (int i = threadIdx.x; i < 9 * a.C; i += 256) red[i] = 0.f;
+    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    float wr[8][9], acc[8][9];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            wr[r][t] = a.w[(c0 + r) * 9 + t];
+            acc[r][t] = 0.f;
+        }
+    const int HW = a.H * a.W, M = a.N * HW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / HW, pix = m - n * HW, h = pix / a.W, wc = pix - h * a.W;
+        float d0[8], gx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        unpack8(*reinterpret_cast<const uint4*>(dz + size_t(m) * a.C + c0), d0, false);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
             for (int kw = 0; kw < 3; ++kw) {
                 // dx[h,w] += dz[h+1-kh, w+1-kw] * w[kh,kw]
-                int oh = h + 1 - kh, ow = wcol + 1 - kw;
-                if (oh >= 0 && oh < a.H && ow >= 0 && ow < a.W)
-                    gx += a.w[c * 9 + kh * 3 + kw] * bf2f(dz[(n * a.H * a.W + int64_t(oh) * a.W + ow) * a.C + c]);
+                const int oh = h + 1 - kh, ow = wc + 1 - kw;
+                if (unsigned(oh) < unsigned(a.H) && unsigned(ow) < unsigned(a.W)) {
+                    float dv[8];
+                    unpack8(*reinterpret_cast<const uint4*>(dz + size_t(n * HW + oh * a.W + ow) * a.C + c0), dv, false);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) gx[r] += wr[r][kh * 3 + kw] * dv[r];
+                }
                 // dW[kh,kw] += dz[h,w] * x[h-1+kh, w-1+kw]
-                int ih = h - 1 + kh, iw = wcol - 1 + kw;
-                if (ih >= 0 && ih < a.H && iw >= 0 && iw < a.W)
-                    atomicAdd(&sh[c * 9 + kh * 3 + kw],
-                              bf2f(dz[m * a.C + c]) * h2f(a.x[n * a.x_bs + (int64_t(ih) * a.W + iw) * a.x_ld + sc]));
+                const int ih = h - 1 + kh, iw = wc - 1 + kw;
+                if (unsigned(ih) < unsigned(a.H) && unsigned(iw) < unsigned(a.W)) {
+                    float xv[8];
+                    unpack8(*reinterpret_cast<const uint4*>(a.x + n * a.x_bs + int64_t(ih * a.W + iw) * a.x_ld + sc0),
+                            xv, true);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) acc[r][kh * 3 + kw] += d0[r] * xv[r];
+                }
             }
-        bf16_t* yp = a.y + n * a.y_bs + pix * a.y_ld + sc;
-        *yp = f2bf(accumulate ? bf2f(*yp) + gx : gx);
+        bf16_t* yp = a.y + n * a.y_bs + int64_t(pix) * a.y_ld + sc0;
+        if (accumulate) {
+            float old[8];
+            unpack8(*reinterpret_cast<const uint4*>(yp), old, false);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) gx[r] += old[r];
+        }
+        *reinterpret_cast<uint4*>(yp) = make_uint4(pk2bf(gx[0], gx[1]), pk2bf(gx[2], gx[3]), pk2bf(gx[4], gx[5]),
+                                                   pk2bf(gx[6], gx[7]));
     }
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+            for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
     __syncthreads();
-    for (int i = threadIdx.x; i < 9 * a.C; i += blockDim.x) atomicAdd(&dw[i], sh[i]);
+    if ((threadIdx.x & 63) < G)
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) atomicAdd(&red[(c0 + r) * 9 + t], acc[r][t]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 9 * a.C; i += 256) atomicAdd(&dw[i], red[i]);
 }
 
 // ------------------------------------------------------------------ weight preparation
@@ -611,29 +711,40 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
 extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
                                  int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
                                  void* stream) {
-    YM_CHECK_ARG(cout % 4 == 0 && 256 % (cout / 4) == 0, "ym_conv_first_fwd: cout=%d unsupported", cout);
-    size_t lds = (size_t(cout) * 9 + 2 * cout) * sizeof(float);
-    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), lds, as_stream(stream), img, w_oihw, y,
-                       stat_sum, stat_sq, n, h, w, oh, ow, cout, 9, stride, pad);
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd: cout=%d unsupported", cout);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+                 "ym_conv_first_fwd: too many pixels");
+    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
+                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad);
     YM_LAUNCH_CHECK("ym_conv_first_fwd");
     return YM_OK;
 }
 
 extern "C" int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh,
                                    int ow, int cout, int stride, int pad, void* stream) {
-    YM_CHECK_ARG(cout % 4 == 0 && 256 % (cout / 4) == 0, "ym_conv_first_wgrad: cout=%d unsupported", cout);
-    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(1024), dim3(256), size_t(cout) * 9 * sizeof(float),
-                       as_stream(stream), dz, img, dw_oihw, n, h, w, oh, ow, cout, stride, pad);
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_wgrad: cout=%d unsupported",
+                 cout);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+                 "ym_conv_first_wgrad: too many pixels");
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(1024), dim3(256), 0, as_stream(stream), dz, img, dw_oihw, n, h,
+                       w, oh, ow, cout, stride, pad);
     YM_LAUNCH_CHECK("ym_conv_first_wgrad");
     return YM_OK;
+}
+
+static bool dw_shape_ok(int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, int c) {
+    const int G = c / 8;
+    return c % 8 == 0 && G >= 1 && G <= 64 && (G & (G - 1)) == 0 && gsz % 8 == 0 && gstride % 8 == 0 &&
+           goff % 8 == 0 && x_bs % 8 == 0 && x_ld % 8 == 0;
 }
 
 extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
                             const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
                             int blocks, void* stream) {
+    YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
+                 "ym_dw3x3_fwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
     DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), size_t(2 * c) * sizeof(float), as_stream(stream), a,
-                       stat_sum, stat_sq);
+    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
     YM_LAUNCH_CHECK("ym_dw3x3_fwd");
     return YM_OK;
 }
@@ -641,9 +752,11 @@ extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
 extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
                             const float* w, const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw,
                             int n, int h, int wd, int c, int accumulate, void* stream) {
+    YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && dx_bs % 8 == 0 && dx_ld % 8 == 0 &&
+                     int64_t(n) * h * wd < (int64_t(1) << 31),
+                 "ym_dw3x3_bwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
     DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, dx, dx_bs, dx_ld, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(256), dim3(256), size_t(9 * c) * sizeof(float), as_stream(stream), a, dz,
-                       dw, accumulate);
+    hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(512), dim3(256), 0, as_stream(stream), a, dz, dw, accumulate);
     YM_LAUNCH_CHECK("ym_dw3x3_bwd");
     return YM_OK;
 }

@@ -46,89 +46,92 @@ int grid_for(int64_t work, int threads = 256, int cap = 8192) {
     return int(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
 }
 
-// ------------------------------------------------------------------ max pool 5x5, stride 1, pad 2
-__global__ void maxpool5_fwd_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld, bf16_t* __restrict__ y,
-                                    int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
-    const int cg = C / 8;
-    const int64_t total = int64_t(N) * H * W * cg;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int g = int(i % cg);
-        int64_t m = i / cg;
-        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
-        int h = int(pix / W), w = int(pix % W);
-        float mx[8];
+// ------------------------------------------------------------------ max pool 5x5, stride 1, pad 2 (SPPF)
+// SPPF's chained pools run on fp32 values (the first-max routing of the backward must see the
+// fp32 reference's ties).  Forward: one thread per (pixel, 4 channels), 32-bit index math; the
+// window argmax (kh*5 + kw, first maximum in kh-major scan order, NaN wins as in ATen's CPU
+// kernel) is kept as one byte per element so the backward is a gather instead of atomics.
+__global__ void __launch_bounds__(256) maxpool5_f32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               uint8_t* __restrict__ code, uint16_t* __restrict__ yv,
+                                                               int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
+    const int C4 = C >> 2;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N * H * W * C4) return;
+    const int c4 = i % C4, m = i / C4;
+    const int HW = H * W, n = m / HW, pix = m - n * HW, h = pix / W, w = pix - h * W;
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    uint32_t cd[4] = {0, 0, 0, 0};
+    bool first = true;
+    for (int dh = -2; dh <= 2; ++dh) {
+        const int ih = h + dh;
+        if (ih < 0 || ih >= H) continue;
+        for (int dw = -2; dw <= 2; ++dw) {
+            const int iw = w + dw;
+            if (iw < 0 || iw >= W) continue;
+            const float4 v = *reinterpret_cast<const float4*>(x + (size_t(n * HW + ih * W + iw) * C + c4 * 4));
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t k = uint32_t((dh + 2) * 5 + dw + 2);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) mx[k] = -INFINITY;
-        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
-            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
-                float v[8];
-                unpack8h(*reinterpret_cast<const uint4*>(x + n * x_bs + (int64_t(ih) * W + iw) * x_ld + g * 8), v);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) mx[k] = (v[k] > mx[k] || v[k] != v[k]) ? v[k] : mx[k];
-            }
-        *reinterpret_cast<uint4*>(y + n * y_bs + pix * y_ld + g * 8) = pack8h(mx);
+            for (int r = 0; r < 4; ++r)
+                if (first || vv[r] > mx[r] || vv[r] != vv[r]) { mx[r] = vv[r]; cd[r] = k; }
+            first = false;
+        }
     }
+    const size_t o = size_t(m) * C + c4 * 4;
+    *reinterpret_cast<float4*>(y + o) = make_float4(mx[0], mx[1], mx[2], mx[3]);
+    *reinterpret_cast<uint32_t*>(code + o) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
+    uint2 hv;
+    hv.x = uint32_t(f2h(mx[0])) | (uint32_t(f2h(mx[1])) << 16);
+    hv.y = uint32_t(f2h(mx[2])) | (uint32_t(f2h(mx[3])) << 16);
+    *reinterpret_cast<uint2*>(yv + n * y_bs + int64_t(pix) * y_ld + c4 * 4) = hv;
 }
 
-// fp32 chain for SPPF: y32 = maxpool(x32) and its bf16 copy into the concat slice
-__global__ void maxpool5_f32_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, bf16_t* __restrict__ yb,
-                                        int64_t y_bs, int64_t y_ld, int N, int H, int W, int C) {
-    const int64_t total = int64_t(N) * H * W * C;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int c = int(i % C);
-        int64_t m = i / C;
-        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
-        int h = int(pix / W), w = int(pix % W);
-        float mx = -INFINITY;
-        bool first = true;
-        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
-            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
-                float v = x[(n * H * W + int64_t(ih) * W + iw) * C + c];
-                if (v > mx || v != v || first) { mx = v; first = false; }
+// dx[p] = init[p] + sum of dy[q] over the windows q whose argmax is p (gather, no atomics);
+// out to a dense fp32 buffer and/or a bf16 gradient view (overwrite or accumulate)
+__global__ void __launch_bounds__(256) maxpool5_f32_bwd_kernel(const uint8_t* __restrict__ code,
+                                                               const float* __restrict__ dy,
+                                                               const uint16_t* __restrict__ init, int64_t i_bs,
+                                                               int64_t i_ld, float* __restrict__ dx,
+                                                               uint16_t* __restrict__ dxv, int64_t v_bs, int64_t v_ld,
+                                                               int accumulate, int N, int H, int W, int C) {
+    const int C4 = C >> 2;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N * H * W * C4) return;
+    const int c4 = i % C4, m = i / C4;
+    const int HW = H * W, n = m / HW, pix = m - n * HW, h = pix / W, w = pix - h * W;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int qh = h - 2; qh <= h + 2; ++qh) {
+        if (qh < 0 || qh >= H) continue;
+        for (int qw = w - 2; qw <= w + 2; ++qw) {
+            if (qw < 0 || qw >= W) continue;
+            const uint32_t want = uint32_t((h - qh + 2) * 5 + (w - qw + 2));
+            const size_t o = size_t(n * HW + qh * W + qw) * C + c4 * 4;
+            const uint32_t cq = *reinterpret_cast<const uint32_t*>(code + o);
+            const bool hit[4] = {(cq & 0xff) == want, ((cq >> 8) & 0xff) == want, ((cq >> 16) & 0xff) == want,
+                                 (cq >> 24) == want};
+            if (hit[0] | hit[1] | hit[2] | hit[3]) {
+                const float4 g = *reinterpret_cast<const float4*>(dy + o);
+                acc[0] += hit[0] ? g.x : 0.f;
+                acc[1] += hit[1] ? g.y : 0.f;
+                acc[2] += hit[2] ? g.z : 0.f;
+                acc[3] += hit[3] ? g.w : 0.f;
             }
-        y[m * C + c] = mx;
-        yb[n * y_bs + pix * y_ld + c] = f2h(mx);
+        }
     }
-}
-
-__global__ void maxpool5_f32_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                        float* __restrict__ dx, int N, int H, int W, int C) {
-    const int64_t total = int64_t(N) * H * W * C;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int c = int(i % C);
-        int64_t m = i / C;
-        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
-        int h = int(pix / W), w = int(pix % W);
-        float mx = -INFINITY;
-        int64_t arg = -1;
-        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
-            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
-                float v = x[(n * H * W + int64_t(ih) * W + iw) * C + c];
-                if (v > mx || v != v || arg < 0) { mx = v; arg = int64_t(ih) * W + iw; }
-            }
-        float g = dy[m * C + c];
-        if (g != 0.f) atomicAdd(&dx[(n * H * W + arg) * C + c], g);
+    if (init) {
+        const uint2 b = *reinterpret_cast<const uint2*>(init + n * i_bs + int64_t(pix) * i_ld + c4 * 4);
+        acc[0] += bf2f(bf16_t(b.x & 0xffff)); acc[1] += bf2f(bf16_t(b.x >> 16));
+        acc[2] += bf2f(bf16_t(b.y & 0xffff)); acc[3] += bf2f(bf16_t(b.y >> 16));
     }
-}
-
-// dx_f32[argmax] += dy_f32 (first maximal element in kh-major scan order, as ATen's CPU kernel)
-__global__ void maxpool5_bwd_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int64_t x_ld,
-                                    const float* __restrict__ dy, float* __restrict__ dx, int N, int H, int W, int C) {
-    const int64_t total = int64_t(N) * H * W * C;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int c = int(i % C);
-        int64_t m = i / C;
-        int64_t n = m / (int64_t(H) * W), pix = m - n * H * W;
-        int h = int(pix / W), w = int(pix % W);
-        float mx = -INFINITY;
-        int64_t arg = -1;
-        for (int ih = max(h - 2, 0); ih <= min(h + 2, H - 1); ++ih)
-            for (int iw = max(w - 2, 0); iw <= min(w + 2, W - 1); ++iw) {
-                float v = h2f(x[n * x_bs + (int64_t(ih) * W + iw) * x_ld + c]);
-                if (v > mx || v != v || arg < 0) { mx = v; arg = int64_t(ih) * W + iw; }
-            }
-        float g = dy[m * C + c];
-        if (g != 0.f) atomicAdd(&dx[(n * H * W + arg) * C + c], g);
+    if (dx) *reinterpret_cast<float4*>(dx + size_t(m) * C + c4 * 4) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (dxv) {
+        uint16_t* p = dxv + n * v_bs + int64_t(pix) * v_ld + c4 * 4;
+        if (accumulate) {
+            const uint2 b = *reinterpret_cast<const uint2*>(p);
+            acc[0] += bf2f(bf16_t(b.x & 0xffff)); acc[1] += bf2f(bf16_t(b.x >> 16));
+            acc[2] += bf2f(bf16_t(b.y & 0xffff)); acc[3] += bf2f(bf16_t(b.y >> 16));
+        }
+        *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(acc[0], acc[1]), pk2bf(acc[2], acc[3]));
     }
 }
 
@@ -544,35 +547,30 @@ using namespace ym;
 
 #define VIEW_ALIGNED(bs, ld) ((bs) % 8 == 0 && (ld) % 8 == 0)
 
-extern "C" int ym_maxpool5_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld,
-                               int n, int h, int w, int c, void* stream) {
-    YM_CHECK_ARG(c % 8 == 0 && VIEW_ALIGNED(x_bs, x_ld) && VIEW_ALIGNED(y_bs, y_ld), "ym_maxpool5_fwd: alignment");
-    hipLaunchKernelGGL(maxpool5_fwd_kernel, dim3(grid_for(int64_t(n) * h * w * (c / 8))), dim3(256), 0,
-                       as_stream(stream), x, x_bs, x_ld, y, y_bs, y_ld, n, h, w, c);
-    YM_LAUNCH_CHECK("ym_maxpool5_fwd");
-    return YM_OK;
-}
-
-extern "C" int ym_maxpool5_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, const float* dy, float* dx, int n, int h,
-                               int w, int c, void* stream) {
-    hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0, as_stream(stream), x,
-                       x_bs, x_ld, dy, dx, n, h, w, c);
-    YM_LAUNCH_CHECK("ym_maxpool5_bwd");
-    return YM_OK;
-}
-
-extern "C" int ym_maxpool5_f32_fwd(const float* x, float* y, uint16_t* yb, int64_t y_bs, int64_t y_ld, int n, int h,
-                                   int w, int c, void* stream) {
-    hipLaunchKernelGGL(maxpool5_f32_fwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0,
-                       as_stream(stream), x, y, yb, y_bs, y_ld, n, h, w, c);
+extern "C" int ym_maxpool5_f32_fwd(const float* x, float* y, uint8_t* code, uint16_t* yv, int64_t y_bs,
+                                   int64_t y_ld, int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(x && y && code && yv, "ym_maxpool5_f32_fwd: null argument");
+    YM_CHECK_ARG(c % 4 == 0 && y_bs % 4 == 0 && y_ld % 4 == 0, "ym_maxpool5_f32_fwd: alignment");
+    const int64_t t = int64_t(n) * h * w * (c / 4);
+    YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_maxpool5_f32_fwd: too large");
+    if (t == 0) return YM_OK;
+    hipLaunchKernelGGL(maxpool5_f32_fwd_kernel, dim3(unsigned((t + 255) / 256)), dim3(256), 0, as_stream(stream), x, y,
+                       code, yv, y_bs, y_ld, n, h, w, c);
     YM_LAUNCH_CHECK("ym_maxpool5_f32_fwd");
     return YM_OK;
 }
 
-extern "C" int ym_maxpool5_f32_bwd(const float* x, const float* dy, float* dx, int n, int h, int w, int c,
-                                   void* stream) {
-    hipLaunchKernelGGL(maxpool5_f32_bwd_kernel, dim3(grid_for(int64_t(n) * h * w * c)), dim3(256), 0,
-                       as_stream(stream), x, dy, dx, n, h, w, c);
+extern "C" int ym_maxpool5_f32_bwd(const uint8_t* code, const float* dy, const uint16_t* init, int64_t i_bs,
+                                   int64_t i_ld, float* dx, uint16_t* dxv, int64_t v_bs, int64_t v_ld, int accumulate,
+                                   int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(code && dy && (dx || dxv), "ym_maxpool5_f32_bwd: null argument");
+    YM_CHECK_ARG(c % 4 == 0 && i_bs % 4 == 0 && i_ld % 4 == 0 && v_bs % 4 == 0 && v_ld % 4 == 0,
+                 "ym_maxpool5_f32_bwd: alignment");
+    const int64_t t = int64_t(n) * h * w * (c / 4);
+    YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_maxpool5_f32_bwd: too large");
+    if (t == 0) return YM_OK;
+    hipLaunchKernelGGL(maxpool5_f32_bwd_kernel, dim3(unsigned((t + 255) / 256)), dim3(256), 0, as_stream(stream), code,
+                       dy, init, i_bs, i_ld, dx, dxv, v_bs, v_ld, accumulate, n, h, w, c);
     YM_LAUNCH_CHECK("ym_maxpool5_f32_bwd");
     return YM_OK;
 }

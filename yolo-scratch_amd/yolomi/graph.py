@@ -404,33 +404,32 @@ class SPPFPools:
         x = slices[0]
         self.M, self.C, self.H, self.W = x.M, x.c, x.H, x.W
         self.P = torch.empty(4, self.M, self.C, dtype=F32, device=plan.dev)   # fp32 chain values
+        self.code = torch.empty(3, self.M, self.C, dtype=torch.uint8, device=plan.dev)   # window argmax
         self.G = torch.empty(2, self.M, self.C, dtype=F32, device=plan.dev)   # grad ping-pong
         cv1_op.out32 = self.P[0]
 
     def forward(self, plan, st):
         for j in range(3):
             y = self.slices[j + 1]
-            call("ym_maxpool5_f32_fwd", self.P[j].data_ptr(), self.P[j + 1].data_ptr(), y.ptr(), y.bs, y.ld, plan.B,
-                 self.H, self.W, self.C, st)
+            call("ym_maxpool5_f32_fwd", self.P[j].data_ptr(), self.P[j + 1].data_ptr(), self.code[j].data_ptr(),
+                 y.ptr(), y.bs, y.ld, plan.B, self.H, self.W, self.C, st)
 
     def backward(self, plan, st):
         HW = self.H * self.W
         cur = self.G[0]
         s3 = self.slices[3]
         call("ym_view_to_f32", s3.grad_for_read(st), s3.bs, s3.ld, cur.data_ptr(), self.M, self.C, HW, st)
-        for j in (2, 1, 0):
+        # pool j's output grad = its concat slice grad + the next pool's routed grad
+        for j in (2, 1):
             nxt = self.G[(3 - j) % 2]
             sj = self.slices[j]
-            if j > 0:
-                call("ym_view_to_f32", sj.grad_for_read(st), sj.bs, sj.ld, nxt.data_ptr(), self.M, self.C, HW, st)
-            else:
-                nxt.zero_()
-            call("ym_maxpool5_f32_bwd", self.P[j].data_ptr(), cur.data_ptr(), nxt.data_ptr(), plan.B, self.H, self.W,
-                 self.C, st)
+            call("ym_maxpool5_f32_bwd", self.code[j].data_ptr(), cur.data_ptr(), sj.grad_for_read(st), sj.bs, sj.ld,
+                 nxt.data_ptr(), None, 0, 0, 0, plan.B, self.H, self.W, self.C, st)
             cur = nxt
         s0 = self.slices[0]
         acc = s0.grad_for_write(st)
-        call("ym_f32_to_view", cur.data_ptr(), s0.gptr(), s0.bs, s0.ld, self.M, self.C, HW, acc, st)
+        call("ym_maxpool5_f32_bwd", self.code[0].data_ptr(), cur.data_ptr(), None, 0, 0, None, s0.gptr(), s0.bs, s0.ld,
+             acc, plan.B, self.H, self.W, self.C, st)
         s0.mark()
 
 
