@@ -35,7 +35,6 @@ namespace {
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
 constexpr int BK = 64;   // k per LDS stage = two MFMA k-steps
-constexpr int NCH = BK / 8;
 
 struct GemmArgs {
     const bf16_t* x; int64_t x_bs, x_ld;    // gathered activation view
@@ -53,29 +52,48 @@ struct GemmArgs {
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
 };
 
-// LDS row slot of (row, chunk): row ^ g(c), g = {0,1,2,3,12,13,14,15}.  A staging write group
-// (8 lanes = one row, chunks 0..7) hits 8 distinct 16-B slots mod 16, and a ds_read_b128 lane
-// group (chunk 2j: rows {0-3,12-15}, chunk 2j+1: rows {4-11}, or the converse) stays a
-// permutation of the 16 slots because every g keeps bit2 == bit3.
-__device__ __forceinline__ int swz(int row, int c) { return row ^ (c + ((c & 4) << 1)); }
+// LDS images are lane-linear (LDS-DMA writes lane l of a wave-instruction at base + 16*l): 128-B
+// rows of 8 16-B slots, row r's chunk c stored in slot c ^ f(r), f(r) = (r >> 1) & 7.  The swizzle
+// lives on the global (source) side: a DMA lane that fills slot s of row r loads chunk s ^ f(r), so
+// each 8-lane group still reads one whole 128-B row.  A ds_read_b128 lane group (rows {0-3,12-15}
+// at chunk c, rows {4-11} at chunk c^1) then covers 16 distinct (row parity, slot) bank quads.
+__device__ __forceinline__ int fsw(int r) { return (r >> 1) & 7; }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
+// workgroup barrier without the vmcnt(0) drain __syncthreads() implies; LDS-DMA ordering is
+// the caller's (counted wait_vmcnt before it), the asm clobbers keep LDS accesses on their side
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+#ifndef YM_CONV_STAGES
+#define YM_CONV_STAGES 2
+#endif
 
 template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
+__global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_kernel(GemmArgs a) {
     constexpr int TM = BN / 32;          // 16-channel subtiles per wave
     constexpr int TN = BM / 32;          // 16-pixel subtiles per wave
-    constexpr int A_ITEMS = BN * NCH / 256;
-    constexpr int B_ITEMS = BM * NCH / 256;
-    static_assert(A_ITEMS >= 1 && B_ITEMS >= 1, "tile too small for the staging map");
-    __shared__ uint4 As[2][NCH][BN];
-    __shared__ uint4 Bs[2][NCH][BM];
-    __shared__ float red[2][2][BN];      // [sum|sq][wave pixel half][channel]
+    constexpr int AI = BN / 32;          // A (weight) DMA instructions per wave per stage (8 rows each)
+    constexpr int BI = BM / 32;          // B (activation) DMA instructions per wave per stage
+    constexpr int STAGE = (BM + BN) * 128;
+    constexpr int NSTAGE = YM_CONV_STAGES;   // LDS ring depth: NSTAGE-1 stages in flight
+    static_assert(AI >= 1 && BI >= 1, "tile too small for the staging map");
+    // one LDS array (a second __shared__ object can de-pipeline LDS-DMA, cdna_hip_programming.md §5)
+    __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
     const int fc = lane >> 4, fr = lane & 15;
-    const int sc = tid & (NCH - 1);      // 16-B chunk this thread stages (fixed)
-    const int srow = tid / NCH;          // first staged row; item it adds 256/NCH*it
-    constexpr int RSTEP = 256 / NCH;
     const int n0 = blockIdx.y * BN;
     const int kc = (a.Kin + BK - 1) / BK;
     // output pixel mapping: oh = i*os + py, ow = j*os + px over a class grid OHc x OWc;
@@ -93,12 +111,16 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
     const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
     const uint32_t xld_b = uint32_t(a.x_ld) * 2u;
 
+    // DMA geometry: instruction j of this wave fills rows (wave*I + j)*8 + lane/8, slot lane%8
+    const int lrow = lane >> 3, lslot = lane & 7;
     const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
-    uint32_t a_off[A_ITEMS];
+    uint32_t a_off[AI], a_chk[AI];
 #pragma unroll
-    for (int it = 0; it < A_ITEMS; ++it) {
-        const int ch = n0 + srow + RSTEP * it;
-        a_off[it] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t(sc) * 16u : OOB;
+    for (int j = 0; j < AI; ++j) {
+        const int r = (wave * AI + j) * 8 + lrow;
+        const int ch = n0 + r;
+        a_chk[j] = uint32_t(lslot ^ fsw(r)) * 8u;          // chunk (in elements) this lane loads
+        a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b : OOB;
     }
 
     float ssum[TM][4], ssq[TM][4];
@@ -117,65 +139,61 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
         const uint32_t nfirst = uint32_t(m0 / OHW);
         const __amdgpu_buffer_rsrc_t xres =
             make_rsrc(a.x + int64_t(nfirst) * a.x_bs, (int64_t(a.N) - nfirst) * a.x_bs * 2);
-        int b_oh[B_ITEMS], b_ow[B_ITEMS];
-        uint32_t b_img[B_ITEMS], b_off[B_ITEMS];
+        int b_oh[BI], b_ow[BI];
+        uint32_t b_img[BI], b_off[BI], b_chk[BI];
 #pragma unroll
-        for (int it = 0; it < B_ITEMS; ++it) {
-            const int64_t m = m0 + srow + RSTEP * it;
+        for (int j = 0; j < BI; ++j) {
+            const int r = (wave * BI + j) * 8 + lrow;
+            const int64_t m = m0 + r;
             const uint32_t um = m < Mc ? uint32_t(m) : 0u;
             const uint32_t n = um / OHW, pix = um - n * OHW;
             const uint32_t i = pix / uint32_t(OWc);
-            b_img[it] = m < Mc ? (n - nfirst) * uint32_t(a.x_bs) * 2u + uint32_t(sc) * 16u : OOB;
-            b_oh[it] = int(i) * os + py;
-            b_ow[it] = int(pix - i * uint32_t(OWc)) * os + px;
+            b_chk[j] = uint32_t(lslot ^ fsw(r)) * 8u;
+            b_img[j] = m < Mc ? (n - nfirst) * uint32_t(a.x_bs) * 2u : OOB;
+            b_oh[j] = int(i) * os + py;
+            b_ow[j] = int(pix - i * uint32_t(OWc)) * os + px;
         }
         auto tap_setup = [&](int t) {
             const int ti = t / nkw;
             const int kh = kh0 + ti * os, kw = kw0 + (t - ti * nkw) * os;
 #pragma unroll
-            for (int it = 0; it < B_ITEMS; ++it) {
+            for (int j = 0; j < BI; ++j) {
                 int gh, gw;
                 if (MODE == MODE_FWD) {
-                    gh = b_oh[it] * a.stride - a.pad + kh;
-                    gw = b_ow[it] * a.stride - a.pad + kw;
+                    gh = b_oh[j] * a.stride - a.pad + kh;
+                    gw = b_ow[j] * a.stride - a.pad + kw;
                 } else {                       // th, tw are multiples of the stride here
-                    gh = (b_oh[it] + a.pad - kh) >> (a.stride - 1);
-                    gw = (b_ow[it] + a.pad - kw) >> (a.stride - 1);
+                    gh = (b_oh[j] + a.pad - kh) >> (a.stride - 1);
+                    gw = (b_ow[j] + a.pad - kw) >> (a.stride - 1);
                 }
-                const bool ok = b_img[it] != OOB && gh >= 0 && gh < a.GH && gw >= 0 && gw < a.GW;
-                b_off[it] = ok ? b_img[it] + uint32_t(gh * a.GW + gw) * xld_b : OOB;
+                const bool ok = b_img[j] != OOB && gh >= 0 && gh < a.GH && gw >= 0 && gw < a.GW;
+                b_off[j] = ok ? b_img[j] + uint32_t(gh * a.GW + gw) * xld_b : OOB;
             }
             return uint32_t((kh * a.KW + kw) * a.Kin) * 2u;
         };
-        uint4 ra[A_ITEMS], rb[B_ITEMS];
         int t_next = 0, c_next = 0;
         uint32_t a_tap = 0;
-        auto load = [&]() {
+        // issue one stage of LDS-DMA: AI + BI buffer_load_dwordx4 ... lds per wave
+        auto issue = [&](int buf) {
             if (c_next == 0) a_tap = tap_setup(t_next);
             const int k0 = c_next * BK;
-            const bool in_k = k0 + 8 * sc < a.Kin;
-            const uint32_t kb = uint32_t(k0) * 2u;
+            char* st = smem + buf * STAGE;
 #pragma unroll
-            for (int it = 0; it < A_ITEMS; ++it)
-                ra[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       wres, in_k && a_off[it] != OOB ? a_off[it] + a_tap + kb : OOB, 0, 0));
+            for (int j = 0; j < AI; ++j) {
+                const uint32_t kk = uint32_t(k0) + a_chk[j];
+                const uint32_t off = (kk < uint32_t(a.Kin) && a_off[j] != OOB) ? a_off[j] + a_tap + kk * 2u : OOB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    wres, (__attribute__((address_space(3))) void*)(st + (wave * AI + j) * 1024), 16, off, 0, 0, 0);
+            }
 #pragma unroll
-            for (int it = 0; it < B_ITEMS; ++it)
-                rb[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       xres, in_k && b_off[it] != OOB ? b_off[it] + kb : OOB, 0, 0));
+            for (int j = 0; j < BI; ++j) {
+                const uint32_t kk = uint32_t(k0) + b_chk[j];
+                const uint32_t off = (kk < uint32_t(a.Kin) && b_off[j] != OOB) ? b_off[j] + kk * 2u : OOB;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    xres, (__attribute__((address_space(3))) void*)(st + BN * 128 + (wave * BI + j) * 1024), 16, off,
+                    0, 0, 0);
+            }
             if (++c_next == kc) { c_next = 0; ++t_next; }
-        };
-        auto store = [&](int buf) {
-#pragma unroll
-            for (int it = 0; it < A_ITEMS; ++it) {
-                const int row = srow + RSTEP * it;
-                As[buf][sc][swz(row, sc)] = ra[it];
-            }
-#pragma unroll
-            for (int it = 0; it < B_ITEMS; ++it) {
-                const int row = srow + RSTEP * it;
-                Bs[buf][sc][swz(row, sc)] = rb[it];
-            }
         };
 
         f32x4 acc[TM][TN];
@@ -185,23 +203,33 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
             for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         // nk == 0: a parity class no tap reaches (1x1 stride-2): zero gradient
-        if (nk > 0) load();
-        __syncthreads();     // previous tile's readers are done with both buffers
-        if (nk > 0) store(0);
-        __syncthreads();
+        raw_barrier();                     // previous tile's readers are done with every stage
+#pragma unroll
+        for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
+            if (s0 < nk) issue(s0);
         for (int k = 0; k < nk; ++k) {
-            const int buf = k & 1;
-            if (k + 1 < nk) load();
+            const int buf = k % NSTAGE;
+            // this wave's DMAs of stage k have landed (the later stages may stay in flight)
+            if (NSTAGE == 3 && k + 1 < nk) wait_vmcnt<AI + BI>();
+            else wait_vmcnt<0>();
+            raw_barrier();                 // ... everyone's, and everyone finished reading stage k-1
+            if (k + NSTAGE - 1 < nk) issue((k + NSTAGE - 1) % NSTAGE);
+            const char* As = smem + buf * STAGE;
+            const char* Bs = As + BN * 128;
 #pragma unroll
             for (int kk = 0; kk < BK / 32; ++kk) {
                 const int cch = kk * 4 + fc;
                 bf16x8 af[TM], bfr[TN];
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    af[i] = __builtin_bit_cast(bf16x8, As[buf][cch][swz(wr * (BN / 2) + i * 16 + fr, cch)]);
+                for (int i = 0; i < TM; ++i) {
+                    const int r = wr * (BN / 2) + i * 16 + fr;
+                    af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((cch ^ fsw(r)) << 4));
+                }
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    bfr[j] = __builtin_bit_cast(bf16x8, Bs[buf][cch][swz(wc * (BM / 2) + j * 16 + fr, cch)]);
+                for (int j = 0; j < TN; ++j) {
+                    const int r = wc * (BM / 2) + j * 16 + fr;
+                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((cch ^ fsw(r)) << 4));
+                }
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -214,8 +242,6 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
                     }
             }
-            if (k + 1 < nk) store(buf ^ 1);
-            __syncthreads();
         }
 
         // epilogue: D[channel][pixel]; lane holds 4 consecutive channels of one pixel
@@ -281,6 +307,8 @@ __global__ void __launch_bounds__(256, 2) conv_gemm_kernel(GemmArgs a) {
     }
 
     if (a.st_sum) {
+        float (*red)[2][BN] = reinterpret_cast<float (*)[2][BN]>(smem);   // [sum|sq][wave pixel half][channel]
+        raw_barrier();                     // staging LDS is free again
         // reduce over the 16 pixel lanes, then over the two pixel-half waves
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -631,23 +659,32 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
 
 using namespace ym;
 
+// widest channel tile that still gives >= 1.5 workgroups per CU (small late layers: 20x20 maps)
+static int pick_bn(int64_t blocks_per_ntile, int nout) {
+    int bn = nout >= 128 ? 128 : (nout >= 64 ? 64 : 32);
+    while (bn > 32 && blocks_per_ntile * ((nout + bn - 1) / bn) < 384) bn >>= 1;
+    return bn;
+}
+
 static int pick_and_launch(GemmArgs a, int mode, int max_blocks, hipStream_t st) {
-    // channel tile from the output channel count
+    const int os = a.ostep;
+    const int64_t Mc = int64_t(a.N) * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);
+    const int bn = pick_bn(((Mc + 127) / 128) * (os == 2 ? 4 : 1), a.Nout);
     if (mode == MODE_FWD) {
-        if (a.Nout >= 128) return launch_gemm<128, 128, MODE_FWD>(a, max_blocks, st);
-        if (a.Nout >= 64) return launch_gemm<128, 64, MODE_FWD>(a, max_blocks, st);
+        if (bn == 128) return launch_gemm<128, 128, MODE_FWD>(a, max_blocks, st);
+        if (bn == 64) return launch_gemm<128, 64, MODE_FWD>(a, max_blocks, st);
         return launch_gemm<128, 32, MODE_FWD>(a, max_blocks, st);
     }
-    if (a.Nout >= 128) return launch_gemm<128, 128, MODE_DGRAD>(a, max_blocks, st);
-    if (a.Nout >= 64) return launch_gemm<128, 64, MODE_DGRAD>(a, max_blocks, st);
+    if (bn == 128) return launch_gemm<128, 128, MODE_DGRAD>(a, max_blocks, st);
+    if (bn == 64) return launch_gemm<128, 64, MODE_DGRAD>(a, max_blocks, st);
     return launch_gemm<128, 32, MODE_DGRAD>(a, max_blocks, st);
 }
 
 extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     // grid-x used for the stats partials by ym_conv_fwd (callers size the partial buffers with it)
-    int BN = Cout >= 128 ? 128 : (Cout >= 64 ? 64 : 32);
-    int ntiles = (Cout + BN - 1) / BN;
-    int mtiles = int((M + 127) / 128);
+    const int mtiles = int((M + 127) / 128);
+    const int BN = pick_bn(mtiles, Cout);
+    const int ntiles = (Cout + BN - 1) / BN;
     return grid_x(mtiles, ntiles, true, 2048);
 }
 

@@ -1,7 +1,6 @@
 // Non-GEMM graph ops of the YOLOv11 neck/backbone, NHWC bf16 (gfx950):
 //   SPPF max-pool 5x5 s1 p2 fwd/bwd     (yolo11_modules.py:92-105)
 //   nearest 2x upsample fwd/bwd         (configs/yolo11n_crater.yaml head rows 0, 3; nn.Upsample)
-//   C2PSA attention core fwd/bwd        (yolo11_modules.py:124-136): softmax(q^T k * kd^-0.5), v attn^T
 //   dtype/view conversions and the Detect-head gradient split (+ bias grads)
 // Activation buffers are fp16, gradient buffers bf16 (see yolomi/graph.py).
 #include <algorithm>
@@ -275,271 +274,6 @@ __global__ void head_grad_kernel(const float* __restrict__ dh, int64_t A, int64_
     }
 }
 
-// ------------------------------------------------------------------ attention core (flash-style, fp32 VALU)
-constexpr int KD = 32, HD = 64, QT = 64;
-
-struct AttnArgs {
-    const bf16_t* qkv; int64_t q_bs, q_ld;   // per head h: q = h*(2KD+HD) + [0,KD), k = +KD, v = +2KD
-    int N, heads;
-    float scale;
-};
-
-__global__ void __launch_bounds__(256) attn_fwd_kernel(AttnArgs a, bf16_t* __restrict__ out, int64_t o_bs, int64_t o_ld,
-                                                       float* __restrict__ lse) {
-    __shared__ float Ks[QT][KD + 1];
-    __shared__ float Vs[QT][HD + 1];
-    __shared__ float Ps[QT][QT + 1];
-    const int t = threadIdx.x, qi = t >> 2, sub = t & 3;
-    const int h = blockIdx.y, b = blockIdx.z;
-    const int i = blockIdx.x * QT + qi;
-    const int hs = 2 * KD + HD;
-    const bf16_t* base = a.qkv + int64_t(b) * a.q_bs + h * hs;
-    float q[KD];
-    if (i < a.N) {
-#pragma unroll
-        for (int c = 0; c < KD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(i) * a.q_ld + c * 8), q + c * 8);
-    } else {
-#pragma unroll
-        for (int d = 0; d < KD; ++d) q[d] = 0.f;
-    }
-    float o[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) o[e] = 0.f;
-    float m = -INFINITY, l = 0.f;
-    for (int k0 = 0; k0 < a.N; k0 += QT) {
-        {   // K tile: 64 keys x 32 d
-            int key = t >> 2, d0 = (t & 3) * 8;
-            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (k0 + key < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(k0 + key) * a.q_ld + KD + d0), v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) Ks[key][d0 + e] = v[e];
-        }
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {   // V tile: 64 keys x 64 d
-            int id = t + 256 * it, key = id >> 3, d0 = (id & 7) * 8;
-            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (k0 + key < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(k0 + key) * a.q_ld + 2 * KD + d0), v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) Vs[key][d0 + e] = v[e];
-        }
-        __syncthreads();
-        float s[16];
-        float tmax = -INFINITY;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            int kk = sub * 16 + e;
-            float acc = 0.f;
-#pragma unroll
-            for (int d = 0; d < KD; ++d) acc += q[d] * Ks[kk][d];
-            s[e] = (k0 + kk < a.N) ? acc * a.scale : -INFINITY;
-            tmax = fmaxf(tmax, s[e]);
-        }
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 1, 64));
-        tmax = fmaxf(tmax, __shfl_xor(tmax, 2, 64));
-        const float mn = fmaxf(m, tmax);
-        const float alpha = __expf(m - mn);
-        float psum = 0.f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            float p = __expf(s[e] - mn);
-            Ps[qi][sub * 16 + e] = p;
-            psum += p;
-        }
-        psum += __shfl_xor(psum, 1, 64);
-        psum += __shfl_xor(psum, 2, 64);
-        l = l * alpha + psum;
-        m = mn;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[e] *= alpha;
-        __syncthreads();
-        for (int kk = 0; kk < QT; ++kk) {
-            float p = Ps[qi][kk];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) o[e] += p * Vs[kk][sub * 16 + e];
-        }
-        __syncthreads();
-    }
-    if (i < a.N) {
-        float inv = 1.0f / l;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[e] *= inv;
-        bf16_t* op = out + int64_t(b) * o_bs + int64_t(i) * o_ld + h * HD + sub * 16;
-        *reinterpret_cast<uint4*>(op) = pack8h(o);
-        *reinterpret_cast<uint4*>(op + 8) = pack8h(o + 8);
-        if (sub == 0) lse[(int64_t(b) * a.heads + h) * a.N + i] = m + __logf(l);
-    }
-}
-
-// D[b,h,i] = sum_d dO[i][h*HD+d] * O[i][h*HD+d]
-__global__ void attn_bwd_pre_kernel(const bf16_t* __restrict__ o, int64_t o_bs, int64_t o_ld, const bf16_t* __restrict__ dout,
-                                    int64_t d_bs, int64_t d_ld, int B, int heads, int N, float* __restrict__ D) {
-    int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (idx >= int64_t(B) * heads * N) return;
-    int i = int(idx % N);
-    int h = int((idx / N) % heads);
-    int b = int(idx / (int64_t(N) * heads));
-    float s = 0.f;
-    for (int c = 0; c < HD / 8; ++c) {
-        float x[8], y[8];
-        unpack8h(*reinterpret_cast<const uint4*>(o + int64_t(b) * o_bs + int64_t(i) * o_ld + h * HD + c * 8), x);
-        unpack8(*reinterpret_cast<const uint4*>(dout + int64_t(b) * d_bs + int64_t(i) * d_ld + h * HD + c * 8), y);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += x[k] * y[k];
-    }
-    D[idx] = s;
-}
-
-// block owns 64 keys of one (b, h); loops over query tiles; dq via fp32 atomics
-__global__ void __launch_bounds__(256) attn_bwd_kernel(AttnArgs a, const bf16_t* __restrict__ dout, int64_t d_bs,
-                                                       int64_t d_ld, const float* __restrict__ lse,
-                                                       const float* __restrict__ D, bf16_t* __restrict__ dqkv,
-                                                       int64_t g_bs, int64_t g_ld, float* __restrict__ dq,
-                                                       int acc_k, int acc_v) {
-    __shared__ float Qs[QT][KD + 1];
-    __shared__ float dOs[QT][HD + 1];
-    __shared__ float Ks[QT][KD + 1];
-    __shared__ float PT[QT][QT + 1];
-    __shared__ float dST[QT][QT + 1];
-    __shared__ float Ls[QT], Ds[QT];
-    const int t = threadIdx.x, kk = t >> 2, sub = t & 3;
-    const int h = blockIdx.y, b = blockIdx.z;
-    const int j = blockIdx.x * QT + kk;
-    const int hs = 2 * KD + HD;
-    const bf16_t* base = a.qkv + int64_t(b) * a.q_bs + h * hs;
-    float kr[KD], vr[HD];
-    if (j < a.N) {
-#pragma unroll
-        for (int c = 0; c < KD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(j) * a.q_ld + KD + c * 8), kr + c * 8);
-#pragma unroll
-        for (int c = 0; c < HD / 8; ++c) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(j) * a.q_ld + 2 * KD + c * 8), vr + c * 8);
-    } else {
-#pragma unroll
-        for (int d = 0; d < KD; ++d) kr[d] = 0.f;
-#pragma unroll
-        for (int d = 0; d < HD; ++d) vr[d] = 0.f;
-    }
-    {   // K tile in LDS for the dq product
-        int key = t >> 2, d0 = (t & 3) * 8;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Ks[key][d0 + e] = kr[d0 + e];
-    }
-    float dk[8], dv[16];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) dk[e] = 0.f;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) dv[e] = 0.f;
-    const float* lse_bh = lse + (int64_t(b) * a.heads + h) * a.N;
-    const float* D_bh = D + (int64_t(b) * a.heads + h) * a.N;
-    for (int q0 = 0; q0 < a.N; q0 += QT) {
-        {
-            int qq = t >> 2, d0 = (t & 3) * 8;
-            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (q0 + qq < a.N) unpack8h(*reinterpret_cast<const uint4*>(base + int64_t(q0 + qq) * a.q_ld + d0), v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) Qs[qq][d0 + e] = v[e];
-        }
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            int id = t + 256 * it, qq = id >> 3, d0 = (id & 7) * 8;
-            float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (q0 + qq < a.N)
-                unpack8(*reinterpret_cast<const uint4*>(dout + int64_t(b) * d_bs + int64_t(q0 + qq) * d_ld + h * HD + d0), v);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dOs[qq][d0 + e] = v[e];
-        }
-        if (t < QT) {
-            bool ok = q0 + t < a.N;
-            Ls[t] = ok ? lse_bh[q0 + t] : INFINITY;
-            Ds[t] = ok ? D_bh[q0 + t] : 0.f;
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int e = 0; e < 16; ++e) {
-            int qi = sub * 16 + e;
-            float s = 0.f, dp = 0.f;
-#pragma unroll
-            for (int d = 0; d < KD; ++d) s += Qs[qi][d] * kr[d];
-#pragma unroll
-            for (int d = 0; d < HD; ++d) dp += dOs[qi][d] * vr[d];
-            float p = (j < a.N) ? __expf(s * a.scale - Ls[qi]) : 0.f;
-            PT[kk][qi] = p;
-            dST[kk][qi] = p * (dp - Ds[qi]);
-        }
-        __syncthreads();
-        for (int qi = 0; qi < QT; ++qi) {
-            float p = PT[kk][qi], ds = dST[kk][qi];
-#pragma unroll
-            for (int e = 0; e < 16; ++e) dv[e] += p * dOs[qi][sub * 16 + e];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dk[e] += ds * Qs[qi][sub * 8 + e];
-        }
-        {   // dq for query (t>>2), d in sub*8 .. +8
-            int qi = t >> 2;
-            if (q0 + qi < a.N) {
-                float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                for (int k2 = 0; k2 < QT; ++k2) {
-                    float ds = dST[k2][qi];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) acc[e] += ds * Ks[k2][sub * 8 + e];
-                }
-                float* dqp = dq + (int64_t(b) * a.N + q0 + qi) * (a.heads * KD) + h * KD + sub * 8;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) atomicAdd(dqp + e, acc[e] * a.scale);
-            }
-        }
-        __syncthreads();
-    }
-    if (j < a.N) {
-        bf16_t* g = dqkv + int64_t(b) * g_bs + int64_t(j) * g_ld + h * hs;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dk[e] *= a.scale;
-        bf16_t* pk = g + KD + sub * 8;
-        bf16_t* pv = g + 2 * KD + sub * 16;
-        if (acc_k) {
-            float u[8];
-            unpack8(*reinterpret_cast<const uint4*>(pk), u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dk[e] += u[e];
-        }
-        if (acc_v) {
-            float u[8];
-            unpack8(*reinterpret_cast<const uint4*>(pv), u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dv[e] += u[e];
-            unpack8(*reinterpret_cast<const uint4*>(pv + 8), u);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) dv[8 + e] += u[e];
-        }
-        *reinterpret_cast<uint4*>(pk) = pack8(dk);
-        *reinterpret_cast<uint4*>(pv) = pack8(dv);
-        *reinterpret_cast<uint4*>(pv + 8) = pack8(dv + 8);
-    }
-}
-
-// dq fp32 [B][N][heads*KD] -> q channels of dqkv
-__global__ void attn_dq_store_kernel(const float* __restrict__ dq, bf16_t* __restrict__ dqkv, int64_t g_bs, int64_t g_ld,
-                                     int B, int N, int heads, int accumulate) {
-    int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;   // one per (b, i, h, 8-chunk)
-    const int per = heads * (KD / 8);
-    if (idx >= int64_t(B) * N * per) return;
-    int c = int(idx % per);
-    int64_t bi = idx / per;
-    int h = c / (KD / 8), d0 = (c % (KD / 8)) * 8;
-    int64_t b = bi / N, i = bi % N;
-    const float* s = dq + bi * (heads * KD) + h * KD + d0;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = s[e];
-    bf16_t* o = dqkv + b * g_bs + i * g_ld + h * (2 * KD + HD) + d0;
-    if (accumulate) {
-        float u[8];
-        unpack8(*reinterpret_cast<const uint4*>(o), u);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += u[e];
-    }
-    *reinterpret_cast<uint4*>(o) = pack8(v);
-}
-
 }  // namespace
 }  // namespace ym
 
@@ -630,40 +364,3 @@ extern "C" int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, 
     return YM_OK;
 }
 
-extern "C" int ym_attn_fwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, int b, int heads, int n, int key_dim,
-                           int head_dim, float scale, uint16_t* out, int64_t o_bs, int64_t o_ld, float* lse,
-                           void* stream) {
-    YM_CHECK_ARG(key_dim == KD && head_dim == HD, "ym_attn_fwd: only key_dim=32, head_dim=64 (got %d, %d)", key_dim,
-                 head_dim);
-    AttnArgs a{qkv, q_bs, q_ld, n, heads, scale};
-    hipLaunchKernelGGL(attn_fwd_kernel, dim3((n + QT - 1) / QT, heads, b), dim3(256), 0, as_stream(stream), a, out,
-                       o_bs, o_ld, lse);
-    YM_LAUNCH_CHECK("ym_attn_fwd");
-    return YM_OK;
-}
-
-extern "C" int ym_attn_bwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, const uint16_t* out, int64_t o_bs,
-                           int64_t o_ld, const uint16_t* dout, int64_t d_bs, int64_t d_ld, const float* lse, int b,
-                           int heads, int n, float scale, float* workspace, uint16_t* dqkv, int64_t g_bs, int64_t g_ld,
-                           int acc_q, int acc_k, int acc_v, void* stream) {
-    // workspace: D [b*heads*n] + dq [b*n*heads*KD] fp32
-    hipStream_t st = as_stream(stream);
-    float* D = workspace;
-    float* dq = workspace + int64_t(b) * heads * n;
-    int64_t nD = int64_t(b) * heads * n;
-    hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3(unsigned((nD + 255) / 256)), dim3(256), 0, st, out, o_bs, o_ld, dout,
-                       d_bs, d_ld, b, heads, n, D);
-    if (hipMemsetAsync(dq, 0, size_t(b) * n * heads * KD * sizeof(float), st) != hipSuccess) return YM_ERR_HIP;
-    AttnArgs a{qkv, q_bs, q_ld, n, heads, scale};
-    hipLaunchKernelGGL(attn_bwd_kernel, dim3((n + QT - 1) / QT, heads, b), dim3(256), 0, st, a, dout, d_bs, d_ld, lse, D,
-                       dqkv, g_bs, g_ld, dq, acc_k, acc_v);
-    int64_t nq = int64_t(b) * n * heads * (KD / 8);
-    hipLaunchKernelGGL(attn_dq_store_kernel, dim3(unsigned((nq + 255) / 256)), dim3(256), 0, st, dq, dqkv, g_bs, g_ld, b,
-                       n, heads, acc_q);
-    YM_LAUNCH_CHECK("ym_attn_bwd");
-    return YM_OK;
-}
-
-extern "C" size_t ym_attn_workspace_size(int b, int heads, int n) {
-    return (size_t(b) * heads * n + size_t(b) * n * heads * KD) * sizeof(float);
-}
