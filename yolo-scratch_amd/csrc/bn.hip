@@ -48,17 +48,14 @@ __device__ __forceinline__ uint4 pack8h(const float* f) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2bf(f[2 * i])) | (uint32_t(f2bf(f[2 * i + 1])) << 16);
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return make_uint4(pk2bf(f[0], f[1]), pk2bf(f[2], f[3]), pk2bf(f[4], f[5]), pk2bf(f[6], f[7]));
 }
 __device__ __forceinline__ void load8(const float* p, float* v) {
     float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
     v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 __device__ __forceinline__ float dsilu(float u) {
-    float sg = 1.0f / (1.0f + __expf(-u));
+    const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-u));
     return sg * (1.0f + u * (1.0f - sg));
 }
 
@@ -90,13 +87,26 @@ __global__ void __launch_bounds__(256) partials_reduce_kernel(const float* __res
     }
 }
 
-__device__ __forceinline__ void fold(const double* p, int R, int C, int c, double& s, double& q) {
+// second level: 64 channels per block, the R level-1 rows split over the 4 waves, combined in
+// LDS; returns true on the wave-0 lanes that own a channel (s, q valid there)
+__device__ __forceinline__ bool fold(const double* p, int R, int C, double& s, double& q, int& c) {
+    __shared__ double sh[2][4][64];
+    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    c = blockIdx.x * 64 + cl;
     s = 0.0;
     q = 0.0;
-    for (int r = 0; r < R; ++r) {
-        s += p[(int64_t(r) * 2 + 0) * C + c];
-        q += p[(int64_t(r) * 2 + 1) * C + c];
-    }
+    if (c < C)
+        for (int r = rg; r < R; r += 4) {
+            s += p[(int64_t(r) * 2 + 0) * C + c];
+            q += p[(int64_t(r) * 2 + 1) * C + c];
+        }
+    sh[0][rg][cl] = s;
+    sh[1][rg][cl] = q;
+    __syncthreads();
+    if (rg != 0 || c >= C) return false;
+    s = (sh[0][0][cl] + sh[0][1][cl]) + (sh[0][2][cl] + sh[0][3][cl]);
+    q = (sh[1][0][cl] + sh[1][1][cl]) + (sh[1][2][cl] + sh[1][3][cl]);
+    return true;
 }
 
 __global__ void bn_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
@@ -104,11 +114,10 @@ __global__ void bn_finalize_kernel(const double* __restrict__ p2, int R, int C, 
                                    float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
                                    float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
                                    float* __restrict__ rstd_out) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (nbt && c == 0) *nbt += 1;
-    if (c >= C) return;
+    if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
     double s, q;
-    fold(p2, R, C, c, s, q);
+    int c;
+    if (!fold(p2, R, C, s, q, c)) return;
     double mean = s / count;
     double var = q / count - mean * mean;
     if (var < 0) var = 0;
@@ -128,10 +137,9 @@ __global__ void bn_finalize_kernel(const double* __restrict__ p2, int R, int C, 
 __global__ void bn_bwd_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
                                        const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
                                        float* dbeta, int accumulate, float* __restrict__ coef) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
     double s, q;
-    fold(p2, R, C, c, s, q);
+    int c;
+    if (!fold(p2, R, C, s, q, c)) return;
     if (dgamma) dgamma[c] = float(accumulate ? dgamma[c] + q : q);
     if (dbeta) dbeta[c] = float(accumulate ? dbeta[c] + s : s);
     coef[c] = gamma[c] * rstd[c];               // k1
@@ -176,25 +184,41 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
     float sc[8], sf[8];
     load8(scale + c0, sc);
     load8(shift + c0, sf);
-    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
-        float v[8];
-        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            float u = v[k] * sc[k] + sf[k];
-            v[k] = act ? silu_f(u) : u;
-        }
+    const int64_t step = int64_t(gridDim.x) * L.rows;
+    // two rows per iteration: both rows' loads are in flight before either is used
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
+        const int64_t m2 = m + step;
+        const bool two = m2 < M;
+        uint4 zr[2], rr[2];
+        zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
+        if (two) zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
         if (res) {
-            float r[8];
-            unpack8h(*reinterpret_cast<const uint4*>(res + m * r_ld + c0), r);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] += r[k];
+            rr[0] = *reinterpret_cast<const uint4*>(res + m * r_ld + c0);
+            if (two) rr[1] = *reinterpret_cast<const uint4*>(res + m2 * r_ld + c0);
         }
-        *reinterpret_cast<uint4*>(out + m * o_ld + c0) = pack8h(v);
-        if (out32) {
-            float4* o = reinterpret_cast<float4*>(out32 + m * C + c0);
-            o[0] = make_float4(v[0], v[1], v[2], v[3]);
-            o[1] = make_float4(v[4], v[5], v[6], v[7]);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (u == 1 && !two) break;
+            const int64_t mm = u ? m2 : m;
+            float v[8];
+            unpack8h(zr[u], v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float t = v[k] * sc[k] + sf[k];
+                v[k] = act ? silu_f(t) : t;
+            }
+            if (res) {
+                float r[8];
+                unpack8h(rr[u], r);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] += r[k];
+            }
+            *reinterpret_cast<uint4*>(out + mm * o_ld + c0) = pack8h(v);
+            if (out32) {
+                float4* o = reinterpret_cast<float4*>(out32 + mm * C + c0);
+                o[0] = make_float4(v[0], v[1], v[2], v[3]);
+                o[1] = make_float4(v[4], v[5], v[6], v[7]);
+            }
         }
     }
 }
@@ -217,15 +241,29 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         load8(shift + c0, sf);
         load8(mean + c0, mu);
         load8(rstd + c0, rs);
-        for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
-            float zv[8], dv[8];
-            unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), zv);
-            unpack8(*reinterpret_cast<const uint4*>(dy + m * d_ld + c0), dv);
+        const int64_t step = int64_t(gridDim.x) * L.rows;
+        for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
+            const int64_t m2 = m + step;
+            const bool two = m2 < M;
+            uint4 zr[2], dr[2];
+            zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
+            dr[0] = *reinterpret_cast<const uint4*>(dy + m * d_ld + c0);
+            if (two) {
+                zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
+                dr[1] = *reinterpret_cast<const uint4*>(dy + m2 * d_ld + c0);
+            }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
-                s[k] += gg;
-                sx[k] += gg * ((zv[k] - mu[k]) * rs[k]);
+            for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !two) break;
+                float zv[8], dv[8];
+                unpack8h(zr[u], zv);
+                unpack8(dr[u], dv);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
+                    s[k] += gg;
+                    sx[k] += gg * ((zv[k] - mu[k]) * rs[k]);
+                }
             }
         }
 #pragma unroll
@@ -265,17 +303,31 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     load8(coef + c0, k1);
     load8(coef + C + c0, k2);
     load8(coef + 2 * C + c0, k3);
-    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += int64_t(gridDim.x) * L.rows) {
-        float zv[8], dv[8], o[8];
-        unpack8h(*reinterpret_cast<const uint4*>(z + m * C + c0), zv);
-        unpack8(*reinterpret_cast<const uint4*>(dy + m * d_ld + c0), dv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
-            float xh = (zv[k] - mu[k]) * rs[k];
-            o[k] = k1[k] * (gg - k2[k] - xh * k3[k]);
+    const int64_t step = int64_t(gridDim.x) * L.rows;
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
+        const int64_t m2 = m + step;
+        const bool two = m2 < M;
+        uint4 zr[2], dr[2];
+        zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
+        dr[0] = *reinterpret_cast<const uint4*>(dy + m * d_ld + c0);
+        if (two) {
+            zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
+            dr[1] = *reinterpret_cast<const uint4*>(dy + m2 * d_ld + c0);
         }
-        *reinterpret_cast<uint4*>(dz + m * C + c0) = pack8(o);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            if (u == 1 && !two) break;
+            float zv[8], dv[8], o[8];
+            unpack8h(zr[u], zv);
+            unpack8(dr[u], dv);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
+                const float xh = (zv[k] - mu[k]) * rs[k];
+                o[k] = k1[k] * (gg - k2[k] - xh * k3[k]);
+            }
+            *reinterpret_cast<uint4*>(dz + (u ? m2 : m) * C + c0) = pack8(o);
+        }
     }
 }
 
@@ -307,7 +359,7 @@ extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int p
     double* p2 = static_cast<double*>(workspace);
     hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_sq, parts,
                        c, RED_R, p2);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, st, p2, RED_R, c, count, gamma, beta,
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma, beta,
                        running_mean, running_var, num_batches_tracked, momentum, eps, scale, shift, mean, rstd);
     YM_LAUNCH_CHECK("ym_bn_finalize");
     return YM_OK;
@@ -357,7 +409,7 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
     double* p2 = static_cast<double*>(workspace);
     hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_dot, parts,
                        c, RED_R, p2);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 255) / 256), dim3(256), 0, st, p2, RED_R, c, count, gamma,
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma,
                        rstd, dgamma, dbeta, accumulate, coef);
     YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
     return YM_OK;

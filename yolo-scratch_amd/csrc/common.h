@@ -59,6 +59,7 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-__device__ __forceinline__ float silu_f(float u) { return u / (1.0f + __expf(-u)); }
+// SiLU with the hardware reciprocal (v_rcp_f32, ~1 ulp; results are stored in 16 bits)
+__device__ __forceinline__ float silu_f(float u) { return u * __builtin_amdgcn_rcpf(1.0f + __expf(-u)); }
 
 }  // namespace ym

@@ -24,6 +24,7 @@
 // conv_first_*  Cin = 1 stem (K = 9): direct fp32 VALU kernels.
 // dw3x3_*       depthwise 3x3 (Attention.pe, yolo11_modules.py:122): direct.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "tile.h"
@@ -79,12 +80,15 @@ __device__ __forceinline__ void raw_barrier() {
 #define YM_CONV_STAGES 2
 #endif
 
-template <int BM, int BN, int MODE>
-__global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_kernel(GemmArgs a) {
-    constexpr int TM = BN / 32;          // 16-channel subtiles per wave
-    constexpr int TN = BM / 32;          // 16-pixel subtiles per wave
-    constexpr int AI = BN / 32;          // A (weight) DMA instructions per wave per stage (8 rows each)
-    constexpr int BI = BM / 32;          // B (activation) DMA instructions per wave per stage
+// WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile
+template <int BM, int BN, int WM, int WN, int MODE>
+__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && YM_CONV_STAGES == 2) ? 2 : 1)
+conv_gemm_kernel(GemmArgs a) {
+    constexpr int NW = WM * WN, NT = NW * 64;
+    constexpr int TM = BN / WM / 16;     // 16-channel subtiles per wave
+    constexpr int TN = BM / WN / 16;     // 16-pixel subtiles per wave
+    constexpr int AI = BN / 8 / NW;      // A (weight) DMA instructions per wave per stage (8 rows each)
+    constexpr int BI = BM / 8 / NW;      // B (activation) DMA instructions per wave per stage
     constexpr int STAGE = (BM + BN) * 128;
     constexpr int NSTAGE = YM_CONV_STAGES;   // LDS ring depth: NSTAGE-1 stages in flight
     static_assert(AI >= 1 && BI >= 1, "tile too small for the staging map");
@@ -92,7 +96,7 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
     __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / WN, wc = wave % WN;
     const int fc = lane >> 4, fr = lane & 15;
     const int n0 = blockIdx.y * BN;
     const int kc = (a.Kin + BK - 1) / BK;
@@ -222,12 +226,12 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
                 bf16x8 af[TM], bfr[TN];
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
-                    const int r = wr * (BN / 2) + i * 16 + fr;
+                    const int r = wr * (BN / WM) + i * 16 + fr;
                     af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((cch ^ fsw(r)) << 4));
                 }
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
-                    const int r = wc * (BM / 2) + j * 16 + fr;
+                    const int r = wc * (BM / WN) + j * 16 + fr;
                     bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((cch ^ fsw(r)) << 4));
                 }
 #pragma unroll
@@ -247,7 +251,7 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
         // epilogue: D[channel][pixel]; lane holds 4 consecutive channels of one pixel
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int64_t m = m0 + wc * (BM / 2) + j * 16 + fr;
+            const int64_t m = m0 + wc * (BM / WN) + j * 16 + fr;
             if (m >= Mc) continue;
             const uint32_t n = uint32_t(m) / OHW, pix = uint32_t(m) - n * OHW;
             const uint32_t ci_ = pix / uint32_t(OWc);
@@ -255,7 +259,7 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
             const int64_t obase = int64_t(n) * a.y_bs + opix * a.y_ld;
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int cb = n0 + wr * (BN / 2) + i * 16 + fc * 4;
+                const int cb = n0 + wr * (BN / WM) + i * 16 + fc * 4;
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -307,7 +311,7 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
     }
 
     if (a.st_sum) {
-        float (*red)[2][BN] = reinterpret_cast<float (*)[2][BN]>(smem);   // [sum|sq][wave pixel half][channel]
+        float (*red)[WN][BN] = reinterpret_cast<float (*)[WN][BN]>(smem);   // [sum|sq][pixel wave][channel]
         raw_barrier();                     // staging LDS is free again
         // reduce over the 16 pixel lanes, then over the two pixel-half waves
 #pragma unroll
@@ -321,17 +325,20 @@ __global__ void __launch_bounds__(256, YM_CONV_STAGES == 2 ? 2 : 1) conv_gemm_ke
                     q += __shfl_xor(q, o, 64);
                 }
                 if (fr == 0) {
-                    int cl = wr * (BN / 2) + i * 16 + (lane >> 4) * 4 + r;
+                    int cl = wr * (BN / WM) + i * 16 + (lane >> 4) * 4 + r;
                     red[0][wc][cl] = s;
                     red[1][wc][cl] = q;
                 }
             }
         __syncthreads();
-        for (int c = tid; c < BN; c += 256) {
+        for (int c = tid; c < BN; c += NT) {
             int ch = n0 + c;
             if (ch < a.Nout) {
-                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = red[0][0][c] + red[0][1][c];
-                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = red[1][0][c] + red[1][1][c];
+                float ps = 0.f, pq = 0.f;
+#pragma unroll
+                for (int w = 0; w < WN; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
+                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = pq;
             }
         }
     }
@@ -638,11 +645,11 @@ static int grid_x(int mtiles, int ntiles, bool stats, int max_blocks) {
 
 // the kernel's buffer offsets are 32-bit, relative to the first image of a tile
 static bool offsets_fit(int64_t bs, int64_t class_pixels) {
-    const int64_t images = 128 / std::max<int64_t>(class_pixels, 1) + 2;
+    const int64_t images = 256 / std::max<int64_t>(class_pixels, 1) + 2;
     return bs * 2 * images < (int64_t(1) << 31);
 }
 
-template <int BM, int BN, int MODE>
+template <int BM, int BN, int WM, int WN, int MODE>
 int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     GemmArgs a = a0;
     const int os = a.ostep;
@@ -650,7 +657,8 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1),
+                       dim3(WM * WN * 64), 0, st, a);
     return gx;
 }
 
@@ -659,33 +667,47 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
 
 using namespace ym;
 
-// widest channel tile that still gives >= 1.5 workgroups per CU (small late layers: 20x20 maps)
-static int pick_bn(int64_t blocks_per_ntile, int nout) {
+struct Tile {
+    int bm, bn;
+};
+
+// Large problems: 256 x 128 tiles on 8 waves (a quarter fewer operand bytes per FLOP than 128x128,
+// the L2 -> LDS stream being what bounds this kernel; 256 x 256 does not fit 256 VGPRs per lane).  Otherwise 128-pixel tiles with the widest
+// channel tile that still gives >= 1.5 workgroups per CU (small late layers: 20x20 maps).
+// Measured (tools/layer_bench.py, s@640 bs64): 256 x 128 tiles are 9 % slower in sum than
+// 128 x 128 at this kernel's pipeline depth, so they are opt-in: YM_CONV_TILE=256.
+static Tile pick_tile(int64_t Mc, int classes, int nout) {
+    static const int use256 = [] {
+        const char* e = getenv("YM_CONV_TILE");
+        return e && atoi(e) == 256;
+    }();
+    if (nout >= 128 && use256 && ((Mc + 255) / 256) * classes * ((nout + 127) / 128) >= 512) return {256, 128};
+    const int64_t blocks_per_ntile = ((Mc + 127) / 128) * classes;
     int bn = nout >= 128 ? 128 : (nout >= 64 ? 64 : 32);
     while (bn > 32 && blocks_per_ntile * ((nout + bn - 1) / bn) < 384) bn >>= 1;
-    return bn;
+    return {128, bn};
+}
+
+template <int MODE>
+static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
+    if (t.bm == 256) return launch_gemm<256, 128, 2, 4, MODE>(a, max_blocks, st);
+    if (t.bn == 128) return launch_gemm<128, 128, 2, 2, MODE>(a, max_blocks, st);
+    if (t.bn == 64) return launch_gemm<128, 64, 2, 2, MODE>(a, max_blocks, st);
+    return launch_gemm<128, 32, 2, 2, MODE>(a, max_blocks, st);
 }
 
 static int pick_and_launch(GemmArgs a, int mode, int max_blocks, hipStream_t st) {
     const int os = a.ostep;
     const int64_t Mc = int64_t(a.N) * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);
-    const int bn = pick_bn(((Mc + 127) / 128) * (os == 2 ? 4 : 1), a.Nout);
-    if (mode == MODE_FWD) {
-        if (bn == 128) return launch_gemm<128, 128, MODE_FWD>(a, max_blocks, st);
-        if (bn == 64) return launch_gemm<128, 64, MODE_FWD>(a, max_blocks, st);
-        return launch_gemm<128, 32, MODE_FWD>(a, max_blocks, st);
-    }
-    if (bn == 128) return launch_gemm<128, 128, MODE_DGRAD>(a, max_blocks, st);
-    if (bn == 64) return launch_gemm<128, 64, MODE_DGRAD>(a, max_blocks, st);
-    return launch_gemm<128, 32, MODE_DGRAD>(a, max_blocks, st);
+    const Tile t = pick_tile(Mc, os == 2 ? 4 : 1, a.Nout);
+    return mode == MODE_FWD ? launch_tile<MODE_FWD>(a, t, max_blocks, st) : launch_tile<MODE_DGRAD>(a, t, max_blocks, st);
 }
 
 extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     // grid-x used for the stats partials by ym_conv_fwd (callers size the partial buffers with it)
-    const int mtiles = int((M + 127) / 128);
-    const int BN = pick_bn(mtiles, Cout);
-    const int ntiles = (Cout + BN - 1) / BN;
-    return grid_x(mtiles, ntiles, true, 2048);
+    const Tile t = pick_tile(M, 1, Cout);
+    const int mtiles = int((M + t.bm - 1) / t.bm);
+    return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, 2048);
 }
 
 extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
