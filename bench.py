@@ -143,10 +143,15 @@ def main():
     convs = [op for op in plan.ops if type(op) is ConvBN]
     dom = max(convs, key=lambda op: op.flops())
     plan.probe, plan.probe_events = dom, []
-    # launches sharing the probe's kernel + grid (same pixel count and channel count), for
-    # matching the probe in a rocprofv3 counter pass (tools/pmc_traffic.py)
-    same = [op for op in convs if (op.M, op.co) == (dom.M, dom.co)]
-    probe_rank, probe_count = same.index(dom), len(same)
+    # position of the probe among a step's implicit-GEMM forward launches (ConvBN: 1, Detect
+    # level: 2), for finding it in a rocprofv3 counter pass (tools/pmc_traffic.py)
+    fwd_seq = []
+    for op in plan.ops:
+        if type(op) is ConvBN:
+            fwd_seq.append(op)
+        elif type(op).__name__ == "HeadLevel":
+            fwd_seq += [op, op]
+    probe_rank, probe_count = fwd_seq.index(dom), len(fwd_seq)
     probe_key = f"{dom.ci}->{dom.co} k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W} bs{args.batch}"
 
     if dp:
@@ -182,6 +187,17 @@ def main():
     train_flop = 3 * fwd - sum(2 * op.M * op.co * 9 for op in stem) + 3 * att
     per_img = train_flop / args.batch
     dom_tf = dom.flops() / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
+    # algorithmic HBM bytes of the probe launch: fp16 input view read once, fp16 weights, fp16 z
+    # written once (BN partials are negligible); the binding roof is the larger time bound
+    alg_bytes = 2 * (args.batch * dom.x.H * dom.x.W * dom.ci + dom.co * dom.ci * dom.k * dom.k + dom.M * dom.co)
+    hbm_bound = alg_bytes / (HBM_PEAK_GBS * 1e9) > dom.flops() / (PEAK_BF16_TFLOPS * 1e12)
+    dom_gbs = alg_bytes / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    if hbm_bound:
+        roof = {"bound": "hbm", "achieved": round(dom_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dom_gbs / HBM_PEAK_GBS, 4)}
+    else:
+        roof = {"bound": "mfma", "achieved": round(dom_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4)}
     step_tf = value / world * per_img / 1e12
     out = {
         "metric": METRIC,
@@ -200,11 +216,12 @@ def main():
                                f"(fwd+loss+bwd+allreduce+clip+AdamW)",
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch, "imgsz": args.imgsz,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "achieved": round(dom_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic_for(probe_key),
+        "roofline": {**roof, "traffic": traffic_for(probe_key),
                      "kernel": f"conv_gemm_kernel fwd {dom.m.__class__.__name__} {dom.ci}->{dom.co} "
-                               f"k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W}, {dom.flops() / 1e9:.1f} GFLOP/launch, "
-                               f"{kern_ms:.3f} ms avg over {len(lens)} launches"},
+                               f"k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W}, {dom.flops() / 1e9:.1f} GFLOP and "
+                               f"{alg_bytes / 1e6:.0f} MB algorithmic per launch, {kern_ms:.3f} ms avg over "
+                               f"{len(lens)} launches ({dom_tf:.0f} TFLOP/s = {dom_tf / PEAK_BF16_TFLOPS:.3f} of the "
+                               f"MFMA peak, {dom_gbs:.0f} GB/s = {dom_gbs / HBM_PEAK_GBS:.3f} of HBM)"},
         "roofline_step": {"bound": "mfma", "achieved": round(step_tf, 2), "peak": PEAK_BF16_TFLOPS,
                           "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16_TFLOPS, 4),
                           "train_gflop_per_img": round(per_img / 1e9, 2)},

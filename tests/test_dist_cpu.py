@@ -67,3 +67,67 @@ def test_gradsync_world2_gloo():
     for r in range(world):
         for i, g in enumerate(res[r][2]):
             assert g == pytest.approx(1.5 * (i + 1))
+
+
+class _FakePlan:
+    """The parts of yolomi.graph.Plan that GradSync touches: flat grads, views, the backward hook."""
+
+    def __init__(self, model):
+        self.params = [p for p in model.parameters()]
+        n = sum(p.numel() for p in self.params)
+        self.grad_flat = torch.zeros(n)
+        self.grad_views, off = {}, 0
+        for p in self.params:
+            self.grad_views[id(p)] = self.grad_flat[off:off + p.numel()].view(p.shape)
+            off += p.numel()
+        self.grad_hook = None
+
+    def backward(self, rank, step):
+        """Write per-rank grads parameter by parameter, in reverse (as the plan's backward does)."""
+        for i, p in reversed(list(enumerate(self.params))):
+            self.grad_views[id(p)].fill_(float((rank + 1) * (i + 1) * (step + 1)))
+            if self.grad_hook is not None:
+                self.grad_hook([p])
+
+
+def _bucket_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from yolomi import dist as ydist
+        ctx = ydist.init_from_env("gloo")
+        m = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(6)])
+        plan = _FakePlan(m)
+        m.__dict__["_ym_last_plan"] = plan
+        sync = ydist.GradSync(m, ctx, bucket_mb=0.02)     # ~20 KB buckets: several per step
+        res = []
+        for step in range(3):                             # step 0: plain all-reduce, then buckets
+            plan.backward(rank, step)
+            sync.sync()
+            res.append([float(plan.grad_views[id(p)].mean()) for p in plan.params])
+        q.put((rank, res, len(sync.buckets.ranges)))
+        ydist.shutdown()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_bucketed_overlap_world2_gloo():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=120)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in res.values():
+        assert r[1] != "error", r[2]
+    assert res[0][2] > 2                                  # the buffer really was split
+    for r in range(world):
+        for step, means in enumerate(res[r][1]):
+            for i, g in enumerate(means):
+                assert g == pytest.approx(1.5 * (i + 1) * (step + 1)), (r, step, i)

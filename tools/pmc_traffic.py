@@ -25,18 +25,16 @@ def dispatches(path, counter):
 def main():
     fetch_csv, write_csv, bench_json = sys.argv[1:4]
     b = json.loads(Path(bench_json).read_text().strip().splitlines()[-1])
-    key, rank, count = b["probe"]["key"], b["probe"]["rank"], b["probe"]["count"]
-    kname = "conv_gemm_kernel<128, 128, 0>" if "->" in key else None
+    key, rank, per_step = b["probe"]["key"], b["probe"]["rank"], b["probe"]["count"]
     out = {}
     for counter, path in (("FETCH_SIZE", fetch_csv), ("WRITE_SIZE", write_csv)):
-        rows = [r for r in dispatches(path, counter) if kname in r["Kernel_Name"]]
-        grids = {}
-        for r in rows:
-            grids.setdefault(r["Grid_Size"], []).append(r)
-        # the probe's shape group: the grid whose launch count is a multiple of `count`, largest first
-        cand = [g for g, rs in grids.items() if len(rs) % count == 0]
-        best = max(cand, key=lambda g: len(grids[g]))
-        sel = grids[best][rank::count]
+        # a step's implicit-GEMM forward launches, in dispatch order (MODE 0 instantiations)
+        rows = [r for r in dispatches(path, counter)
+                if "conv_gemm_kernel<" in r["Kernel_Name"] and r["Kernel_Name"].split(">")[0].endswith(", 0")]
+        assert len(rows) % per_step == 0, (len(rows), per_step)
+        sel = rows[rank::per_step]
+        names = {r["Kernel_Name"].split("(")[0] for r in sel}
+        assert len(names) == 1, names
         out[counter] = [float(r["Counter_Value"]) * 1024.0 for r in sel]   # KB -> bytes
     n = min(len(out["FETCH_SIZE"]), len(out["WRITE_SIZE"]))
     fetch = sum(out["FETCH_SIZE"][:n]) / n

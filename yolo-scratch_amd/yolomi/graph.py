@@ -523,6 +523,17 @@ class HeadLevel:
             x.mark()
 
 
+def op_params(op):
+    """Parameters whose gradients an op's backward finalises (in the flat gradient buffer)."""
+    if isinstance(op, HeadLevel):
+        mods = (op.box, op.cls)
+    elif isinstance(op, ConvBN):
+        mods = (op.m,)
+    else:
+        return []
+    return [p for m in mods for p in m.parameters() if p.requires_grad]
+
+
 # ----------------------------------------------------------------------------- plan
 class Plan:
     def __init__(self, root, B, H, W, dev, training):
@@ -536,6 +547,7 @@ class Plan:
         self.head = None           # (B, A, 64+nc) fp32 for the full model
         self.dhead = None
         self._scratch = []
+        self.grad_hook = None      # called with each op's finished parameters during backward (DP buckets)
         # flat parameter-gradient buffer; each .grad is a view of it
         params = [p for p in root.parameters() if p.requires_grad]
         self.params = params
@@ -584,8 +596,11 @@ class Plan:
         self.grad_flat.zero_()
         for t in self._scratch:
             t.zero_()
+        hook = self.grad_hook
         for op in reversed(self.ops):
             op.backward(self, st)
+            if hook is not None:
+                hook(op_params(op))
 
     def install_grads(self):
         """Expose the flat buffer as parameter .grad (accumulating if a grad already exists)."""
