@@ -111,7 +111,12 @@ def main():
     torch.manual_seed(0)
     model = build_yolo11(cfg, ch=1, nc=5).to(dev).train()
     crit = v8DetectionLoss(model, tal_topk=10)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=5e-4)
+    # same AdamW math as the reference (train_yolo11_cuda.py:440-451); the fused single-kernel
+    # implementation where PyTorch offers it for this device
+    try:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=5e-4, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=5e-4)
     dp = ydist.GradSync(model, ctx) if ctx else None
     if dp:
         dp.broadcast_state()

@@ -9,7 +9,8 @@ by fp32 accumulation order and the output rounding:
     OIHW, overwrite and accumulate; the 3x3 (all taps per block), 1x1 (flat pixels) and generic
     (here: 1x1 stride 2) kernels are all covered
 Shapes cover odd spatial sizes, both strides, k = 1 and 3, channel counts that are not
-multiples of the tile sizes, and the 4-parity-class stride-2 dgrad (a 1x1 stride-2 conv
+multiples of the tile sizes, 8/16/32-channel inputs (taps packed into one K step), and the
+4-parity-class stride-2 dgrad (a 1x1 stride-2 conv
 leaves three of the classes with no tap: their gradient must be exactly zero).
 """
 import ctypes
@@ -31,6 +32,10 @@ SHAPES = [
     (1, 5, 7, 520, 264, 3, 1, 1),
     (2, 9, 9, 256, 136, 1, 1, 0),
     (2, 33, 17, 64, 64, 3, 1, 1),
+    # narrow inputs: several taps share one 64-deep K step (fwd Kin = cin, dgrad Kin = cout)
+    (2, 9, 7, 64, 32, 3, 1, 1),
+    (1, 10, 10, 8, 16, 3, 1, 1),
+    (2, 11, 11, 16, 32, 3, 2, 1),
 ]
 
 

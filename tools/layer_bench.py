@@ -73,12 +73,22 @@ def main():
         for j in range(3):
             tot[j] += ms[j]
         tf = [fl / (m * 1e-3) / 1e12 if m > 0 else 0.0 for m in ms]
-        rows.append((i, d.cin, d.cout, d.k, d.stride, d.oh, d.ow, fl / 1e9, ms, tf))
-    print(f"{'op':>4} {'cin':>4} {'cout':>4} k s {'out':>7} {'GFLOP':>7} | {'fwd ms':>7} {'TF/s':>5} | "
-          f"{'dgrad':>7} {'TF/s':>5} | {'wgrad':>7} {'TF/s':>5}")
-    for i, ci, co, k, s, oh, ow, gf, ms, tf in rows:
-        print(f"{i:4d} {ci:4d} {co:4d} {k} {s} {oh:3d}x{ow:<3d} {gf:7.1f} | {ms[0]:7.3f} {tf[0]:5.0f} | "
-              f"{ms[1]:7.3f} {tf[1]:5.0f} | {ms[2]:7.3f} {tf[2]:5.0f}")
+        # binding-roof fraction per kernel: algorithmic bytes (16-bit tensors read/written once)
+        xin = args.batch * d.h * d.w * d.cin * 2
+        yout = args.batch * d.oh * d.ow * d.cout * 2
+        wb = d.cout * d.cin * d.k * d.k * 2
+        byts = [xin + wb + yout, yout + wb + xin, yout + xin + 2 * wb]
+        frac = []
+        for m, b in zip(ms, byts):
+            t_floor = max(fl / 2.5e15, b / 8e12)
+            frac.append(t_floor / (m * 1e-3) if m > 0 else 0.0)
+        rows.append((i, d.cin, d.cout, d.k, d.stride, d.oh, d.ow, fl / 1e9, ms, tf, frac,
+                     "hbm" if byts[0] / 8e12 > fl / 2.5e15 else "mfma"))
+    print(f"{'op':>4} {'cin':>4} {'cout':>4} k s {'out':>7} {'GFLOP':>7} roof | {'fwd ms':>7} {'TF/s':>5} {'frac':>5} | "
+          f"{'dgrad':>7} {'TF/s':>5} {'frac':>5} | {'wgrad':>7} {'TF/s':>5} {'frac':>5}")
+    for i, ci, co, k, s, oh, ow, gf, ms, tf, fr, roof in rows:
+        print(f"{i:4d} {ci:4d} {co:4d} {k} {s} {oh:3d}x{ow:<3d} {gf:7.1f} {roof:>4} | {ms[0]:7.3f} {tf[0]:5.0f} {fr[0]:5.2f} | "
+              f"{ms[1]:7.3f} {tf[1]:5.0f} {fr[1]:5.2f} | {ms[2]:7.3f} {tf[2]:5.0f} {fr[2]:5.2f}")
     print(f"total ms: fwd {tot[0]:.3f}  dgrad {tot[1]:.3f}  wgrad {tot[2]:.3f}")
 
 

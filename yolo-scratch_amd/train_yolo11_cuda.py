@@ -224,7 +224,12 @@ def main():
         n_params = sum(p.numel() for p in model.parameters())
         print(f"Total parameters: {n_params:,} ({n_params / 1e6:.2f}M)")
     criterion = v8DetectionLoss(model, tal_topk=10)
-    optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
+    # the reference's AdamW (:440-451); PyTorch's fused single-kernel form on the GPU
+    try:
+        optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay,
+                                      fused=device.type == "cuda")
+    except (RuntimeError, TypeError):
+        optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
     dp = ydist.GradSync(model, dp_ctx) if dp_ctx else None
     start_epoch, best_loss, best_mAP50 = 0, float("inf"), 0.0
     if args.resume and os.path.isfile(args.resume):
