@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", type=int, nargs="*", help="plan op indices to time (default: every ConvBN)")
     args = ap.parse_args()
     import torch
     import yaml
@@ -46,7 +47,7 @@ def main():
     rows = []
     tot = [0.0, 0.0, 0.0]
     for i, op in enumerate(plan.ops):
-        if type(op) is not ConvBN:
+        if type(op) is not ConvBN or (args.only and i not in args.only):
             continue
         d = op.desc
         fl = op.flops()
