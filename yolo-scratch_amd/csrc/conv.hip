@@ -25,6 +25,7 @@
 // dw3x3_*       depthwise 3x3 (Attention.pe, yolo11_modules.py:122): direct.
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "common.h"
 #include "tile.h"
@@ -35,7 +36,6 @@ namespace {
 
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
-constexpr int BK = 64;   // k per LDS stage = two MFMA k-steps
 
 struct GemmArgs {
     const bf16_t* x; int64_t x_bs, x_ld;    // gathered activation view
@@ -58,7 +58,13 @@ struct GemmArgs {
 // lives on the global (source) side: a DMA lane that fills slot s of row r loads chunk s ^ f(r), so
 // each 8-lane group still reads one whole 128-B row.  A ds_read_b128 lane group (rows {0-3,12-15}
 // at chunk c, rows {4-11} at chunk c^1) then covers 16 distinct (row parity, slot) bank quads.
-__device__ __forceinline__ int fsw(int r) { return (r >> 1) & 7; }
+// 64-B rows (32-deep K stages, 4 slots): slot c ^ F[(r >> 2) & 3], F = {0, 3, 2, 1} — for each
+// row residue mod 4 a read group's four rows then land on four distinct slots.
+template <int RB>
+__device__ __forceinline__ int fsw(int r) {
+    if constexpr (RB == 128) return (r >> 1) & 7;
+    else return (0x1E4 >> (((r >> 2) & 3) * 2)) & 3;   // F = {0, 3, 2, 1}
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -76,21 +82,22 @@ __device__ __forceinline__ void raw_barrier() {
     asm volatile("" ::: "memory");
 }
 
-#ifndef YM_CONV_STAGES
-#define YM_CONV_STAGES 2
-#endif
-
-// WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile
-template <int BM, int BN, int WM, int WN, int MODE>
-__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && YM_CONV_STAGES == 2) ? 2 : 1)
+// WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile; KB-deep K stages
+// (rows of KB*2 bytes), an NS-stage LDS ring with NS-1 stages in flight
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
+__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NS * (BM + BN) * KB * 2 <= 72 * 1024) ? 2 : 1)
 conv_gemm_kernel(GemmArgs a) {
+    constexpr int BK = KB;
+    constexpr int RB = KB * 2;           // LDS row bytes
+    constexpr int CPR = KB / 8;          // 16-B chunks per row
+    constexpr int RPI = 1024 / RB;       // rows per DMA wave-instruction
     constexpr int NW = WM * WN, NT = NW * 64;
     constexpr int TM = BN / WM / 16;     // 16-channel subtiles per wave
     constexpr int TN = BM / WN / 16;     // 16-pixel subtiles per wave
-    constexpr int AI = BN / 8 / NW;      // A (weight) DMA instructions per wave per stage (8 rows each)
-    constexpr int BI = BM / 8 / NW;      // B (activation) DMA instructions per wave per stage
-    constexpr int STAGE = (BM + BN) * 128;
-    constexpr int NSTAGE = YM_CONV_STAGES;   // LDS ring depth: NSTAGE-1 stages in flight
+    constexpr int AI = BN / RPI / NW;    // A (weight) DMA instructions per wave per stage
+    constexpr int BI = BM / RPI / NW;    // B (activation) DMA instructions per wave per stage
+    constexpr int STAGE = (BM + BN) * RB;
+    constexpr int NSTAGE = NS;
     static_assert(AI >= 1 && BI >= 1, "tile too small for the staging map");
     // one LDS array (a second __shared__ object can de-pipeline LDS-DMA, cdna_hip_programming.md §5)
     __shared__ __attribute__((aligned(16))) char smem[NSTAGE * STAGE];
@@ -115,15 +122,15 @@ conv_gemm_kernel(GemmArgs a) {
     const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
     const uint32_t xld_b = uint32_t(a.x_ld) * 2u;
 
-    // DMA geometry: instruction j of this wave fills rows (wave*I + j)*8 + lane/8, slot lane%8
-    const int lrow = lane >> 3, lslot = lane & 7;
+    // DMA geometry: instruction j of this wave fills rows (wave*I + j)*RPI + lane/CPR, slot lane%CPR
+    const int lrow = lane / CPR, lslot = lane % CPR;
     const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
     uint32_t a_off[AI], a_chk[AI];
 #pragma unroll
     for (int j = 0; j < AI; ++j) {
-        const int r = (wave * AI + j) * 8 + lrow;
+        const int r = (wave * AI + j) * RPI + lrow;
         const int ch = n0 + r;
-        a_chk[j] = uint32_t(lslot ^ fsw(r)) * 8u;          // chunk (in elements) this lane loads
+        a_chk[j] = uint32_t(lslot ^ fsw<RB>(r)) * 8u;      // chunk (in elements) this lane loads
         a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b : OOB;
     }
 
@@ -147,12 +154,12 @@ conv_gemm_kernel(GemmArgs a) {
         uint32_t b_img[BI], b_off[BI], b_chk[BI];
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
-            const int r = (wave * BI + j) * 8 + lrow;
+            const int r = (wave * BI + j) * RPI + lrow;
             const int64_t m = m0 + r;
             const uint32_t um = m < Mc ? uint32_t(m) : 0u;
             const uint32_t n = um / OHW, pix = um - n * OHW;
             const uint32_t i = pix / uint32_t(OWc);
-            b_chk[j] = uint32_t(lslot ^ fsw(r)) * 8u;
+            b_chk[j] = uint32_t(lslot ^ fsw<RB>(r)) * 8u;
             b_img[j] = m < Mc ? (n - nfirst) * uint32_t(a.x_bs) * 2u : OOB;
             b_oh[j] = int(i) * os + py;
             b_ow[j] = int(pix - i * uint32_t(OWc)) * os + px;
@@ -194,7 +201,7 @@ conv_gemm_kernel(GemmArgs a) {
                 const uint32_t kk = uint32_t(k0) + b_chk[j];
                 const uint32_t off = (kk < uint32_t(a.Kin) && b_off[j] != OOB) ? b_off[j] + kk * 2u : OOB;
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    xres, (__attribute__((address_space(3))) void*)(st + BN * 128 + (wave * BI + j) * 1024), 16, off,
+                    xres, (__attribute__((address_space(3))) void*)(st + BN * RB + (wave * BI + j) * 1024), 16, off,
                     0, 0, 0);
             }
             if (++c_next == kc) { c_next = 0; ++t_next; }
@@ -214,12 +221,14 @@ conv_gemm_kernel(GemmArgs a) {
         for (int k = 0; k < nk; ++k) {
             const int buf = k % NSTAGE;
             // this wave's DMAs of stage k have landed (the later stages may stay in flight)
-            if (NSTAGE == 3 && k + 1 < nk) wait_vmcnt<AI + BI>();
+            const int ahead = min(NSTAGE - 2, nk - 1 - k);
+            if (NSTAGE >= 4 && ahead >= 2) wait_vmcnt<(NSTAGE >= 4 ? 2 : 0) * (AI + BI)>();
+            else if (NSTAGE >= 3 && ahead >= 1) wait_vmcnt<(NSTAGE >= 3 ? 1 : 0) * (AI + BI)>();
             else wait_vmcnt<0>();
             raw_barrier();                 // ... everyone's, and everyone finished reading stage k-1
             if (k + NSTAGE - 1 < nk) issue((k + NSTAGE - 1) % NSTAGE);
             const char* As = smem + buf * STAGE;
-            const char* Bs = As + BN * 128;
+            const char* Bs = As + BN * RB;
 #pragma unroll
             for (int kk = 0; kk < BK / 32; ++kk) {
                 const int cch = kk * 4 + fc;
@@ -227,12 +236,12 @@ conv_gemm_kernel(GemmArgs a) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     const int r = wr * (BN / WM) + i * 16 + fr;
-                    af[i] = *reinterpret_cast<const bf16x8*>(As + r * 128 + ((cch ^ fsw(r)) << 4));
+                    af[i] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((cch ^ fsw<RB>(r)) << 4));
                 }
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const int r = wc * (BM / WN) + j * 16 + fr;
-                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * 128 + ((cch ^ fsw(r)) << 4));
+                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((cch ^ fsw<RB>(r)) << 4));
                 }
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
@@ -649,7 +658,7 @@ static bool offsets_fit(int64_t bs, int64_t class_pixels) {
     return bs * 2 * images < (int64_t(1) << 31);
 }
 
-template <int BM, int BN, int WM, int WN, int MODE>
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
 int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     GemmArgs a = a0;
     const int os = a.ostep;
@@ -657,7 +666,7 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1),
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1),
                        dim3(WM * WN * 64), 0, st, a);
     return gx;
 }
@@ -688,12 +697,32 @@ static Tile pick_tile(int64_t Mc, int classes, int nout) {
     return {128, bn};
 }
 
+template <int KB, int NS, int MODE>
+static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
+    if (t.bm == 256) return launch_gemm<256, 128, 2, 4, KB, NS, MODE>(a, max_blocks, st);
+    if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+    if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+    // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
+    return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
+}
+
+// K-stage depth x ring depth; YM_CONV_CFG=32x4 / 32x3 / 64x3 selects the alternatives (A/B runs)
 template <int MODE>
 static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
-    if (t.bm == 256) return launch_gemm<256, 128, 2, 4, MODE>(a, max_blocks, st);
-    if (t.bn == 128) return launch_gemm<128, 128, 2, 2, MODE>(a, max_blocks, st);
-    if (t.bn == 64) return launch_gemm<128, 64, 2, 2, MODE>(a, max_blocks, st);
-    return launch_gemm<128, 32, 2, 2, MODE>(a, max_blocks, st);
+    static const int cfg = [] {
+        const char* e = getenv("YM_CONV_CFG");
+        if (!e) return 0;
+        const std::string v(e);
+        return v == "32x4" ? 1 : v == "32x3" ? 2 : v == "64x3" ? 3 : 0;
+    }();
+    switch (cfg) {
+        case 1: return launch_tile_k<32, 4, MODE>(a, t, max_blocks, st);
+        case 2: return launch_tile_k<32, 3, MODE>(a, t, max_blocks, st);
+        case 3: return launch_tile_k<64, 3, MODE>(a, t, max_blocks, st);
+        default:   // measured per layer (tools/layer_bench.py): 64-channel tiles prefer 32-deep stages
+            return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE>(a, t, max_blocks, st)
+                                             : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
+    }
 }
 
 static int pick_and_launch(GemmArgs a, int mode, int max_blocks, hipStream_t st) {
