@@ -17,6 +17,7 @@
 //   staging offsets are fixed for the whole K loop; T x T tiles, 64 pixels per stage.
 // wgrad_generic_kernel<T>  any other geometry (per-tap columns, fp32 atomics into split 0).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "tile.h"
@@ -47,26 +48,35 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
 }
 
 // ------------------------------------------------------------------ 3x3
-template <int S>
-__global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
+// NWV = 4: waves own (co half, ci half), all 9 taps (144 accumulators, one wave per SIMD);
+// NWV = 8: waves own (co half, ci quarter), all 9 taps (72 accumulators, two waves per SIMD
+// sharing the same staged dz / halo)
+template <int S, int NWV>
+__global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
+    constexpr int NT = NWV * 64;
+    constexpr int TI = 2;                     // 16-co subtiles per wave
+    constexpr int TJ = NWV == 8 ? 1 : 2;      // 16-ci subtiles per wave
+    constexpr int WCI = TJ * 16;              // ci per wave
+    constexpr int RPP = NT / 8;               // staged rows per pass
+    constexpr int DI = 64 / RPP;              // dz chunks per thread
     constexpr int TC = 64;                    // co and ci tile
     constexpr int RSD = TC * 2 + 32;          // dz rows: consecutive-row tr reads conflict free
     constexpr int RSX = S == 1 ? 160 : 144;   // halo rows: reads step S rows (S=2 needs 36-dword rows)
     constexpr int HD = 7 * S + 3;             // halo side
     constexpr int HR = HD * HD;
-    constexpr int XI = (HR * 8 + 255) / 256;  // 16-B halo chunks per thread
+    constexpr int XI = (HR * 8 + NT - 1) / NT;  // 16-B halo chunks per thread
     __shared__ __attribute__((aligned(16))) char Dz[64 * RSD];
     __shared__ __attribute__((aligned(16))) char Xh[HR * RSX];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave >> 1, wc = wave & 1;
+    const int wr = wave / (NWV / 2), wc = wave % (NWV / 2);
     const int co0 = blockIdx.x * TC, ci0 = blockIdx.y * TC;
-    const int sc = tid & 7, srow = tid >> 3;  // staging: chunk sc of rows srow + 32*it
+    const int sc = tid & 7, srow = tid >> 3;  // staging: chunk sc of rows srow + RPP*it
     const bool co_ok = co0 + sc * 8 < a.Cout, ci_ok = ci0 + sc * 8 < a.Cin;
     int x_hy[XI], x_hx[XI];
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
-        const int r = srow + 32 * it;
+        const int r = srow + RPP * it;
         x_hy[it] = r / HD;
         x_hx[it] = r - x_hy[it] * HD;
     }
@@ -84,15 +94,15 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
         hb_hi[kk] = (phi >> 3) * S * HD + (phi & 7) * S;
     }
 
-    f32x4 acc[9][2][2];
+    f32x4 acc[9][TI][TJ];
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 rdz[2], rx[XI];
+    uint4 rdz[DI], rx[XI];
     auto load = [&](int64_t t) {
         const int tw = int(t % ntw);
         const int64_t r = t / ntw;
@@ -101,8 +111,8 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
         const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + int64_t(n) * a.dz_bs, a.dz_bs * 2);
         const __amdgpu_buffer_rsrc_t rxs = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            const int p = srow + 32 * it;
+        for (int it = 0; it < DI; ++it) {
+            const int p = srow + RPP * it;
             const int oh = oh0 + (p >> 3), ow = ow0 + (p & 7);
             const bool ok = co_ok && oh < a.OH && ow < a.OW;
             rdz[it] = buf_load16(rd, ok ? uint32_t(((oh * a.OW + ow) * int(a.dz_ld) + co0 + sc * 8) * 2) : OOB);
@@ -111,18 +121,18 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
 #pragma unroll
         for (int it = 0; it < XI; ++it) {
             const int ih = ih0 + x_hy[it], iw = iw0 + x_hx[it];
-            const bool ok = ci_ok && srow + 32 * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
+            const bool ok = ci_ok && srow + RPP * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
             rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + sc * 8) * 2) : OOB);
         }
     };
     auto store = [&]() {
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
-            *reinterpret_cast<uint4*>(Dz + (srow + 32 * it) * RSD + sc * 16) = rdz[it];
+        for (int it = 0; it < DI; ++it)
+            *reinterpret_cast<uint4*>(Dz + (srow + RPP * it) * RSD + sc * 16) = rdz[it];
 #pragma unroll
         for (int it = 0; it < XI; ++it)
-            if (srow + 32 * it < HR)
-                *reinterpret_cast<uint4*>(Xh + (srow + 32 * it) * RSX + sc * 16) = h8_to_bf8(rx[it]);
+            if (srow + RPP * it < HR)
+                *reinterpret_cast<uint4*>(Xh + (srow + RPP * it) * RSX + sc * 16) = h8_to_bf8(rx[it]);
     };
 
     if (t_begin < t_end) {
@@ -135,9 +145,9 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
         if (more) load(t + 1);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-            bf16x8 af[2];
+            bf16x8 af[TI];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < TI; ++i) {
                 const int col = (wr * 32 + i * 16 + 4 * pp) * 2;
                 af[i] = tr_frag(Dz + (kk * 32 + 4 * g + q) * RSD + col, Dz + (kk * 32 + 16 + 4 * g + q) * RSD + col);
             }
@@ -146,16 +156,16 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw) {
                     const int toff = kh * HD + kw;
-                    bf16x8 bfr[2];
+                    bf16x8 bfr[TJ];
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) {
-                        const int col = (wc * 32 + j * 16 + 4 * pp) * 2;
+                    for (int j = 0; j < TJ; ++j) {
+                        const int col = (wc * WCI + j * 16 + 4 * pp) * 2;
                         bfr[j] = tr_frag(Xh + (hb_lo[kk] + toff) * RSX + col, Xh + (hb_hi[kk] + toff) * RSX + col);
                     }
 #pragma unroll
-                    for (int i = 0; i < 2; ++i)
+                    for (int i = 0; i < TI; ++i)
 #pragma unroll
-                        for (int j = 0; j < 2; ++j)
+                        for (int j = 0; j < TJ; ++j)
                             acc[kh * 3 + kw][i][j] =
                                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[kh * 3 + kw][i][j], 0, 0, 0);
                 }
@@ -172,10 +182,10 @@ __global__ void __launch_bounds__(256) wgrad3_kernel(WgArgs a) {
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int ci = ci0 + wc * 32 + j * 16 + (lane & 15);
+            for (int j = 0; j < TJ; ++j) {
+                const int ci = ci0 + wc * WCI + j * 16 + (lane & 15);
                 if (ci >= a.Cin) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
@@ -499,10 +509,18 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
         splits = 0;
     } else if (p.kind == 3) {
         YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
-        if (d->stride == 1)
-            hipLaunchKernelGGL(wgrad3_kernel<1>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
-        else
-            hipLaunchKernelGGL(wgrad3_kernel<2>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+        static const bool w4 = [] {            // YM_WGRAD_WAVES=4: the one-wave-per-SIMD form (A/B runs)
+            const char* e = getenv("YM_WGRAD_WAVES");
+            return e && atoi(e) == 4;
+        }();
+        const dim3 grid(p.co_t, p.ci_t, unsigned(splits));
+        if (d->stride == 1) {
+            if (w4) hipLaunchKernelGGL((wgrad3_kernel<1, 4>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((wgrad3_kernel<1, 8>), grid, dim3(512), 0, st, a);
+        } else {
+            if (w4) hipLaunchKernelGGL((wgrad3_kernel<2, 4>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((wgrad3_kernel<2, 8>), grid, dim3(512), 0, st, a);
+        }
     } else if (p.kind == 1) {
         if (p.T == 128)
             hipLaunchKernelGGL(wgrad1_kernel<128>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
