@@ -116,3 +116,23 @@ def test_precision_model_restores_and_rounds():
     for r, e in zip(ref, emu):
         err = float((r - e).norm() / r.norm())
         assert 0 < err < 2e-2
+
+
+def test_oracle_training_curve_first_steps(golden):
+    """The oracle's train loop (AdamW, clip 10) reproduces the reference's curve (curve.npz)."""
+    from datasets.synthetic import synth_batch
+    d = golden("curve.npz")
+    layers, save, P = om.build(om.load_cfg("n"))
+    params = [v.requires_grad_(True) for k, v in P.items()
+              if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")]
+    opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
+    for step in range(3):
+        b = synth_batch(4, 320, seed=100 + step)
+        np.testing.assert_allclose([b["img"].double().sum(), b["bboxes"].double().sum(), len(b["cls"])],
+                                   d["batch_sums"][step], rtol=1e-9)
+        opt.zero_grad(set_to_none=True)
+        loss, items = ol.v8_loss(om.forward(P, layers, save, b["img"], training=True), b)
+        loss.backward()
+        gn = torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
+        opt.step()
+        np.testing.assert_allclose([float(loss), *items.tolist(), float(gn)], d["rows"][step], rtol=1e-4)

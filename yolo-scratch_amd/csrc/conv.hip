@@ -84,7 +84,7 @@ __device__ __forceinline__ void raw_barrier() {
 
 // WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile; KB-deep K stages
 // (rows of KB*2 bytes), an NS-stage LDS ring with NS-1 stages in flight
-template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE, int ABL = 0>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NS * (BM + BN) * KB * 2 <= 72 * 1024) ? 2 : 1)
 conv_gemm_kernel(GemmArgs a) {
     constexpr int BK = KB;
@@ -217,7 +217,7 @@ conv_gemm_kernel(GemmArgs a) {
         raw_barrier();                     // previous tile's readers are done with every stage
 #pragma unroll
         for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
-            if (s0 < nk) issue(s0);
+            if (s0 < nk && ABL != 2) issue(s0);
         for (int k = 0; k < nk; ++k) {
             const int buf = k % NSTAGE;
             // this wave's DMAs of stage k have landed (the later stages may stay in flight)
@@ -226,7 +226,7 @@ conv_gemm_kernel(GemmArgs a) {
             else if (NSTAGE >= 3 && ahead >= 1) wait_vmcnt<(NSTAGE >= 3 ? 1 : 0) * (AI + BI)>();
             else wait_vmcnt<0>();
             raw_barrier();                 // ... everyone's, and everyone finished reading stage k-1
-            if (k + NSTAGE - 1 < nk) issue((k + NSTAGE - 1) % NSTAGE);
+            if (k + NSTAGE - 1 < nk && ABL != 2) issue((k + NSTAGE - 1) % NSTAGE);   // ABL 2: no staging
             const char* As = smem + buf * STAGE;
             const char* Bs = As + BN * RB;
 #pragma unroll
@@ -247,7 +247,9 @@ conv_gemm_kernel(GemmArgs a) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
+                        if constexpr (ABL == 1) {          // ABL 1 (timing only): no MFMA
+                            acc[i][j][0] += float(af[i][0]) * float(bfr[j][0]);
+                        } else if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
                                                                                __builtin_bit_cast(f16x8, bfr[j]),
                                                                                acc[i][j], 0, 0, 0);
@@ -666,8 +668,18 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), dim3(gx, ntiles, os == 2 ? 4 : 1),
-                       dim3(WM * WN * 64), 0, st, a);
+    // YM_CONV_ABLATE=nomma|nodma: timing-only builds without the MFMAs / without the staging
+    static const int abl = [] {
+        const char* e = getenv("YM_CONV_ABLATE");
+        return !e ? 0 : std::string(e) == "nomma" ? 1 : std::string(e) == "nodma" ? 2 : 0;
+    }();
+    const dim3 grid(gx, ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
+    if (abl == 1)
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, 1>), grid, block, 0, st, a);
+    else if (abl == 2)
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, 2>), grid, block, 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), grid, block, 0, st, a);
     return gx;
 }
 
