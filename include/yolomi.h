@@ -74,6 +74,38 @@ int ym_nms(const float* boxes, const float* scores, int64_t n, float iou_thr, vo
            size_t workspace_bytes, int64_t* keep, int32_t* count, void* stream);
 
 
+/* ------------------------------------------------------------------ detection metrics
+ * Replaces evaluate_detections / calculate_iou_batch / calculate_ap
+ * (utils/metrics.py:49-81, :84-274, :277-323).
+ */
+
+/* Workspace bytes for ym_eval_detections. */
+size_t ym_eval_workspace_size(int64_t n_img, int64_t n_pred, int n_thr);
+
+/* evaluate_detections over n_img images, all on the device, no host sync.
+ * Predictions of image b are rows pred_off[b]..pred_off[b+1) of pred_boxes (xyxy fp32,
+ * n_pred x 4) / pred_scores; its GT boxes rows gt_off[b]..gt_off[b+1) of gt_boxes
+ * (n_gt x 4).  pred_off / gt_off are device int64 arrays of n_img+1 prefix offsets.
+ * thresholds (host, n_thr <= 15 doubles) are the IoU thresholds matched at once;
+ * the first n_ap give mAP50-95 (their mean) and mAP50 (the first); pr_index selects
+ * the threshold precision / recall are counted at (the reference uses 0.5).
+ * max_gt_per_img <= 4096.  out (device, n_thr + 7 doubles): AP per threshold, then
+ * precision, recall, mAP50, mAP50-95, TP, FP, predictions kept by conf. */
+int ym_eval_detections(const float* pred_boxes, const float* pred_scores, const int64_t* pred_off,
+                       const float* gt_boxes, const int64_t* gt_off, int64_t n_img, int64_t n_pred, int64_t n_gt,
+                       int64_t max_gt_per_img, const double* thresholds, int n_thr, int n_ap, int pr_index,
+                       float conf, void* workspace, size_t workspace_bytes, double* out, void* stream);
+
+/* calculate_ap (utils/metrics.py:277-323) on one flat detection list: scores[n] and
+ * is_tp[n] (0/1); workspace ym_eval_workspace_size(1, n, 1).  out (device, 8 doubles):
+ * out[0] = AP (0 when n_gt == 0 or n == 0), the rest as ym_eval_detections. */
+int ym_eval_ap(const float* scores, const uint8_t* is_tp, int64_t n, int64_t n_gt, void* workspace,
+               size_t workspace_bytes, double* out, void* stream);
+
+/* calculate_iou_batch (utils/metrics.py:49-81): out[i*m+j] = IoU(boxes1[i], boxes2[j]),
+ * xyxy fp32 in the reference's op order. */
+int ym_iou_matrix(const float* boxes1, const float* boxes2, int64_t n, int64_t m, float* out, void* stream);
+
 /* ------------------------------------------------------------------ convolution
  * Replaces nn.Conv2d forward/backward inside Conv (models/yolo11_modules.py:21-33)
  * and the Detect head's bias convs (:221-234).  NHWC; fp16 forward / bf16 backward MFMA, fp32 accumulate.

@@ -136,3 +136,23 @@ def test_oracle_training_curve_first_steps(golden):
         gn = torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
         opt.step()
         np.testing.assert_allclose([float(loss), *items.tolist(), float(gn)], d["rows"][step], rtol=1e-4)
+
+
+def test_metrics_oracle_matches_reference(golden):
+    """oracle/metrics.py reproduces the reference's evaluate_detections on its own run."""
+    from oracle import metrics as omet
+    from metrics_cases import golden_case
+    d = golden("metrics.npz")
+    preds, tgts = golden_case(d)
+    r = omet.evaluate_detections(preds, tgts, 0.25, 0.5)
+    got = [r["precision"], r["recall"], r["mAP50"], r["mAP50-95"]]
+    assert got == list(d["out"])
+
+
+def test_metrics_oracle_ap_tie_order():
+    """calculate_ap: on equal scores the TPs come first (the stable sort of tp + fp lists)."""
+    from oracle import metrics as omet
+    # one TP and one FP at the same score: TP first -> precision 1 at the recall step
+    assert omet.calculate_ap([0.5], [0.5], 1) == pytest.approx(1.0 / (1 + 1e-6))
+    assert omet.calculate_ap([], [0.9], 3) == 0.0
+    assert omet.calculate_ap([0.9], [], 0) == 0.0

@@ -20,3 +20,8 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
     python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof_bench.json 2> $OUT/prof_bench.err
 echo "rocprof exit $?"
 find $OUT/prof -name "*stats*" | head
+timeout -k 10 300 python3 $R/tools/eval_bench.py > $OUT/eval_bench.json 2> $OUT/eval_bench.err || { echo "eval bench failed $?"; tail -20 $OUT/eval_bench.err; exit 1; }
+cat $OUT/eval_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_eval -o run -- \
+    python3 $R/tools/eval_bench.py --reps 5 --cpu-images 5 > $OUT/prof_eval.json 2> $OUT/prof_eval.err
+echo "rocprof eval exit $?"

@@ -101,11 +101,7 @@ def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_thre
         batches += 1
         if max_batches is not None and batches >= max_batches:
             break
-    for p in all_predictions:
-        for k in ("boxes", "scores", "labels"):
-            p[k] = p[k].cpu()
-    for t in all_targets:
-        t["boxes"], t["labels"] = t["boxes"].cpu(), t["labels"].cpu()
+    # predictions and targets stay in HBM: the metrics run on the GPU (utils/metrics.py)
     metrics = evaluate_detections(all_predictions, all_targets, conf_threshold=conf_threshold, iou_threshold=0.5)
     nb = batches if max_batches else len(dataloader)
     s = (sums / max(nb, 1)).tolist()

@@ -1,3 +1,3 @@
-from .metrics import evaluate_detections, calculate_iou
+from .metrics import calculate_ap, calculate_iou, calculate_iou_batch, evaluate_detections, evaluate_packed
 
-__all__ = ["evaluate_detections", "calculate_iou"]
+__all__ = ["evaluate_detections", "evaluate_packed", "calculate_ap", "calculate_iou", "calculate_iou_batch"]
