@@ -12,7 +12,8 @@ for r in rows:
     n = r["Name"]
     k = re.sub(r"\(.*", "", n.replace("ym::(anonymous namespace)::", "").replace("void ", ""))
     if "conv_gemm" in n:
-        k = "conv_gemm " + ("fwd" if n.split("<")[1].split(">")[0].endswith(" 0") else "dgrad")
+        targs = [t.strip() for t in n.split("<")[1].split(">")[0].split(",")]
+        k = "conv_gemm " + ("fwd" if targs[6] == "0" else "dgrad")   # <BM,BN,WM,WN,KB,NS,MODE,ABL>
     else:
         k = re.sub(r"<.*", "", k)
     fam[k][0] += float(r["TotalDurationNs"]) / 1e6 / steps

@@ -76,6 +76,7 @@ class Buckets:
             self._close(start, size, cur)
         self.handles = []
         self.remaining = []
+        self.side_stream = None    # callable -> the producing plan's side stream (or None)
 
     def _close(self, start, size, members):
         b = len(self.ranges)
@@ -100,7 +101,16 @@ class Buckets:
 
     def _launch(self, b):
         s, e = self.ranges[b]
-        self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+        side = self.side_stream() if self.side_stream else None
+        if side is None:
+            self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+        else:
+            # the bucket's gradients come from both streams (BN on the main one, weight gradients on
+            # the plan's side stream): the collective is issued from the side stream after it has
+            # caught up with the main stream, so RCCL orders it after both
+            side.wait_stream(torch.cuda.current_stream(side.device))
+            with torch.cuda.stream(side):
+                self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
         self.launched[b] = True
 
     def finish(self, world: int):
@@ -125,6 +135,7 @@ class GradSync:
         """Hook the plan's backward so the NEXT backward launches buckets as it goes."""
         self.plan = plan
         self.buckets = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
+        self.buckets.side_stream = lambda _p=plan: _p.side_stream
 
         def hook(params, _b=self.buckets):
             if not _b.remaining:

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -234,10 +235,10 @@ class ConvBN:
             call("ym_view_axpy", dy, self.y.bs, self.y.ld, self.res.gptr(), self.res.bs, self.res.ld, self.M, self.co,
                  self.HW, acc, 0, st)
             self.res.mark()
-        # weight gradient
+        # weight gradient: on the side stream, beside this layer's data gradient and the next BN backward
         ws = plan.wgrad_ws()
         call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
-             plan.gptr(self.m.conv.weight), 0, st)
+             plan.gptr(self.m.conv.weight), 0, plan.side(st))
         # data gradient
         if plan.needs_grad(self.x):
             acc = self.x.grad_for_write(st)
@@ -509,12 +510,14 @@ class HeadLevel:
         call("ym_head_grad", plan.dhead.data_ptr(), A, self.a_off, self.HW, self.M, self.nc, self.dzb.data_ptr(),
              self.dzc.data_ptr(), plan.gptr(self.box.bias), plan.gptr(self.cls.bias), st)
         ws = plan.wgrad_ws()
+        sst = plan.side(st)
         call("ym_conv_wgrad", ctypes.byref(self.bb), self.dzb.data_ptr(), self.xb.ptr(), ws.data_ptr(), ws.numel() * 4,
-             plan.gptr(self.box.weight), 0, st)
+             plan.gptr(self.box.weight), 0, sst)
         call("ym_conv_wgrad", ctypes.byref(self.bc), self.dzc.data_ptr(), self.xc.ptr(), ws.data_ptr(), ws.numel() * 4,
-             self.wsc.data_ptr(), 0, st)
+             self.wsc.data_ptr(), 0, sst)
         g = plan.grad_view(self.cls.weight).view(self.nc, -1)
-        g.copy_(self.wsc[: self.nc])
+        with torch.cuda.stream(plan.side_stream or torch.cuda.current_stream(plan.dev)):
+            g.copy_(self.wsc[: self.nc])
         for d, dz, wt, x in ((self.bb, self.dzb, self.wb_t, self.xb), (self.bc, self.dzc, self.wc_t, self.xc)):
             acc = x.grad_for_write(st)
             d.accumulate = acc
@@ -548,6 +551,7 @@ class Plan:
         self.dhead = None
         self._scratch = []
         self.grad_hook = None      # called with each op's finished parameters during backward (DP buckets)
+        self.side_stream = None    # weight-gradient stream (see side())
         # flat parameter-gradient buffer; each .grad is a view of it
         params = [p for p in root.parameters() if p.requires_grad]
         self.params = params
@@ -557,6 +561,31 @@ class Plan:
         for p, n in zip(params, sizes):
             self.grad_views[id(p)] = self.grad_flat[off:off + n].view(p.shape)
             off += n
+
+    # --------------------------------------------------------------- side stream (weight gradients)
+    # Weight gradients only read dz and the forward activation, and only write their own slice of
+    # grad_flat, so they run on a second HIP stream: each conv's wgrad starts once its dz is ready
+    # (an event on the main stream) and overlaps that layer's dgrad and the next ops' BN backward;
+    # small late layers fill the chip together instead of each draining it.  The wgrads stay ordered
+    # among themselves (they share the split-K workspace).  YM_SIDE_STREAM=0 runs them in line.
+    def side(self, st):
+        """Side-stream pointer for a launch that depends on everything issued so far on `st`."""
+        s = self.side_stream
+        if s is None:
+            return st
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        return s.cuda_stream
+
+    def _begin_side(self):
+        use = self.dev.type == "cuda" and os.environ.get("YM_SIDE_STREAM", "1") != "0"
+        if use and self.side_stream is None:
+            self.side_stream = torch.cuda.Stream(device=self.dev)
+        elif not use:
+            self.side_stream = None
+
+    def _join_side(self):
+        if self.side_stream is not None:
+            torch.cuda.current_stream(self.dev).wait_stream(self.side_stream)
 
     def act(self, C, H, W, name=""):
         return View(Act(self, C, H, W, name=name))
@@ -597,10 +626,12 @@ class Plan:
         for t in self._scratch:
             t.zero_()
         hook = self.grad_hook
+        self._begin_side()
         for op in reversed(self.ops):
             op.backward(self, st)
             if hook is not None:
                 hook(op_params(op))
+        self._join_side()
 
     def install_grads(self):
         """Expose the flat buffer as parameter .grad (accumulating if a grad already exists)."""
@@ -878,8 +909,10 @@ def run_block(module, x: torch.Tensor):
             plan.grad_flat.zero_()
             for t in plan._scratch:
                 t.zero_()
+            plan._begin_side()
             for op in reversed(plan.ops):
                 op.backward(plan, st)
+            plan._join_side()
         plan.backward_from_output = backward_from_output
         cache[key] = plan
     anchor = module.__dict__.setdefault("_ym_anchor", torch.zeros(1, requires_grad=True))
