@@ -129,8 +129,19 @@ typedef struct {
     int32_t cout_t;            /* row length of dst_t (>= cout; zero padding is the caller's) */
 } ym_wprep_entry;
 
-/* Number of grid-x blocks (= rows of the BN statistics partials) ym_conv_fwd uses. */
+/* Number of grid-x blocks (= rows of the BN statistics partials) of the implicit-GEMM forward
+ * for m output pixels (kept for callers sizing buffers by shape only). */
 int ym_conv_stat_blocks(int64_t m, int cout);
+/* Rows of the BN statistics partials ym_conv_fwd writes for this conv (the halo-staged 3x3
+ * kernel and the implicit GEMM use different grids); size stat_sum / stat_sq with it. */
+int ym_conv_fwd_stat_rows(const ym_conv_desc* d);
+/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 1 = the
+ * halo-staged 3x3 stride-1 kernel, 0 = the implicit GEMM. */
+int ym_conv_algo(const ym_conv_desc* d, int dgrad);
+/* Selection policy of the halo-staged kernel for later calls: -1 YM_CONV_HALO / default, 0 never,
+ * 1 wherever it applies, 2 where it measured faster (default: maps <= 24 wide).  Returns the
+ * previous setting.  Process-wide; not for use while other threads launch convolutions. */
+int ym_conv_set_halo(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
  * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
@@ -147,15 +158,19 @@ int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, 
 /* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0). */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
+/* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
+ * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). cout <= 128. */
+size_t ym_conv_first_wgrad_workspace_size(int cout);
 int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
-                        int cout, int stride, int pad, void* stream);
+                        int cout, int stride, int pad, float* workspace, size_t workspace_bytes, void* stream);
 /* Depthwise 3x3 s1 p1 (Attention.pe, yolo11_modules.py:122); input channel c reads source
  * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
 int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks, void* stream);
+size_t ym_dw3x3_bwd_workspace_size(int c);
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
-                 int c, int accumulate, void* stream);
+                 int c, int accumulate, float* workspace, size_t workspace_bytes, void* stream);
 /* All conv weights fp32 OIHW -> fp16 forward / bf16 dgrad layouts in one launch (table in device memory). */
 int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream);
 
@@ -210,8 +225,10 @@ int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t ld, int64_t 
                    void* stream);
 /* dhead (B, A, 64+nc) fp32 rows of one pyramid level -> bf16 dz for the box / cls 1x1 convs
  * (cls zero-padded to 8 channels) and bias grads (+=). */
+size_t ym_head_grad_workspace_size(void);
 int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc, uint16_t* dz_box,
-                 uint16_t* dz_cls, float* dbias_box, float* dbias_cls, void* stream);
+                 uint16_t* dz_cls, float* dbias_box, float* dbias_cls, float* workspace, size_t workspace_bytes,
+                 void* stream);
 int ym_attn_fwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, int b, int heads, int n, int key_dim, int head_dim,
                 float scale, uint16_t* out, int64_t o_bs, int64_t o_ld, float* lse, void* stream);
 size_t ym_attn_workspace_size(int b, int heads, int n);

@@ -32,6 +32,13 @@ SHAPES = [
     (1, 5, 7, 520, 264, 3, 1, 1),
     (2, 9, 9, 256, 136, 1, 1, 0),
     (2, 33, 17, 64, 64, 3, 1, 1),
+    # halo-staged 3x3 stride-1 kernel (conv_halo.hip): 16-wide tiles, whole-row tiles (20, 40, 10
+    # wide), 8-wave 256x128 tiles, channel counts that are not multiples of the 32-channel chunk
+    (2, 32, 32, 64, 128, 3, 1, 1),
+    (5, 20, 20, 96, 64, 3, 1, 1),
+    (1, 40, 40, 128, 136, 3, 1, 1),
+    (16, 64, 64, 32, 128, 3, 1, 1),
+    (3, 24, 10, 72, 80, 3, 1, 1),
     # narrow inputs: several taps share one 64-deep K step (fwd Kin = cin, dgrad Kin = cout)
     (2, 9, 7, 64, 32, 3, 1, 1),
     (1, 10, 10, 8, 16, 3, 1, 1),
@@ -50,8 +57,17 @@ def _desc(n, h, w, cin, cout, k, s, p):
     return d, oh, ow
 
 
+@pytest.fixture(params=["auto", "halo"])
+def halo_mode(request):
+    """Run each shape under the default kernel selection and with the halo kernel wherever it applies."""
+    from yolomi._lib import lib
+    prev = lib().ym_conv_set_halo(2 if request.param == "auto" else 1)
+    yield request.param
+    lib().ym_conv_set_halo(prev)
+
+
 @pytest.mark.parametrize("shape", SHAPES, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in SHAPES])
-def test_conv_kernels_vs_torch(shape):
+def test_conv_kernels_vs_torch(shape, halo_mode):
     from yolomi._lib import call
     n, h, w, cin, cout, k, s, p = shape
     d, oh, ow = _desc(*shape)
@@ -104,6 +120,29 @@ def test_conv_kernels_vs_torch(shape):
         # pixels at odd rows or odd columns receive no tap
         dxc = dx.float().cpu()
         assert (dxc[:, 1::2] == 0).all() and (dxc[:, :, 1::2] == 0).all()
+
+
+HALO = [(2, 32, 32, 64, 128, 3, 1, 1), (5, 20, 20, 96, 64, 3, 1, 1), (1, 40, 40, 128, 136, 3, 1, 1),
+        (16, 64, 64, 32, 128, 3, 1, 1), (3, 24, 10, 72, 80, 3, 1, 1), (2, 33, 17, 64, 64, 3, 1, 1)]
+
+
+def test_halo_kernel_selected(halo_mode):
+    """The 3x3 stride-1 shapes above with >= 64 output channels run the halo kernel (fwd) when forced;
+    by default only maps <= 24 wide do."""
+    from yolomi._lib import lib
+    if halo_mode == "auto":
+        d, _, _ = _desc(5, 20, 20, 96, 64, 3, 1, 1)
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 1
+        d, _, _ = _desc(1, 40, 40, 128, 136, 3, 1, 1)
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 0
+        return
+    for shape in HALO:
+        d, _, _ = _desc(*shape)
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 1, shape
+    d, _, _ = _desc(2, 32, 32, 64, 128, 3, 1, 1)
+    assert lib().ym_conv_algo(ctypes.byref(d), 1) == 1          # dgrad: 64 output channels
+    d, _, _ = _desc(2, 9, 11, 64, 96, 3, 2, 1)
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) == 0          # stride 2: implicit GEMM
 
 
 def test_dgrad_accumulate_stride2():

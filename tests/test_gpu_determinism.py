@@ -1,0 +1,54 @@
+"""Bit-reproducibility of a training step on the GPU.
+
+Every reduction in the HIP path runs in a fixed order (per-block partial rows summed in row order,
+waves combined in wave order; no float atomics), so the same step on the same inputs gives
+bit-identical heads, loss and parameter gradients — across repeated runs and with the weight
+gradients on the side stream or in line.  (The reference is a single-process fp32 PyTorch loop;
+reproducibility is what lets tests/test_gpu_curve.py compare 20-step curves without run-to-run drift.)
+"""
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(model, crit, b):
+    model.zero_grad(set_to_none=True)
+    heads = model(b["img"])
+    loss, items = crit(heads, b)
+    loss.backward()
+    torch.cuda.synchronize()
+    return (heads.detach().clone() if torch.is_tensor(heads) else [h.detach().clone() for h in heads],
+            loss.detach().clone(), items.detach().clone(),
+            [p.grad.detach().clone() for p in model.parameters() if p.grad is not None])
+
+
+def test_train_step_bit_reproducible():
+    from oracle import model as om
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    cfg = om.load_cfg("n")
+    _, _, P = om.build(cfg)
+    m = build_yolo11(cfg, ch=1, nc=5)
+    m.load_state_dict(P)
+    m = m.cuda().train()
+    crit = v8DetectionLoss(m)
+    b = {k: v.cuda() for k, v in synth_batch(4, 320, seed=11).items()}
+    # BatchNorm running statistics move every step; restore them so each step sees the same model
+    bufs = {k: v.clone() for k, v in m.state_dict().items()}
+    runs = []
+    for side in ("1", "1", "0"):
+        os.environ["YM_SIDE_STREAM"] = side
+        m.load_state_dict(bufs)
+        runs.append(_step(m, crit, b))
+    os.environ.pop("YM_SIDE_STREAM", None)
+    ref = runs[0]
+    for other in runs[1:]:
+        for a, c in zip(ref[0], other[0]):
+            assert torch.equal(a, c)
+        assert torch.equal(ref[1], other[1]) and torch.equal(ref[2], other[2])
+        for i, (a, c) in enumerate(zip(ref[3], other[3])):
+            assert torch.equal(a, c), f"parameter {i}: max |diff| {float((a - c).abs().max())}"

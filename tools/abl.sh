@@ -1,6 +1,8 @@
 set -o pipefail
-mkdir -p gpurun_out/abl
-for A in none nomma nodma; do
-  YM_CONV_ABLATE=$A timeout -k 10 200 python3 tools/layer_bench.py --only 6 11 48 73 21 5 52 --reps 20 > gpurun_out/abl/$A.txt 2>&1 || exit 1
+mkdir -p gpurun_out/pin
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_conv.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pin/conv_tests.log 2>&1 || { tail -40 gpurun_out/pin/conv_tests.log; exit 1; }
+tail -1 gpurun_out/pin/conv_tests.log
+for V in "X=0" "YM_CONV_HALO=0"; do
+  env $V timeout -k 10 240 python3 tools/layer_bench.py --reps 10 > gpurun_out/pin/$V.txt 2>&1 || exit 1
 done
-YM_CONV_TILE=256 timeout -k 10 200 python3 tools/layer_bench.py --only 6 11 48 73 21 5 52 --reps 20 > gpurun_out/abl/t256.txt 2>&1 || exit 1
+tail -1 gpurun_out/pin/*.txt

@@ -28,6 +28,8 @@
 #include <string>
 
 #include "common.h"
+#include "conv_halo.h"
+#include "reduce.h"
 #include "tile.h"
 
 namespace ym {
@@ -229,34 +231,46 @@ conv_gemm_kernel(GemmArgs a) {
             if (k + NSTAGE - 1 < nk && ABL != 2) issue((k + NSTAGE - 1) % NSTAGE);   // ABL 2: no staging
             const char* As = smem + buf * STAGE;
             const char* Bs = As + BN * RB;
+            // fragments of both 32-deep halves first, then the MFMAs (two register sets; the order is
+            // pinned with sched_group_barrier: left to itself the compiler re-reads one A fragment at a
+            // time behind an lgkmcnt(0), exposing the LDS latency every 4 MFMAs)
+            constexpr int KS = BK / 32;
+            bf16x8 af[KS][TM], bfr[KS][TN];
 #pragma unroll
-            for (int kk = 0; kk < BK / 32; ++kk) {
+            for (int kk = 0; kk < KS; ++kk) {
                 const int cch = kk * 4 + fc;
-                bf16x8 af[TM], bfr[TN];
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     const int r = wr * (BN / WM) + i * 16 + fr;
-                    af[i] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((cch ^ fsw<RB>(r)) << 4));
+                    af[kk][i] = *reinterpret_cast<const bf16x8*>(As + r * RB + ((cch ^ fsw<RB>(r)) << 4));
                 }
 #pragma unroll
                 for (int j = 0; j < TN; ++j) {
                     const int r = wc * (BM / WN) + j * 16 + fr;
-                    bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((cch ^ fsw<RB>(r)) << 4));
+                    bfr[kk][j] = *reinterpret_cast<const bf16x8*>(Bs + r * RB + ((cch ^ fsw<RB>(r)) << 4));
                 }
+            }
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
                         if constexpr (ABL == 1) {          // ABL 1 (timing only): no MFMA
-                            acc[i][j][0] += float(af[i][0]) * float(bfr[j][0]);
+                            acc[i][j][0] += float(af[kk][i][0]) * float(bfr[kk][j][0]);
                         } else if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
-                                                                               __builtin_bit_cast(f16x8, bfr[j]),
-                                                                               acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                                __builtin_bit_cast(f16x8, af[kk][i]), __builtin_bit_cast(f16x8, bfr[kk][j]), acc[i][j],
+                                0, 0, 0);
                         else                              // bf16 gradients x bf16 weights
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0,
+                                                                               0, 0);
                     }
             }
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
         }
 
         // epilogue: D[channel][pixel]; lane holds 4 consecutive channels of one pixel
@@ -355,6 +369,35 @@ conv_gemm_kernel(GemmArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ fixed-order wave combines (no float atomics)
+// After the xor reductions, lane l < G of every wave holds the sums of channel group l (channels
+// 8l..8l+7); the 4 waves are combined in wave order so every run rounds identically.
+__device__ __forceinline__ void ordered_wave_add8(float* rs, float* rq, const float* ls, const float* lq, int g, int G) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w && lane < G)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                rs[g * 8 + r] = (w ? rs[g * 8 + r] : 0.f) + ls[r];
+                rq[g * 8 + r] = (w ? rq[g * 8 + r] : 0.f) + lq[r];
+            }
+        __syncthreads();
+    }
+}
+__device__ __forceinline__ void ordered_wave_add72(float* red, const float (*acc)[9], int g, int G) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    for (int w = 0; w < 4; ++w) {
+        if (wave == w && lane < G)
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) red[(g * 8 + r) * 9 + t] = (w ? red[(g * 8 + r) * 9 + t] : 0.f) + acc[r][t];
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ stem conv (Cin = 1), fp32 image input
 // one thread per (output pixel, 8 channels), the 8x9 weights in registers, 32-bit index math
 // (N*OH*OW and N*H*W < 2^31, checked on the host).  HBM-bound: writes the fp16 z (2 B/elem).
@@ -365,7 +408,6 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
     __shared__ float red[2][512];
     const int G = Cout >> 3;                 // channel groups (divides 64)
     const int g = threadIdx.x % G;
-    for (int i = threadIdx.x; i < 2 * Cout; i += 256) red[i / Cout][i % Cout] = 0.f;
     float wr[8][9];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -404,35 +446,28 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
         o.w = uint32_t(f2h(v[6])) | (uint32_t(f2h(v[7])) << 16);
         *reinterpret_cast<uint4*>(y + size_t(m) * Cout + g * 8) = o;
     }
-    // lanes with the same channel group: xor-reduce over the other lane bits, then across waves
+    // lanes with the same channel group: xor-reduce over the other lane bits, then the waves in order
 #pragma unroll
     for (int r = 0; r < 8; ++r)
         for (int o = G; o < 64; o <<= 1) {
             ls[r] += __shfl_xor(ls[r], o, 64);
             lq[r] += __shfl_xor(lq[r], o, 64);
         }
-    __syncthreads();
-    if ((threadIdx.x & 63) < G)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            atomicAdd(&red[0][g * 8 + r], ls[r]);
-            atomicAdd(&red[1][g * 8 + r], lq[r]);
-        }
-    __syncthreads();
+    ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < Cout; c += 256) {
         st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
         st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
     }
 }
 
-// dW[co][t] += sum_p dz[p][co] * patch(p)[t]   (no dgrad: the image needs no gradient)
+// part[block][co*9 + t] = sum over the block's pixels p of dz[p][co] * patch(p)[t]  (no dgrad: the
+// image needs no gradient); dW += the rows summed in order (colsum_kernel)
 __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __restrict__ dz, const float* __restrict__ img,
-                                                               float* __restrict__ dw, int N, int H, int W, int OH,
+                                                               float* __restrict__ part, int N, int H, int W, int OH,
                                                                int OW, int Cout, int stride, int pad) {
-    __shared__ float red[512 * 9];
+    __shared__ float red[128 * 9];
     const int G = Cout >> 3;
     const int g = threadIdx.x % G;
-    for (int i = threadIdx.x; i < Cout * 9; i += 256) red[i] = 0.f;
     float acc[8][9];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -466,14 +501,8 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) < G)
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-#pragma unroll
-            for (int t = 0; t < 9; ++t) atomicAdd(&red[(g * 8 + r) * 9 + t], acc[r][t]);
-    __syncthreads();
-    for (int i = threadIdx.x; i < Cout * 9; i += 256) atomicAdd(&dw[i], red[i]);
+    ordered_wave_add72(red, acc, g, G);
+    for (int i = threadIdx.x; i < Cout * 9; i += 256) part[int64_t(blockIdx.x) * Cout * 9 + i] = red[i];
 }
 
 // ------------------------------------------------------------------ depthwise 3x3, stride 1, pad 1
@@ -502,7 +531,6 @@ __device__ __forceinline__ void unpack8(uint4 u, float* f, bool half) {
 __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
     __shared__ float red[2][512];
     const int G = a.C >> 3, g = threadIdx.x % G;
-    for (int i = threadIdx.x; i < 2 * a.C; i += 256) red[i / a.C][i % a.C] = 0.f;
     const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
     float wr[8][9];
 #pragma unroll
@@ -545,14 +573,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
             ls[r] += __shfl_xor(ls[r], o, 64);
             lq[r] += __shfl_xor(lq[r], o, 64);
         }
-    __syncthreads();
-    if ((threadIdx.x & 63) < G)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            atomicAdd(&red[0][c0 + r], ls[r]);
-            atomicAdd(&red[1][c0 + r], lq[r]);
-        }
-    __syncthreads();
+    ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < a.C; c += 256) {
         st_sum[int64_t(blockIdx.x) * a.C + c] = red[0][c];
         st_sq[int64_t(blockIdx.x) * a.C + c] = red[1][c];
@@ -560,11 +581,10 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
 }
 
 // dx (mapped channels, overwrite or accumulate into the view) and dW (+=) from dense dz (N,H,W,C)
-__global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* __restrict__ dz, float* __restrict__ dw,
+__global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* __restrict__ dz, float* __restrict__ part,
                                                         int accumulate) {
     __shared__ float red[512 * 9];
     const int G = a.C >> 3, g = threadIdx.x % G;
-    for (int i = threadIdx.x; i < 9 * a.C; i += 256) red[i] = 0.f;
     const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
     float wr[8][9], acc[8][9];
 #pragma unroll
@@ -617,14 +637,8 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
-    __syncthreads();
-    if ((threadIdx.x & 63) < G)
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-#pragma unroll
-            for (int t = 0; t < 9; ++t) atomicAdd(&red[(c0 + r) * 9 + t], acc[r][t]);
-    __syncthreads();
-    for (int i = threadIdx.x; i < 9 * a.C; i += 256) atomicAdd(&dw[i], red[i]);
+    ordered_wave_add72(red, acc, g, G);
+    for (int i = threadIdx.x; i < 9 * a.C; i += 256) part[int64_t(blockIdx.x) * 9 * a.C + i] = red[i];
 }
 
 // ------------------------------------------------------------------ weight preparation
@@ -751,6 +765,27 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, 2048);
 }
 
+extern "C" int ym_conv_set_halo(int mode) {
+    // selection policy of the halo-staged 3x3 kernel: -1 env/default, 0 never, 1 wherever it applies,
+    // 2 where it measured faster (the default); returns the previous setting
+    const int prev = g_halo_force;
+    g_halo_force = mode < -1 || mode > 2 ? -1 : mode;
+    return prev;
+}
+
+extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
+    // 1: halo-staged 3x3 kernel (conv_halo.hip), 0: implicit GEMM
+    return d && halo_plan(d, dgrad ? 1 : 0).ok ? 1 : 0;
+}
+
+extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
+    // rows of the BN statistics partials ym_conv_fwd writes for this conv (halo or implicit-GEMM grid)
+    if (!d) return 0;
+    const HaloPlan hp = halo_plan(d, 0);
+    if (hp.ok) return hp.gx;
+    return ym_conv_stat_blocks(int64_t(d->n) * d->oh * d->ow, d->cout);
+}
+
 extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                            float* stat_sum, float* stat_sq, void* stream) {
     YM_CHECK_ARG(d && x && w && y, "ym_conv_fwd: null argument");
@@ -774,6 +809,12 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
+    const HaloPlan hp = halo_plan(d, 0);
+    if (hp.ok) {
+        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
+        return YM_OK;
+    }
     pick_and_launch(a, MODE_FWD, 2048, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
@@ -803,6 +844,12 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->y_bs, int64_t(d->h / d->stride) * (d->w / d->stride)),
                  "ym_conv_dgrad: gradient image stride too large");
+    const HaloPlan hp = halo_plan(d, 1);
+    if (hp.ok) {
+        halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_dgrad (halo)");
+        return YM_OK;
+    }
     pick_and_launch(a, MODE_DGRAD, 4096, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_dgrad");
     return YM_OK;
@@ -820,14 +867,23 @@ extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t
     return YM_OK;
 }
 
+extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
+    return size_t(PARTIAL_BLOCKS) * size_t(cout > 0 ? cout : 0) * 9 * sizeof(float);
+}
+
 extern "C" int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh,
-                                   int ow, int cout, int stride, int pad, void* stream) {
-    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_wgrad: cout=%d unsupported",
+                                   int ow, int cout, int stride, int pad, float* workspace, size_t workspace_bytes,
+                                   void* stream) {
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= 128 && 64 % (cout / 8) == 0, "ym_conv_first_wgrad: cout=%d unsupported",
                  cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_wgrad: too many pixels");
-    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(1024), dim3(256), 0, as_stream(stream), dz, img, dw_oihw, n, h,
-                       w, oh, ow, cout, stride, pad);
+    YM_CHECK_ARG(workspace && workspace_bytes >= ym_conv_first_wgrad_workspace_size(cout),
+                 "ym_conv_first_wgrad: workspace too small");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dz, img, workspace, n, h, w, oh,
+                       ow, cout, stride, pad);
+    colsum_launch(workspace, PARTIAL_BLOCKS, cout * 9, int64_t(cout) * 9, dw_oihw, 1, st);
     YM_LAUNCH_CHECK("ym_conv_first_wgrad");
     return YM_OK;
 }
@@ -849,14 +905,22 @@ extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
     return YM_OK;
 }
 
+extern "C" size_t ym_dw3x3_bwd_workspace_size(int c) {
+    return size_t(PARTIAL_BLOCKS) * size_t(c > 0 ? c : 0) * 9 * sizeof(float);
+}
+
 extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
                             const float* w, const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw,
-                            int n, int h, int wd, int c, int accumulate, void* stream) {
+                            int n, int h, int wd, int c, int accumulate, float* workspace, size_t workspace_bytes,
+                            void* stream) {
     YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && dx_bs % 8 == 0 && dx_ld % 8 == 0 &&
                      int64_t(n) * h * wd < (int64_t(1) << 31),
                  "ym_dw3x3_bwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+    YM_CHECK_ARG(workspace && workspace_bytes >= ym_dw3x3_bwd_workspace_size(c), "ym_dw3x3_bwd: workspace too small");
     DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, dx, dx_bs, dx_ld, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(512), dim3(256), 0, as_stream(stream), a, dz, dw, accumulate);
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, a, dz, workspace, accumulate);
+    colsum_launch(workspace, PARTIAL_BLOCKS, c * 9, int64_t(c) * 9, dw, 1, st);
     YM_LAUNCH_CHECK("ym_dw3x3_bwd");
     return YM_OK;
 }

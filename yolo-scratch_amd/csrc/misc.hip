@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "reduce.h"
 
 namespace ym {
 namespace {
@@ -239,42 +240,63 @@ __global__ void view_axpy_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int
 
 // ------------------------------------------------------------------ Detect head gradient split
 // dhead (B, A, 64+nc) fp32 rows for one level (anchor offset `aoff`, HW anchors per image) ->
-// dz_box bf16 [M][64], dz_cls bf16 [M][8] (nc <= 8, zero padded), bias grads (+=, atomics)
-__global__ void head_grad_kernel(const float* __restrict__ dh, int64_t A, int64_t aoff, int HW, int64_t M, int nc,
-                                 bf16_t* __restrict__ dbox, bf16_t* __restrict__ dcls, float* __restrict__ dbias_box,
-                                 float* __restrict__ dbias_cls) {
-    __shared__ float red[72];
+// dz_box bf16 [M][64], dz_cls bf16 [M][8] (nc <= 8, zero padded), and per-block bias-gradient
+// partials part[blockIdx.x][72] (summed in a fixed order by colsum_kernel; no atomics).
+// Thread t < 252 owns 8-channel group g = t % 9 of pixel slot t / 9 (28 pixels per block pass).
+__global__ void __launch_bounds__(256) head_grad_kernel(const float* __restrict__ dh, int64_t A, int64_t aoff, int HW,
+                                                        int64_t M, int nc, bf16_t* __restrict__ dbox,
+                                                        bf16_t* __restrict__ dcls, float* __restrict__ part) {
+    __shared__ float red[252][9];            // [thread][8 sums] (+1 pad)
+    const int t = threadIdx.x, g = t % 9, slot = t / 9;
     const int no = 64 + nc;
-    for (int i = threadIdx.x; i < 72; i += blockDim.x) red[i] = 0.f;
-    __syncthreads();
-    // thread -> (pixel, 8-channel group); 9 groups: 8 box + 1 cls
-    const int64_t total = M * 9;
-    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += int64_t(gridDim.x) * blockDim.x) {
-        int g = int(i % 9);
-        int64_t m = i / 9;
-        int64_t n = m / HW, pix = m - n * HW;
-        const float* row = dh + (n * A + aoff + pix) * no;
-        float v[8];
-        if (g < 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (t < 252) {
+        for (int64_t m = int64_t(blockIdx.x) * 28 + slot; m < M; m += int64_t(gridDim.x) * 28) {
+            const int64_t n = m / HW, pix = m - n * HW;
+            const float* row = dh + (n * A + aoff + pix) * no;
+            float v[8];
+            if (g < 8) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = row[g * 8 + k];
-            *reinterpret_cast<uint4*>(dbox + m * 64 + g * 8) = pack8(v);
-        } else {
+                for (int k = 0; k < 8; ++k) v[k] = row[g * 8 + k];     // rows of 64+nc floats: 4-B aligned
+                *reinterpret_cast<uint4*>(dbox + m * 64 + g * 8) = pack8(v);
+            } else {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = k < nc ? row[64 + k] : 0.f;
-            *reinterpret_cast<uint4*>(dcls + m * 8) = pack8(v);
+                for (int k = 0; k < 8; ++k) v[k] = k < nc ? row[64 + k] : 0.f;
+                *reinterpret_cast<uint4*>(dcls + m * 8) = pack8(v);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += v[k];
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(&red[g * 8 + k], v[k]);
+        for (int k = 0; k < 8; ++k) red[t][k] = acc[k];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 64 + nc; i += blockDim.x) {
-        if (i < 64) atomicAdd(&dbias_box[i], red[i]);
-        else atomicAdd(&dbias_cls[i - 64], red[i]);
+    if (t < 72) {                            // column t = g * 8 + k: sum the 28 slots in order
+        const int gg = t >> 3, k = t & 7;
+        float s = 0.f;
+        for (int sl = 0; sl < 28; ++sl) s += red[sl * 9 + gg][k];
+        part[int64_t(blockIdx.x) * 72 + t] = s;
     }
 }
 
+// out[j] (+)= sum_r part[r * ld + j] in row order (deterministic; fp32)
+__global__ void colsum_kernel(const float* __restrict__ part, int rows, int n, int64_t ld, float* __restrict__ out,
+                              int accumulate) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += part[int64_t(r) * ld + j];
+    out[j] = accumulate ? out[j] + s : s;
+}
+
 }  // namespace
+
+int colsum_launch(const float* part, int rows, int n, int64_t ld, float* out, int accumulate, hipStream_t st) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(colsum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, rows, n, ld, out, accumulate);
+    return 0;
+}
+
 }  // namespace ym
 
 using namespace ym;
@@ -355,11 +377,18 @@ extern "C" int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t l
     return YM_OK;
 }
 
+extern "C" size_t ym_head_grad_workspace_size(void) { return size_t(PARTIAL_BLOCKS) * 72 * sizeof(float); }
+
 extern "C" int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc,
-                            uint16_t* dz_box, uint16_t* dz_cls, float* dbias_box, float* dbias_cls, void* stream) {
+                            uint16_t* dz_box, uint16_t* dz_cls, float* dbias_box, float* dbias_cls, float* workspace,
+                            size_t workspace_bytes, void* stream) {
     YM_CHECK_ARG(nc >= 1 && nc <= 8, "ym_head_grad: nc must be in [1, 8]");
-    hipLaunchKernelGGL(head_grad_kernel, dim3(grid_for(m * 9, 256, 2048)), dim3(256), 0, as_stream(stream), dhead,
-                       a_total, a_off, hw, m, nc, dz_box, dz_cls, dbias_box, dbias_cls);
+    YM_CHECK_ARG(workspace && workspace_bytes >= ym_head_grad_workspace_size(), "ym_head_grad: workspace too small");
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(head_grad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dhead, a_total, a_off, hw, m, nc,
+                       dz_box, dz_cls, workspace);
+    if (dbias_box) colsum_launch(workspace, PARTIAL_BLOCKS, 64, 72, dbias_box, 1, st);
+    if (dbias_cls) colsum_launch(workspace + 64, PARTIAL_BLOCKS, nc, 72, dbias_cls, 1, st);
     YM_LAUNCH_CHECK("ym_head_grad");
     return YM_OK;
 }

@@ -43,14 +43,19 @@ SIGNATURES = {
     "ym_decode_nms": (R, [P, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
     "ym_nms": (R, [P, P, I64, F32, P, SZ, P, P, P]),
     "ym_conv_stat_blocks": (R, [I64, INT]),
+    "ym_conv_fwd_stat_rows": (R, [P]),
+    "ym_conv_algo": (R, [P, INT]),
+    "ym_conv_set_halo": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
+    "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
-    "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P]),
+    "ym_dw3x3_bwd_workspace_size": (SZ, [INT]),
+    "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
     "ym_bn_workspace_size": (SZ, [INT]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
@@ -67,7 +72,8 @@ SIGNATURES = {
     "ym_view_to_f32": (R, [P, I64, I64, P, I64, INT, INT, P]),
     "ym_f32_to_view": (R, [P, P, I64, I64, I64, INT, INT, INT, P]),
     "ym_view_axpy": (R, [P, I64, I64, P, I64, I64, I64, INT, INT, INT, INT, P]),
-    "ym_head_grad": (R, [P, I64, I64, INT, I64, INT, P, P, P, P, P]),
+    "ym_head_grad_workspace_size": (SZ, []),
+    "ym_head_grad": (R, [P, I64, I64, INT, I64, INT, P, P, P, P, P, SZ, P]),
     "ym_attn_fwd": (R, [P, I64, I64, INT, INT, INT, INT, INT, F32, P, I64, I64, P, P]),
     "ym_attn_workspace_size": (SZ, [INT, INT, INT]),
     "ym_attn_bwd": (R, [P, I64, I64, P, I64, I64, P, I64, I64, P, INT, INT, INT, F32, P, P, I64, I64, INT, INT, INT,

@@ -135,7 +135,7 @@ class GradSync:
         """Hook the plan's backward so the NEXT backward launches buckets as it goes."""
         self.plan = plan
         self.buckets = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
-        self.buckets.side_stream = lambda _p=plan: _p.side_stream
+        self.buckets.side_stream = lambda _p=plan: getattr(_p, "side_stream", None)
 
         def hook(params, _b=self.buckets):
             if not _b.remaining:

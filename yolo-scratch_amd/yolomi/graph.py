@@ -177,16 +177,16 @@ class ConvBN:
         self.M, self.HW = B * oh * ow, oh * ow
         self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
         self.wf, self.wt = plan.weights.add(w, need_t=x.act is not None)
-        self.G = lib().ym_conv_stat_blocks(self.M, co)
-        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
-        self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)      # scale, shift, mean, rstd
-        self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
         d = ConvDesc()
         d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout = B, x.H, x.W, ci, oh, ow, co
         d.k, d.stride, d.pad = k, s, k // 2
         d.x_bs, d.x_ld, d.y_bs, d.y_ld = x.bs, x.ld, self.HW * co, co
         d.out_f32 = 2                                                   # fp16 pre-BN z
         self.desc = d
+        self.G = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
+        self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)      # scale, shift, mean, rstd
+        self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
         plan.need_wgrad_ws(d)
 
     def flops(self):
@@ -295,8 +295,9 @@ class StemConvBN(ConvBN):
              _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
         call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
              1, self.coef.data_ptr(), self.z.data_ptr(), st)
+        ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
         call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight), plan.B,
-             self.H, self.W, self.oh, self.ow, self.co, self.s, 1, st)
+             self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
 
 
 class DWConvBN(ConvBN):
@@ -355,9 +356,10 @@ class DWConvBN(ConvBN):
             vch[self.x.c0 + h * hs + goff: self.x.c0 + h * hs + goff + hd] = True
         acc = int(self.x.act.written[vch].all())
         gsz, gstr, goff = self.map
+        ws = plan.private_ws(self, lib().ym_dw3x3_bwd_workspace_size(self.C))
         call("ym_dw3x3_bwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
              self.z.data_ptr(), self.x.gptr(), self.x.bs, self.x.ld, plan.gptr(self.m.conv.weight), plan.B, self.y.H,
-             self.y.W, self.C, acc, st)
+             self.y.W, self.C, acc, ws.data_ptr(), ws.numel() * 4, st)
         self.x.act.written[vch] = True
 
 
@@ -507,8 +509,10 @@ class HeadLevel:
 
     def backward(self, plan, st):
         B, A, no = self.head.shape
+        ws = plan.private_ws(self, lib().ym_head_grad_workspace_size())
         call("ym_head_grad", plan.dhead.data_ptr(), A, self.a_off, self.HW, self.M, self.nc, self.dzb.data_ptr(),
-             self.dzc.data_ptr(), plan.gptr(self.box.bias), plan.gptr(self.cls.bias), st)
+             self.dzc.data_ptr(), plan.gptr(self.box.bias), plan.gptr(self.cls.bias), ws.data_ptr(), ws.numel() * 4,
+             st)
         ws = plan.wgrad_ws()
         sst = plan.side(st)
         call("ym_conv_wgrad", ctypes.byref(self.bb), self.dzb.data_ptr(), self.xb.ptr(), ws.data_ptr(), ws.numel() * 4,
@@ -589,6 +593,13 @@ class Plan:
 
     def act(self, C, H, W, name=""):
         return View(Act(self, C, H, W, name=name))
+
+    def private_ws(self, op, nbytes):
+        """An op's own fp32 scratch (partial rows of its fixed-order reductions), allocated once."""
+        ws = op.__dict__.get("_ws")
+        if ws is None or ws.numel() * 4 < nbytes:
+            ws = op.__dict__["_ws"] = torch.empty(max((nbytes + 3) // 4, 1), dtype=F32, device=self.dev)
+        return ws
 
     def need_wgrad_ws(self, desc):
         """Size the shared split-K workspace of ym_conv_wgrad (ops run in order on one stream)."""
