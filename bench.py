@@ -174,6 +174,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     plan.probe = None
+    # host time to enqueue one step (Python + ctypes launches) vs its wall time: a step whose
+    # enqueue time approaches its wall time leaves the GPU waiting on the host
+    host = []
+    for i in range(3):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        step(args.warmup + args.steps + i)
+        host.append(time.perf_counter() - h0)
+    torch.cuda.synchronize()
+    host_ms = 1e3 * sorted(host)[1]
     lens = [a.elapsed_time(b) for a, b in plan.probe_events]       # ms
     kern_ms = sum(lens) / max(len(lens), 1)
 
@@ -231,6 +241,7 @@ def main():
                           "unit": "TFLOP/s", "frac": round(step_tf / PEAK_BF16_TFLOPS, 4),
                           "train_gflop_per_img": round(per_img / 1e9, 2)},
         "probe": {"key": probe_key, "rank": probe_rank, "count": probe_count},
+        "host_enqueue_ms_per_step": round(host_ms, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
@@ -238,8 +249,8 @@ def main():
         except Exception as e:  # pragma: no cover
             out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
     if rank == 0:
-        log(f"loss {float(loss):.4f}  {value:.1f} img/s  {ms_step:.1f} ms/step  dominant kernel {kern_ms:.3f} ms "
-            f"({dom_tf:.0f} TFLOP/s)")
+        log(f"loss {float(loss):.4f}  {value:.1f} img/s  {ms_step:.1f} ms/step (host enqueue {host_ms:.1f} ms)  "
+            f"dominant kernel {kern_ms:.3f} ms ({dom_tf:.0f} TFLOP/s)")
         print(json.dumps(out), flush=True)
     ydist.shutdown()
 

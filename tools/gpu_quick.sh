@@ -12,7 +12,7 @@ rc=$?
 echo "pytest_gpu exit $rc"; tail -3 $OUT/pytest_gpu.log
 if [ $rc -ne 0 ]; then tail -40 $OUT/pytest_gpu.log; exit $rc; fi
 timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed $?"; tail -20 $OUT/bench.err; exit 1; }
-python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); print('bench', d['value'], d['ms_per_step'])"
+python3 -c "import json,sys; d=json.load(open('$OUT/bench.json')); print('bench', d['value'], d['ms_per_step'], d.get('host_enqueue_ms_per_step'))"
 for kv in "$@"; do
   env $kv timeout -k 10 300 python3 $R/bench.py --no-cpu-baseline > $OUT/bench_$kv.json 2> $OUT/bench_$kv.err || { echo "bench $kv failed $?"; tail -20 $OUT/bench_$kv.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open('$OUT/bench_$kv.json')); print('bench $kv', d['value'], d['ms_per_step'])"

@@ -279,21 +279,38 @@ __global__ void __launch_bounds__(256) head_grad_kernel(const float* __restrict_
     }
 }
 
-// out[j] (+)= sum_r part[r * ld + j] in row order (deterministic; fp32)
-__global__ void colsum_kernel(const float* __restrict__ part, int rows, int n, int64_t ld, float* __restrict__ out,
-                              int accumulate) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
+// out[j] (+)= sum_r part[r * ld + j] (deterministic; fp32): a block takes 64 columns, its 4 waves
+// the rows r = wave (mod 4) with 16 loads in flight per lane, then the 4 wave sums in wave order
+__global__ void __launch_bounds__(256) colsum_kernel(const float* __restrict__ part, int rows, int n, int64_t ld,
+                                                     float* __restrict__ out, int accumulate) {
+    __shared__ float red[4][64];
+    const int c = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
     float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += part[int64_t(r) * ld + j];
-    out[j] = accumulate ? out[j] + s : s;
+    if (j < n) {
+        int r = w;
+        for (; r + 4 * 15 < rows; r += 4 * 16) {
+            float v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = part[int64_t(r + 4 * u) * ld + j];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) s += v[u];
+        }
+        for (; r < rows; r += 4) s += part[int64_t(r) * ld + j];
+    }
+    red[w][c] = s;
+    __syncthreads();
+    if (w == 0 && j < n) {
+        const float t = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+        out[j] = accumulate ? out[j] + t : t;
+    }
 }
 
 }  // namespace
 
 int colsum_launch(const float* part, int rows, int n, int64_t ld, float* out, int accumulate, hipStream_t st) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(colsum_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, rows, n, ld, out, accumulate);
+    hipLaunchKernelGGL(colsum_kernel, dim3((n + 63) / 64), dim3(256), 0, st, part, rows, n, ld, out, accumulate);
     return 0;
 }
 

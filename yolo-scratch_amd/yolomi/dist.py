@@ -76,7 +76,7 @@ class Buckets:
             self._close(start, size, cur)
         self.handles = []
         self.remaining = []
-        self.side_stream = None    # callable -> the producing plan's side stream (or None)
+        self.streams = None        # callable -> the producing plan's streams (yolomi.graph.Plan.comm_streams)
 
     def _close(self, start, size, members):
         b = len(self.ranges)
@@ -101,15 +101,17 @@ class Buckets:
 
     def _launch(self, b):
         s, e = self.ranges[b]
-        side = self.side_stream() if self.side_stream else None
-        if side is None:
+        streams = self.streams() if self.streams else []
+        if len(streams) <= 1:
             self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
         else:
-            # the bucket's gradients come from both streams (BN on the main one, weight gradients on
-            # the plan's side stream): the collective is issued from the side stream after it has
-            # caught up with the main stream, so RCCL orders it after both
-            side.wait_stream(torch.cuda.current_stream(side.device))
-            with torch.cuda.stream(side):
+            # the bucket's gradients come from several streams (BN backward on the scheduler's
+            # streams, weight gradients on the side stream): the collective is issued from the last
+            # of them after it has caught up with the others, so RCCL orders it after all writers
+            comm = streams[-1]
+            for o in streams[:-1]:
+                comm.wait_stream(o)
+            with torch.cuda.stream(comm):
                 self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
         self.launched[b] = True
 
@@ -135,7 +137,7 @@ class GradSync:
         """Hook the plan's backward so the NEXT backward launches buckets as it goes."""
         self.plan = plan
         self.buckets = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
-        self.buckets.side_stream = lambda _p=plan: getattr(_p, "side_stream", None)
+        self.buckets.streams = getattr(plan, "comm_streams", None)
 
         def hook(params, _b=self.buckets):
             if not _b.remaining:

@@ -162,6 +162,23 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+# buffer-range keys for the stream scheduler: ('a' activation | 'g' gradient, Act id, c0, c1)
+def _ka(v):
+    return ("a", id(v.act), v.c0, v.c0 + v.c)
+
+
+def _kg(v):
+    return ("g", id(v.act), v.c0, v.c0 + v.c)
+
+
+def _overlap(k1, k2):
+    if k1[0] != k2[0] or k1[1] != k2[1]:
+        return False
+    if len(k1) == 2:
+        return True
+    return k1[2] < k2[3] and k2[2] < k1[3]
+
+
 class ConvBN:
     """Conv2d (k in {1,3}, groups=1) -> BatchNorm2d -> SiLU|Identity (+ residual) — reference Conv :21-33."""
 
@@ -192,18 +209,25 @@ class ConvBN:
     def flops(self):
         return 2 * self.M * self.co * self.ci * self.k * self.k
 
+    def rw(self, plan, phase):
+        """(reads, writes) buffer ranges of this op's forward / backward (stream scheduler)."""
+        if phase == "fwd":
+            return [_ka(self.x)] + ([_ka(self.res)] if self.res else []), [_ka(self.y)]
+        w = [_kg(self.y)] + ([_kg(self.x)] if plan.needs_grad(self.x) else []) + ([_kg(self.res)] if self.res else [])
+        return [_ka(self.x), _kg(self.y)], w
+
     def forward(self, plan, st):
         bn = self.m.bn
         ss, sq = self.ps[0], self.ps[1]
         probe = plan.probe is self
         if probe:
             ev0 = torch.cuda.Event(enable_timing=True)
-            ev0.record()
+            ev0.record(plan._cur_stream)
         call("ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
              ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st)
         if probe:
             ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record()
+            ev1.record(plan._cur_stream)
             plan.probe_events.append((ev0, ev1))
         sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
         if plan.training:
@@ -250,6 +274,9 @@ class ConvBN:
 
 class StemConvBN(ConvBN):
     """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
+
+    def rw(self, plan, phase):
+        return ([], [_ka(self.y)]) if phase == "fwd" else ([_kg(self.y)], [_kg(self.y)])
 
     def __init__(self, plan, m, img_shape, y: View, s):
         w = m.conv.weight
@@ -302,6 +329,11 @@ class StemConvBN(ConvBN):
 
 class DWConvBN(ConvBN):
     """Attention.pe: depthwise 3x3 + BN (no act) on v, + the attention output as residual (:122, :134)."""
+
+    def rw(self, plan, phase):
+        if phase == "fwd":
+            return [_ka(self.x), _ka(self.res)], [_ka(self.y)]
+        return [_ka(self.x), _kg(self.y)], [_kg(self.y), _kg(self.res), _kg(self.x)]
 
     def __init__(self, plan, m, qkv: View, heads, kd, hd, y: View, res: View):
         self.m, self.x, self.y, self.res, self.act = m, qkv, y, res, 0
@@ -366,6 +398,11 @@ class DWConvBN(ConvBN):
 class AttnCore:
     """softmax(q^T k * kd^-0.5) and v @ attn^T per head (Attention.forward :124-134)."""
 
+    def rw(self, plan, phase):
+        if phase == "fwd":
+            return [_ka(self.qkv)], [_ka(self.out)]
+        return [_ka(self.qkv), _ka(self.out), _kg(self.out)], [_kg(self.out), _kg(self.qkv)]
+
     def __init__(self, plan, qkv: View, heads, kd, hd, out: View):
         self.qkv, self.out, self.heads, self.kd, self.hd = qkv, out, heads, kd, hd
         self.N = qkv.H * qkv.W
@@ -401,6 +438,12 @@ class SPPFPools:
     first-maximum routing of the backward sees the same ties as the fp32 reference
     (chained pools copy values, so exact ties are structural); the bf16 copies go to
     the concat slices for cv2."""
+
+    def rw(self, plan, phase):
+        sl = self.slices
+        if phase == "fwd":
+            return [_ka(sl[0])], [_ka(v) for v in sl[1:]]
+        return [_kg(v) for v in sl[1:]], [_kg(v) for v in sl]
 
     def __init__(self, plan, cv1_op, slices):
         self.slices = slices                      # [s0 (cv1 out), s1, s2, s3]
@@ -439,6 +482,11 @@ class SPPFPools:
 class Upsample2:
     """nn.Upsample(scale_factor=2, mode='nearest') (yaml head rows 11, 14)."""
 
+    def rw(self, plan, phase):
+        if phase == "fwd":
+            return [_ka(self.x)], [_ka(self.y)]
+        return [_kg(self.y)], [_kg(self.y), _kg(self.x)]
+
     def __init__(self, plan, x: View, y: View):
         self.x, self.y = x, y
 
@@ -456,6 +504,11 @@ class Upsample2:
 
 class Copy:
     """Channel-slice copy for the two concatenations whose halves live in different buffers (PSA / C2PSA)."""
+
+    def rw(self, plan, phase):
+        if phase == "fwd":
+            return [_ka(self.x)], [_ka(self.y)]
+        return [_kg(self.y)], [_kg(self.y), _kg(self.x)]
 
     def __init__(self, plan, x: View, y: View):
         self.x, self.y = x, y
@@ -475,6 +528,11 @@ class Copy:
 class HeadLevel:
     """Detect level i: the two bias 1x1 convs (cv2[i][2] -> 64 box logits, cv3[i][2] -> nc cls logits)
     writing fp32 rows of the (B, A, 64+nc) head buffer (Detect.forward :237-246)."""
+
+    def rw(self, plan, phase):
+        if phase == "fwd":
+            return [_ka(self.xb), _ka(self.xc)], [("head", self.a_off)]
+        return [_ka(self.xb), _ka(self.xc), ("dhead", self.a_off)], [_kg(self.xb), _kg(self.xc)]
 
     def __init__(self, plan, box_conv, cls_conv, xb: View, xc: View, head, a_off):
         self.box, self.cls, self.xb, self.xc, self.head, self.a_off = box_conv, cls_conv, xb, xc, head, a_off
@@ -520,7 +578,7 @@ class HeadLevel:
         call("ym_conv_wgrad", ctypes.byref(self.bc), self.dzc.data_ptr(), self.xc.ptr(), ws.data_ptr(), ws.numel() * 4,
              self.wsc.data_ptr(), 0, sst)
         g = plan.grad_view(self.cls.weight).view(self.nc, -1)
-        with torch.cuda.stream(plan.side_stream or torch.cuda.current_stream(plan.dev)):
+        with torch.cuda.stream(plan.side_stream or plan._cur_stream or torch.cuda.current_stream(plan.dev)):
             g.copy_(self.wsc[: self.nc])
         for d, dz, wt, x in ((self.bb, self.dzb, self.wb_t, self.xb), (self.bc, self.dzc, self.wc_t, self.xc)):
             acc = x.grad_for_write(st)
@@ -548,7 +606,8 @@ class Plan:
         self.acts, self.ops = [], []
         self.weights = WeightStore(self)
         self.probe, self.probe_events = None, []   # bench: time one op's conv launch
-        self.bn_ws = torch.empty(lib().ym_bn_workspace_size(2048) // 4, dtype=F32, device=dev)
+        self._bn_ws = []           # one BN-reduction workspace per scheduler stream (see bn_ws)
+        self._cur = 0              # scheduler stream the current op runs on
         self.input = None          # View for block plans
         self.img = None            # fp32 image for the full model
         self.head = None           # (B, A, 64+nc) fp32 for the full model
@@ -556,6 +615,7 @@ class Plan:
         self._scratch = []
         self.grad_hook = None      # called with each op's finished parameters during backward (DP buckets)
         self.side_stream = None    # weight-gradient stream (see side())
+        self._cur_stream = None    # torch stream the current op is issued on (scheduler)
         # flat parameter-gradient buffer; each .grad is a view of it
         params = [p for p in root.parameters() if p.requires_grad]
         self.params = params
@@ -577,7 +637,7 @@ class Plan:
         s = self.side_stream
         if s is None:
             return st
-        s.wait_stream(torch.cuda.current_stream(self.dev))
+        s.wait_stream(self._cur_stream or torch.cuda.current_stream(self.dev))
         return s.cuda_stream
 
     def _begin_side(self):
@@ -605,11 +665,22 @@ class Plan:
         """Size the shared split-K workspace of ym_conv_wgrad (ops run in order on one stream)."""
         self._wg_bytes = max(getattr(self, "_wg_bytes", 0), int(lib().ym_conv_wgrad_workspace_size(ctypes.byref(desc))))
 
+    @property
+    def bn_ws(self):
+        """BatchNorm reduction scratch of the stream the current op runs on (ops on different
+        streams run concurrently, so each stream has its own)."""
+        while len(self._bn_ws) <= self._cur:
+            self._bn_ws.append(torch.empty(lib().ym_bn_workspace_size(2048) // 4, dtype=F32, device=self.dev))
+        return self._bn_ws[self._cur]
+
     def wgrad_ws(self):
-        ws = getattr(self, "_wg_ws", None)
-        if ws is None:
-            ws = self._wg_ws = torch.empty(max(self._wg_bytes // 4, 1), dtype=F32, device=self.dev)
-        return ws
+        """Split-K scratch of ym_conv_wgrad: one for the side stream (wgrads run there in order), or
+        one per scheduler stream when they run in line."""
+        key = -1 if self.side_stream is not None else self._cur
+        wss = self.__dict__.setdefault("_wg_ws", {})
+        if key not in wss:
+            wss[key] = torch.empty(max(self._wg_bytes // 4, 1), dtype=F32, device=self.dev)
+        return wss[key]
 
     def grad_view(self, p):
         return self.grad_views[id(p)]
@@ -622,15 +693,125 @@ class Plan:
     def needs_grad(self, v: View):
         return v.act is not None and (v.act is not getattr(self.input, "act", None) or self.input_requires_grad)
 
+    # --------------------------------------------------------------- stream scheduler
+    # The op list is a DAG over buffer ranges (each op declares what it reads and writes, `rw`):
+    # independent branches — the six Detect-head chains, C3k's two 1x1 branches, the concat
+    # producers of C2f — run on different HIP streams, so the small 20x20 / 40x40 layers and the
+    # latency-bound BatchNorm reductions of one chain overlap another chain's kernels.  The
+    # schedule (stream per op + the events it waits for) is computed once per plan and phase:
+    # an op follows the stream of its latest dependency while that stream's tail is that
+    # dependency, otherwise it takes a stream whose tail it depends on, or the least recently used
+    # one.  YM_STREAMS sets the stream count (1 = everything in order on the caller's stream).
+    def _nstreams(self):
+        return max(1, int(os.environ.get("YM_STREAMS", "3"))) if self.dev.type == "cuda" else 1
+
+    def _schedule(self, ops, phase, K):
+        key = (phase, K, len(ops))
+        cache = self.__dict__.setdefault("_sched", {})
+        if key in cache:
+            return cache[key]
+        rws = [op.rw(self, phase) for op in ops]
+        writes, reads, deps = [], [], []
+        for i, (R, W) in enumerate(rws):
+            d = set()
+            for k in R:
+                d.update(j for k2, j in writes if _overlap(k, k2))
+            for k in W:
+                d.update(j for k2, j in writes if _overlap(k, k2))
+                d.update(j for k2, j in reads if _overlap(k, k2))
+            deps.append(d)
+            writes.extend((k, i) for k in W)
+            reads.extend((k, i) for k in R)
+        stream_of, tail, plan = [0] * len(ops), [-1] * K, []
+        need_ev = set()
+        for i, d in enumerate(deps):
+            s = 0
+            if d:
+                j = max(d)
+                s = stream_of[j]
+                if tail[s] != j:
+                    cands = [t for t in range(K) if tail[t] in d]
+                    s = max(cands, key=lambda t: tail[t]) if cands else min(range(K), key=lambda t: tail[t])
+            elif i > 0:
+                s = min(range(K), key=lambda t: tail[t])
+            waits = {}
+            for j in d:
+                if stream_of[j] != s:
+                    waits[stream_of[j]] = max(waits.get(stream_of[j], -1), j)
+            stream_of[i] = s
+            tail[s] = i
+            need_ev.update(waits.values())
+            plan.append((s, sorted(waits.values())))
+        cache[key] = (plan, need_ev)
+        return cache[key]
+
+    def _streams(self, K):
+        ss = self.__dict__.setdefault("_dag_streams", [])
+        while len(ss) < K - 1:
+            ss.append(torch.cuda.Stream(device=self.dev))
+        return [torch.cuda.current_stream(self.dev)] + ss[:K - 1]
+
+    def comm_streams(self):
+        """Every stream a backward writes gradients from (the DP buckets join them before a collective)."""
+        out = list(self.__dict__.get("_active_streams", []))
+        if self.side_stream is not None:
+            out.append(self.side_stream)
+        return out
+
+    def _run(self, ops, phase, after=None):
+        K = self._nstreams()
+        if K == 1:
+            st = stream_ptr(self.dev)
+            self._cur = 0
+            self._active_streams = [torch.cuda.current_stream(self.dev)]
+            self._cur_stream = self._active_streams[0]
+            for op in ops:
+                getattr(op, phase == "fwd" and "forward" or "backward")(self, st)
+                if after is not None:
+                    after(op)
+            return
+        sched, need_ev = self._schedule(ops, phase, K)
+        streams = self._streams(K)
+        self._active_streams = streams
+        evs = self.__dict__.setdefault("_events", {}).setdefault(phase, {})
+        main = streams[0]
+        for s in streams[1:]:
+            s.wait_stream(main)
+        ptrs = [s.cuda_stream for s in streams]
+        fwd = phase == "fwd"
+        # ops launch on explicit stream handles (no torch stream context per op: it is host time the
+        # GPU waits for); the few torch-side launches (side-stream joins, probe events) use _cur_stream
+        for i, op in enumerate(ops):
+            k, waits = sched[i]
+            s = streams[k]
+            for j in waits:
+                s.wait_event(evs[j])
+            self._cur, self._cur_stream = k, s
+            if fwd:
+                op.forward(self, ptrs[k])
+            else:
+                op.backward(self, ptrs[k])
+            if after is not None:
+                after(op)
+            if i in need_ev:
+                ev = evs.get(i)
+                if ev is None:
+                    ev = evs[i] = torch.cuda.Event()
+                ev.record(s)
+        for s in streams[1:]:
+            main.wait_stream(s)
+        self._cur, self._cur_stream = 0, None
+
     # --------------------------------------------------------------- run
     def forward(self):
         st = stream_ptr(self.dev)
         self.weights.refresh(st)
-        for op in self.ops:
-            op.forward(self, st)
+        self._run(self.ops, "fwd")
 
     def backward(self):
-        st = stream_ptr(self.dev)
+        self._backward_ops(self.ops)
+
+    def _backward_ops(self, ops):
         for a in self.acts:
             a.written[:] = False
         self.grad_flat.zero_()
@@ -638,10 +819,7 @@ class Plan:
             t.zero_()
         hook = self.grad_hook
         self._begin_side()
-        for op in reversed(self.ops):
-            op.backward(self, st)
-            if hook is not None:
-                hook(op_params(op))
+        self._run(list(reversed(ops)), "bwd", (lambda op: hook(op_params(op))) if hook is not None else None)
         self._join_side()
 
     def install_grads(self):
@@ -913,16 +1091,14 @@ def run_block(module, x: torch.Tensor):
             plan.output = lower_block(plan, module, plan.input)
 
         def backward_from_output():
-            st = stream_ptr(plan.dev)
             for a in plan.acts:
                 a.written[:] = False
-            plan.output.mark()
             plan.grad_flat.zero_()
             for t in plan._scratch:
                 t.zero_()
+            plan.output.mark()
             plan._begin_side()
-            for op in reversed(plan.ops):
-                op.backward(plan, st)
+            plan._run(list(reversed(plan.ops)), "bwd")
             plan._join_side()
         plan.backward_from_output = backward_from_output
         cache[key] = plan
