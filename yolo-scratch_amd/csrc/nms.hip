@@ -275,10 +275,20 @@ nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp
 
     int head = 0;
     while (head < K) {
-        // record + broadcast the head box
-        if (tid == 0) {
+        // record + broadcast the head box: from the registers of the thread that holds sorted
+        // position `head` (no dependent global loads on the serial path), or from HBM for K > 8192
+        if (in_regs) {
+            if (tid == (head & (NMS_THREADS - 1))) {
+                const int hit = head / NMS_THREADS;
+#pragma unroll
+                for (int it = 0; it < REG_ITEMS; ++it)
+                    if (it == hit) head_box = mybox[it];
+            }
+        } else if (tid == 0) {
             int f = int(uint32_t(keys[head]));
             head_box = w.box[base + w.frow[base + f]];
+        }
+        if (tid == 0) {
             out_index[base + kept_pos_count] = head;   // sorted position for now
             kept_pos_count++;
         }
