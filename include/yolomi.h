@@ -266,6 +266,13 @@ int ym_loss_assignment(void* workspace, int64_t B, int64_t A, int M, const int**
 int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h,
                      const int* level_w, const float* strides, const float* dfl_w, float* y, void* stream);
 
+/* ------------------------------------------------------------------ data path
+ * Stretch-resize of a batch of grayscale uint8 images (packed back to back in `src`; meta[3b..3b+2]
+ * = {byte offset, h0, w0}) to size x size with OpenCV's fixed-point INTER_LINEAR, /255 -> fp32
+ * (batch, 1, size, size).  Replaces cv2.resize + astype(float32)/255 of the reference loader
+ * (datasets/crater_dataset_cuda.py:182-184, 253). */
+int ym_resize_linear_u8(const uint8_t* src, const int64_t* meta, int batch, int size, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

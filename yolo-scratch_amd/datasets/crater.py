@@ -1,0 +1,150 @@
+"""Crater dataset (CSV + grayscale images) with a GPU resize step.
+
+Drop-in for CraterDatasetCUDA (/root/reference/yolo_scratch_cuda/datasets/crater_dataset_cuda.py:
+26-286): same constructor, same annotation parsing (_load_annotations :77-124: every
+altitude*/longitude*/truth/detections.csv, rows grouped by inputImage, class from
+crater_classification or 2 when missing / -1, w/h = twice the ellipse semi-axes), same target
+normalisation (__getitem__ :262-279: by the ORIGINAL image size, cx/cy clamped to [0, 1], w/h to
+[0.01, 1]) and the same batch dict after collate + device transfer (img (B, 1, S, S) fp32 in
+[0, 1], batch_idx, cls, bboxes normalised xyxy clamped to [0, 1]).
+
+What moves: the reference decodes AND stretch-resizes every image with cv2 on the CPU inside the
+DataLoader workers and ships fp32 tensors.  Here the workers only decode (PIL; RGB inputs are
+converted with OpenCV's fixed-point luma so IMREAD_GRAYSCALE is matched), __getitem__ returns the
+raw uint8 image (1, h0, w0), collate packs the batch's bytes into one pinned buffer, and
+`prepare_batch` copies it to the GPU (a quarter of the fp32 bytes) where one libyolomi launch
+(ym_resize_linear_u8, OpenCV's fixed-point INTER_LINEAR) produces the fp32 batch.  The FIFO
+image buffer of the reference (:47-58, :188-211) is a RAM-capping cache for Colab; the build keeps
+the `cache_images` flag (whole-dataset cache of the decoded bytes) and drops the FIFO.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+from pathlib import Path
+
+import numpy as np
+import torch
+
+
+def _gray_u8(path: str) -> np.ndarray:
+    from PIL import Image
+    with Image.open(path) as im:
+        if im.mode in ("I;16", "I;16B", "I"):
+            # 16-bit grayscale: IMREAD_GRAYSCALE scales to 8 bits by >> 8
+            return (np.asarray(im, dtype=np.uint32) >> 8).astype(np.uint8)
+        if im.mode in ("L", "LA", "1"):
+            return np.array(im.convert("L"), dtype=np.uint8)
+        rgb = np.asarray(im.convert("RGB"), dtype=np.int64)      # palette / RGB(A): OpenCV's luma below
+    # OpenCV RGB->GRAY fixed point (R*4899 + G*9617 + B*1868 + 8192) >> 14
+    return ((rgb[..., 0] * 4899 + rgb[..., 1] * 9617 + rgb[..., 2] * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+class CraterDatasetCUDA(torch.utils.data.Dataset):
+    """CSV + image crater dataset; images are returned as raw uint8 (1, h0, w0) (see module doc)."""
+
+    def __init__(self, data_dir, img_size=640, cache_images=False, augment=True):
+        self.data_dir = Path(data_dir)
+        self.img_size = img_size
+        self.cache_images = cache_images
+        self.augment = augment
+        self.class_map = {"A": 0, "AB": 1, "B": 2, "BC": 3, "C": 4}
+        self.samples = self._load_annotations()
+        self._cache = {}
+        print(f"Loaded {len(self.samples)} image paths")
+
+    def _load_annotations(self):
+        import pandas as pd
+        samples = []
+        for csv_path in glob.glob(str(self.data_dir / "altitude*/longitude*/truth/detections.csv")):
+            csv_path = Path(csv_path)
+            parent = csv_path.parent.parent
+            df = pd.read_csv(csv_path)
+            for img_name, img_df in df.groupby("inputImage"):
+                img_path = parent / img_name
+                if not img_path.exists():
+                    continue
+                anns = []
+                for _, row in img_df.iterrows():
+                    c = row.get("crater_classification", -1)
+                    c = 2 if (pd.isna(c) or c == -1) else int(c)
+                    anns.append({"cx": float(row["ellipseCenterX(px)"]), "cy": float(row["ellipseCenterY(px)"]),
+                                 "w": 2.0 * float(row["ellipseSemimajor(px)"]),
+                                 "h": 2.0 * float(row["ellipseSemiminor(px)"]), "class": c})
+                if anns:
+                    samples.append({"img_path": str(img_path), "annotations": anns})
+        return samples
+
+    def __len__(self):
+        return len(self.samples)
+
+    def load_image(self, i: int):
+        """(uint8 (h0, w0), (h0, w0)); decoded bytes only — the resize runs on the GPU."""
+        if i < 0 or i >= len(self.samples):
+            raise IndexError(f"Index {i} out of range for dataset of size {len(self.samples)}")
+        im = self._cache.get(i)
+        if im is None:
+            path = self.samples[i]["img_path"]
+            if not Path(path).exists():
+                raise FileNotFoundError(f"Image file does not exist: {path}")
+            im = _gray_u8(path)
+            if im.ndim != 2 or im.size == 0:
+                raise ValueError(f"Invalid image shape {im.shape} for {path}")
+            if self.cache_images:
+                self._cache[i] = im
+        return im, im.shape
+
+    def __getitem__(self, idx):
+        im, (h0, w0) = self.load_image(idx)
+        boxes, labels = [], []
+        for a in self.samples[idx]["annotations"]:
+            boxes.append([max(0.0, min(1.0, a["cx"] / w0)), max(0.0, min(1.0, a["cy"] / h0)),
+                          max(0.01, min(1.0, a["w"] / w0)), max(0.01, min(1.0, a["h"] / h0))])
+            labels.append(a["class"])
+        if boxes:
+            boxes = torch.tensor(boxes, dtype=torch.float32)
+            labels = torch.tensor(labels, dtype=torch.long)
+        else:
+            boxes = torch.zeros((0, 4), dtype=torch.float32)
+            labels = torch.zeros((0,), dtype=torch.long)
+        img = torch.from_numpy(np.ascontiguousarray(im)).unsqueeze(0)      # (1, h0, w0) uint8
+        img.img_size = self.img_size
+        return img, boxes, labels, idx
+
+
+def pack_images(imgs, img_size: int):
+    """Raw uint8 (1, h, w) images -> one pinned byte buffer + meta (B, 3) int64 {offset, h, w}."""
+    sizes = [int(t.shape[-2]) * int(t.shape[-1]) for t in imgs]
+    total = sum(sizes)
+    buf = torch.empty(max(total, 1), dtype=torch.uint8)
+    meta = torch.empty(len(imgs), 3, dtype=torch.int64)
+    off = 0
+    for i, (t, n) in enumerate(zip(imgs, sizes)):
+        buf[off:off + n] = t.reshape(-1)
+        meta[i, 0], meta[i, 1], meta[i, 2] = off, int(t.shape[-2]), int(t.shape[-1])
+        off += n
+    if torch.cuda.is_available():
+        buf, meta = buf.pin_memory(), meta.pin_memory()
+    return {"img_u8": buf, "img_meta": meta, "img_size": int(img_size)}
+
+
+def resize_batch(img_u8: torch.Tensor, meta: torch.Tensor, img_size: int) -> torch.Tensor:
+    """GPU: packed uint8 images -> (B, 1, S, S) fp32 (ym_resize_linear_u8)."""
+    from yolomi._lib import call, require_device, stream_ptr
+    require_device(img_u8, meta)
+    B = meta.shape[0]
+    out = torch.empty(B, 1, img_size, img_size, dtype=torch.float32, device=img_u8.device)
+    call("ym_resize_linear_u8", img_u8.data_ptr(), meta.contiguous().data_ptr(), B, img_size, out.data_ptr(),
+         stream_ptr(img_u8.device))
+    return out
+
+
+def prepare_batch(batch: dict, device) -> dict:
+    """Device transfer of a collated batch (train_yolo11_cuda.py:43-45), running the GPU resize when
+    the batch carries raw images.  Tensors are copied non_blocking from pinned memory."""
+    out = {}
+    for k, v in batch.items():
+        out[k] = v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v
+    if "img_u8" in out:
+        out["img"] = resize_batch(out.pop("img_u8"), out.pop("img_meta"), out.pop("img_size"))
+    return out

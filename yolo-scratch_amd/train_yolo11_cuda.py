@@ -27,7 +27,7 @@ sys.path.insert(0, str(Path(__file__).parent))
 
 from models.yolo11_model import build_yolo11  # noqa: E402
 from losses.yolo_v8_loss import v8DetectionLoss  # noqa: E402
-from datasets import collate_fn_cuda  # noqa: E402
+from datasets import collate_fn_cuda, prepare_batch  # noqa: E402
 from utils.metrics import evaluate_detections  # noqa: E402
 from yolomi import post as _post  # noqa: E402
 
@@ -50,9 +50,7 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, epoch, epoc
     sums = torch.zeros(4, device=device)
     n = 0
     for batch_idx, batch in enumerate(pbar):
-        for k, v in batch.items():
-            if isinstance(v, torch.Tensor):
-                batch[k] = v.to(device, non_blocking=True)
+        batch = prepare_batch(batch, device)        # H2D (+ GPU resize of raw images)
         optimizer.zero_grad(set_to_none=True)
         preds = model(batch["img"])
         loss, loss_items = criterion(preds, batch)
@@ -79,9 +77,7 @@ def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_thre
     all_predictions, all_targets = [], []
     batches = 0
     for batch in _tqdm(dataloader, desc="Validating"):
-        for k, v in batch.items():
-            if isinstance(v, torch.Tensor):
-                batch[k] = v.to(device, non_blocking=True)
+        batch = prepare_batch(batch, device)
         preds = model(batch["img"])
         loss, loss_items = criterion(preds, batch)
         sums[0] += loss
@@ -206,7 +202,9 @@ def main():
         if dp_ctx:
             tr = Subset(tr, list(range(dp_ctx.rank, len(tr), dp_ctx.world)))
         nw = min(args.workers, 4)
-        kw = dict(batch_size=args.batch, num_workers=nw, collate_fn=collate_fn, pin_memory=True,
+        import functools
+        kw = dict(batch_size=args.batch, num_workers=nw, collate_fn=functools.partial(collate_fn, img_size=args.imgsz),
+                  pin_memory=True,
                   persistent_workers=nw > 0, prefetch_factor=2 if nw > 0 else None, drop_last=False)
         train_loader = DataLoader(tr, shuffle=True, **kw)
         val_loader = DataLoader(va, shuffle=False, **kw)
