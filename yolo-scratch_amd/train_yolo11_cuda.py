@@ -143,6 +143,27 @@ def cosine_lr_schedule(optimizer, epoch, epochs, lr_min=1e-6, lr_max=1e-3, warmu
     return lr
 
 
+def make_checkpoint(epoch, model, optimizer, train_metrics, val_metrics, best_loss, best_mAP50):
+    """The reference's checkpoint dict (train_yolo11_cuda.py:628-636), key for key: last.pt / best.pt
+    written by either implementation resume in the other (tests/test_models_cpu.py)."""
+    return {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
+            "train_metrics": train_metrics, "val_metrics": val_metrics, "best_loss": best_loss,
+            "best_mAP50": best_mAP50}
+
+
+def resume_checkpoint(path, model, optimizer, device):
+    """Resume as the reference does (:576-586) -> (start_epoch, best_loss, best_mAP50).  Loaded with
+    weights_only=True (the dict holds tensors, numbers and metric dicts only); the optimizer keeps
+    this process's fused/foreach implementation choice across a reference-written state."""
+    ckpt = torch.load(path, map_location=device, weights_only=True)
+    model.load_state_dict(ckpt["model_state_dict"])
+    impl = [{k: g.get(k) for k in ("fused", "foreach")} for g in optimizer.param_groups]
+    optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    for g, kv in zip(optimizer.param_groups, impl):
+        g.update(kv)
+    return ckpt["epoch"] + 1, ckpt.get("best_loss", float("inf")), ckpt.get("best_mAP50", 0.0)
+
+
 class _SyntheticLoader:
     def __init__(self, n, batch, imgsz, seed):
         from datasets.synthetic import synth_batch
@@ -227,12 +248,9 @@ def main():
     dp = ydist.GradSync(model, dp_ctx) if dp_ctx else None
     start_epoch, best_loss, best_mAP50 = 0, float("inf"), 0.0
     if args.resume and os.path.isfile(args.resume):
-        ckpt = torch.load(args.resume, map_location=device, weights_only=True)
-        model.load_state_dict(ckpt["model_state_dict"])
-        optimizer.load_state_dict(ckpt["optimizer_state_dict"])
-        start_epoch = ckpt["epoch"] + 1
-        best_loss = ckpt.get("best_loss", best_loss)
-        best_mAP50 = ckpt.get("best_mAP50", best_mAP50)
+        start_epoch, best_loss, best_mAP50 = resume_checkpoint(args.resume, model, optimizer, device)
+        if rank0:
+            print(f"Resumed from epoch {start_epoch}, best_loss={best_loss:.4f}, best_mAP50={best_mAP50:.4f}")
     if dp:
         dp.broadcast_state()
 
@@ -251,8 +269,7 @@ def main():
               f"DFL: {vm['dfl_loss']:.4f}")
         print(f"  Metrics - P: {vm.get('precision', 0.0):.4f}, R: {vm.get('recall', 0.0):.4f}, "
               f"mAP50: {vm.get('mAP50', 0.0):.4f}, mAP50-95: {vm.get('mAP50-95', 0.0):.4f}")
-        ckpt = {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
-                "train_metrics": tm, "val_metrics": vm, "best_loss": best_loss, "best_mAP50": best_mAP50}
+        ckpt = make_checkpoint(epoch, model, optimizer, tm, vm, best_loss, best_mAP50)
         torch.save(ckpt, save_dir / "last.pt")
         if "mAP50" in vm:
             if vm["mAP50"] > best_mAP50:
