@@ -1,8 +1,6 @@
 set -o pipefail
-mkdir -p gpurun_out/pin
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_conv.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pin/conv_tests.log 2>&1 || { tail -40 gpurun_out/pin/conv_tests.log; exit 1; }
-tail -1 gpurun_out/pin/conv_tests.log
-for V in "X=0" "YM_CONV_HALO=0"; do
-  env $V timeout -k 10 240 python3 tools/layer_bench.py --reps 10 > gpurun_out/pin/$V.txt 2>&1 || exit 1
-done
-tail -1 gpurun_out/pin/*.txt
+mkdir -p $GRAFT_REPO_ROOT/gpurun_out/nms4
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_post.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > gpurun_out/nms_t.log 2>&1 || { tail -30 gpurun_out/nms_t.log; exit 1; }
+tail -1 gpurun_out/nms_t.log
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/nms4/prof -o run -- python3 $GRAFT_REPO_ROOT/tools/infer_bench.py --no-cpu-baseline --reps 5 > $GRAFT_REPO_ROOT/gpurun_out/nms4/infer.json 2>&1; echo "rocprof $?"
+cd /tmp && YM_NMS_BITMASK=0 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/nms4/prof_off -o run -- python3 $GRAFT_REPO_ROOT/tools/infer_bench.py --no-cpu-baseline --reps 5 --batches 1 > /dev/null 2>&1; echo "rocprof $?"

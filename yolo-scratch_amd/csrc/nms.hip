@@ -17,6 +17,8 @@
 //           tests the boxes it holds in registers, drops IoU > thr, and a
 //           block min-reduction finds the next alive head        (:380-397)
 //        d. write kept boxes / img_size clamped to [0,1]          (:342-350)
+#include <cstdlib>
+
 #include "common.h"
 
 namespace ym {
@@ -33,8 +35,18 @@ struct Ws {
     int32_t* label;   // [B][N]
     int32_t* flag;    // [B][N]
     int32_t* frow;    // [B][N] filtered index -> row
-    uint64_t* keys;   // [B][N] (global sort path)
+    uint64_t* keys;   // [B][KP] (global sort path; sorted keys of the bitmask path)
+    float4* sbox;     // [B][N] boxes in sorted order      (bitmask path)
+    uint64_t* mask;   // [B][N][Wn] suppression bitmask    (bitmask path)
+    int32_t* kcount;  // [B] candidates after the filter   (bitmask path)
 };
+
+// Bitmask path (small batches: one image is too little work for one workgroup's greedy loop):
+// sort per image, then the upper-triangular IoU > thr bitmask of the sorted candidates over the
+// whole GPU, then a chunked greedy scan per image.  Needs the [64][Wn] chunk double buffer in LDS.
+constexpr int64_t BM_MAX_B = 8;
+constexpr int64_t BM_MAX_WN = 150;            // N <= 9600 (640x640: 8400 anchors)
+inline bool bitmask_path(int64_t B, int64_t N) { return B <= BM_MAX_B && (N + 63) / 64 <= BM_MAX_WN && N >= 128; }
 
 __host__ __device__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -42,6 +54,12 @@ inline int64_t pow2_at_least(int64_t x) {
     int64_t p = 1;
     while (p < x) p <<= 1;
     return p;
+}
+
+inline size_t bitmask_bytes(int64_t B, int64_t N) {
+    if (!bitmask_path(B, N)) return 0;
+    const size_t n = size_t(B) * size_t(N), wn = size_t((N + 63) / 64);
+    return align256(n * 16) + align256(n * wn * 8) + align256(size_t(B) * 4);
 }
 
 inline Ws carve(void* base, int64_t B, int64_t N) {
@@ -53,13 +71,21 @@ inline Ws carve(void* base, int64_t B, int64_t N) {
     w.label = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
     w.flag = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
     w.frow = reinterpret_cast<int32_t*>(p); p += align256(n * sizeof(int32_t));
-    w.keys = reinterpret_cast<uint64_t*>(p);
+    w.keys = reinterpret_cast<uint64_t*>(p); p += align256(size_t(B) * pow2_at_least(N) * 8);
+    w.sbox = nullptr; w.mask = nullptr; w.kcount = nullptr;
+    if (bitmask_path(B, N)) {
+        const size_t wn = size_t((N + 63) / 64);
+        w.sbox = reinterpret_cast<float4*>(p);   p += align256(n * 16);
+        w.mask = reinterpret_cast<uint64_t*>(p); p += align256(n * wn * 8);
+        w.kcount = reinterpret_cast<int32_t*>(p);
+    }
     return w;
 }
 
 inline size_t ws_bytes(int64_t B, int64_t N) {
     size_t n = size_t(B) * size_t(N);
-    return align256(n * 16) + 4 * align256(n * 4) + align256(size_t(B) * pow2_at_least(N) * 8) + 256;
+    return align256(n * 16) + 4 * align256(n * 4) + align256(size_t(B) * pow2_at_least(N) * 8) + bitmask_bytes(B, N) +
+           256;
 }
 
 // IoU in the reference's op order (train_yolo11_cuda.py:418-435).
@@ -202,6 +228,7 @@ __device__ void bitonic(uint64_t* keys, int P) {
 }
 
 // ---------------------------------------------------------------- stage 2
+template <bool SORT_ONLY>
 __global__ void __launch_bounds__(NMS_THREADS)
 nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp_norm, Ws w,
                  int32_t* __restrict__ out_count, float* __restrict__ out_boxes, float* __restrict__ out_scores,
@@ -232,7 +259,15 @@ nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp
     }
     __syncthreads();
     if (K == 0) {
-        if (tid == 0) out_count[b] = 0;
+        if (tid == 0) {
+            out_count[b] = 0;
+            if (SORT_ONLY) w.kcount[b] = 0;
+        }
+        return;
+    }
+    if constexpr (SORT_ONLY) {        // bitmask path: the sort runs over the whole GPU (nms_rank_kernel)
+        for (int64_t r = tid; r < N; r += NMS_THREADS) w.flag[base + r] = 0;   // rank counters
+        if (tid == 0) w.kcount[b] = K;
         return;
     }
 
@@ -247,8 +282,10 @@ nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp
         keys[i] = key;
     }
     __syncthreads();
-    if (lds_sort) bitonic<true>(keys, P);
-    else bitonic<false>(keys, P);
+    // the LDS image is sorted through the __shared__ pointer itself (ds_ instructions); the generic
+    // `keys` pointer would compile to flat loads/stores, ~10x slower for the 91 bitonic stages
+    if (lds_sort) bitonic<true>(skeys, P);
+    else bitonic<false>(w.keys + b * KP, P);
 
     // c. greedy loop; sorted position s -> filtered index f = keys[s] low bits
     float4 mybox[REG_ITEMS];
@@ -343,11 +380,237 @@ nms_image_kernel(int64_t N, int64_t KP, float iou_thr, float img_size, int clamp
     if (tid == 0) out_count[b] = nk;
 }
 
+// Sort of the filtered candidates (bitmask path) by rank: the keys (score descending, filtered
+// index ascending) are unique, so key i goes to position #{j : key_j < key_i}.  K^2 comparisons
+// over a (key tile i, key tile j) grid; the per-tile counts are integer atomics into rank[] (w.flag,
+// zeroed by the compaction kernel) — order-independent, so the result is exact.
+__device__ __forceinline__ uint64_t cand_key(const Ws& w, int64_t base, int f) {
+    return (uint64_t(desc_bits(w.score[base + w.frow[base + f]])) << 32) | uint32_t(f);
+}
+
+__global__ void __launch_bounds__(256) nms_rank_kernel(int64_t N, Ws w) {
+    __shared__ uint64_t tile[256];
+    const int64_t b = blockIdx.z;
+    const int K = w.kcount[b];
+    const int i0 = blockIdx.x * 256, j0 = blockIdx.y * 256;
+    if (i0 >= K || j0 >= K) return;
+    const int64_t base = b * N;
+    const int i = i0 + threadIdx.x;
+    tile[threadIdx.x] = j0 + int(threadIdx.x) < K ? cand_key(w, base, j0 + threadIdx.x) : ~0ull;
+    __syncthreads();
+    if (i >= K) return;
+    const uint64_t ki = cand_key(w, base, i);
+    const int jn = min(256, K - j0);
+    int cnt = 0;
+    for (int jj = 0; jj < jn; ++jj) cnt += tile[jj] < ki;
+    if (cnt) atomicAdd(&w.flag[base + i], cnt);
+}
+
+__global__ void nms_rank_scatter_kernel(int64_t N, int64_t KP, Ws w) {
+    const int64_t b = blockIdx.y;
+    const int K = w.kcount[b];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= K) return;
+    const int64_t base = b * N;
+    const int r = w.flag[base + i];
+    w.keys[b * KP + r] = cand_key(w, base, i);
+    w.sbox[base + r] = w.box[base + w.frow[base + i]];
+}
+
+// maskT[b][cb][i] bit j-64cb = (j > i) && !(IoU(i, j) <= thr) for sorted positions i, j < K; only
+// cb >= i/64 is written (the scan reads the upper triangle).  Block = 64 rows of one row block.
+__global__ void __launch_bounds__(64) nms_mask_kernel(int64_t N, int Wn, float iou_thr, Ws w) {
+    __shared__ float4 cols[64];
+    const int cb = blockIdx.x, rb = blockIdx.y;
+    const int64_t b = blockIdx.z;
+    const int K = w.kcount[b];
+    if (cb < rb || rb * 64 >= K) return;
+    const int t = threadIdx.x;
+    const int64_t base = b * N;
+    const int j0 = cb * 64;
+    if (j0 + t < K) cols[t] = w.sbox[base + j0 + t];
+    __syncthreads();
+    const int i = rb * 64 + t;
+    if (i >= K) return;
+    const float4 bi = w.sbox[base + i];
+    uint64_t word = 0;
+    const int jn = min(64, K - j0);
+    for (int jj = 0; jj < jn; ++jj) {
+        const int j = j0 + jj;
+        if (j > i && !(iou_ref(bi, cols[jj]) <= iou_thr)) word |= uint64_t(1) << jj;
+    }
+    w.mask[(b * Wn + cb) * N + i] = word;          // column-major: column cb, row i
+}
+
+// diagnostic segment timers of nms_scan_kernel (block 0, thread 0), read by ym_debug_nms_stamps;
+// enabled only when YM_NMS_STAMPS is set (a wave-uniform branch otherwise)
+__device__ unsigned long long g_nms_stamps[8];
+__device__ __forceinline__ unsigned long long stamp_now() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+
+// Greedy scan over 64-candidate chunks, one 256-thread workgroup per image, on the column-major
+// mask: chunk c's column holds, for every earlier sorted position j, the bits of chunk c that j
+// suppresses.  Removed bits of chunk c = OR over KEPT j < 64c of column c; then the chunk's own
+// 64x64 diagonal block is resolved.  Thread tid owns rows j = tid + 256 q of every column: it keeps
+// the column in registers (two sets: column c+1 streams in while chunk c is processed) and its
+// rows' keep decisions in a bit mask, so the removed-bits reduction is registers + one wave OR +
+// a 4-entry LDS combine; the diagonal segment of chunk c (rows 64c..64c+63) is exactly the register
+// q = c/4 of wave c%4, which resolves the chunk.  Same keep-lists as the one-workgroup greedy loop
+// (a box is kept iff no earlier kept box has IoU > thr with it).
+__device__ __forceinline__ uint64_t wave_or64(uint64_t m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t lo = uint32_t(m), hi = uint32_t(m >> 32);
+        m |= (uint64_t(uint32_t(__shfl_xor(int(hi), o, 64))) << 32) | uint32_t(__shfl_xor(int(lo), o, 64));
+    }
+    return m;
+}
+
+__global__ void __launch_bounds__(256) nms_scan_kernel(int64_t N, int64_t KP, int Wn, float img_size, Ws w,
+                                                       int32_t* __restrict__ out_count, float* __restrict__ out_boxes,
+                                                       float* __restrict__ out_scores, int64_t* __restrict__ out_labels,
+                                                       int64_t* __restrict__ out_index, int stamps) {
+    __shared__ uint64_t red[4];
+    __shared__ uint64_t kept_sh;
+    __shared__ int nkept_sh;
+    const bool st0 = stamps && blockIdx.x == 0 && threadIdx.x == 0;
+    unsigned long long tsum[4] = {0, 0, 0, 0}, tprev = 0;
+    auto stamp = [&](int seg) {
+        if (st0) {
+            const unsigned long long t = stamp_now();
+            if (seg >= 0) tsum[seg] += t - tprev;
+            tprev = t;
+        }
+    };
+    const int64_t b = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = w.kcount[b];
+    const int64_t base = b * N;
+    if (K == 0) {
+        if (tid == 0) out_count[b] = 0;
+        return;
+    }
+    const int nch = (K + 63) / 64;
+    if (tid == 0) nkept_sh = 0;
+    constexpr int LQ = (64 * BM_MAX_WN + 255) / 256;
+    static_assert(LQ <= 64, "keep mask is one 64-bit word per thread");
+    uint64_t colA[LQ], colB[LQ];
+    uint64_t mykeep = 0;                                  // bit q: row tid + 256 q was kept
+    // column c = rows 0 .. min(64(c+1), K) - 1; loads guarded by a wave-uniform bound (scalar
+    // branch) with a clamped index, so they issue back to back.  (hipcc still waits vmcnt(0) for the
+    // older column — measured: an exact-count variant with LQ unguarded loads is slower.)
+    auto load_col = [&](int c, uint64_t* dst) {
+        const uint64_t* src = w.mask + (b * Wn + c) * N;
+        const int L = min(64 * (c + 1), K);
+        const int qn = (L + 255) / 256;
+#pragma unroll
+        for (int q = 0; q < LQ; ++q)
+            if (q < qn) dst[q] = src[min(tid + 256 * q, L - 1)];
+    };
+    auto chunk = [&](int c, const uint64_t* cur) {
+        stamp(0);
+        // removed bits of chunk c: kept rows j < 64c
+        const int qj = (64 * c + 255) / 256;
+        uint64_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < LQ; ++q)
+            if (q < qj && ((mykeep >> q) & 1) && tid + 256 * q < 64 * c) acc |= cur[q];
+        acc = wave_or64(acc);
+        if (lane == 0) red[wave] = acc;
+        __syncthreads();
+        stamp(1);
+        const int qc = c >> 2;
+        if (wave == (c & 3)) {
+            const uint64_t rem = red[0] | red[1] | red[2] | red[3];
+            uint64_t diag = 0;
+#pragma unroll
+            for (int q = 0; q < LQ; ++q)
+                if (q == qc) diag = cur[q];
+            const int rows = min(64, K - 64 * c);
+            if (lane >= rows) diag = 0;
+            // the chunk's decisions are the unique fixpoint of alive = init & ~OR{diag_s : s alive}
+            // (diag_s only has bits after s: acyclic); Jacobi rounds from alive = init reach it in
+            // (longest suppression chain + 1) rounds; two equal rounds mean the fixpoint
+            const uint64_t init = ~rem & (rows == 64 ? ~uint64_t(0) : ((uint64_t(1) << rows) - 1));
+            uint64_t alive = init;
+            for (int it = 0; it <= 64; ++it) {
+                const uint64_t nxt = init & ~wave_or64(((alive >> lane) & 1) ? diag : 0);
+                if (nxt == alive) break;
+                alive = nxt;
+            }
+            const int before = __popcll(alive & ((uint64_t(1) << lane) - 1));
+            if ((alive >> lane) & 1) out_index[base + nkept_sh + before] = 64 * c + lane;
+            if (lane == 0) kept_sh = alive;
+        }
+        __syncthreads();
+        stamp(2);
+        const uint64_t kept = kept_sh;
+        if (wave == (c & 3)) mykeep |= ((kept >> lane) & 1) << qc;
+        if (tid == 0) nkept_sh += __popcll(kept);
+        // nkept_sh / kept_sh are rewritten only after the next chunk's first barrier
+        stamp(3);
+    };
+    load_col(0, colA);
+    stamp(-1);
+    for (int c = 0; c < nch; c += 2) {
+        if (c + 1 < nch) load_col(c + 1, colB);      // in flight while chunk c is processed
+        chunk(c, colA);
+        if (c + 1 >= nch) break;
+        if (c + 2 < nch) load_col(c + 2, colA);
+        chunk(c + 1, colB);
+    }
+    if (st0)
+        for (int k = 0; k < 4; ++k) g_nms_stamps[k] = tsum[k];
+    __syncthreads();
+    // outputs in kept order (sorted position -> filtered index -> row)
+    const int nk = nkept_sh;
+    for (int k = tid; k < nk; k += 256) {
+        const int spos = int(out_index[base + k]);
+        const int f = int(uint32_t(w.keys[b * KP + spos]));
+        const int64_t row = base + w.frow[base + f];
+        float4 bx = w.box[row];
+        bx.x = fminf(fmaxf(bx.x / img_size, 0.0f), 1.0f);
+        bx.y = fminf(fmaxf(bx.y / img_size, 0.0f), 1.0f);
+        bx.z = fminf(fmaxf(bx.z / img_size, 0.0f), 1.0f);
+        bx.w = fminf(fmaxf(bx.w / img_size, 0.0f), 1.0f);
+        reinterpret_cast<float4*>(out_boxes)[base + k] = bx;
+        out_scores[base + k] = w.score[row];
+        out_labels[base + k] = w.label[row];
+    }
+    __syncthreads();
+    for (int k = tid; k < nk; k += 256) out_index[base + k] = int(uint32_t(w.keys[b * KP + out_index[base + k]]));
+    if (tid == 0) out_count[b] = nk;
+}
+
 int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int clamp_norm, Ws w,
                int32_t* out_count, float* out_boxes, float* out_scores, int64_t* out_labels, int64_t* out_index,
                hipStream_t st) {
     size_t lds = size_t(SORT_LDS_KEYS) * sizeof(uint64_t);
-    hipLaunchKernelGGL(nms_image_kernel, dim3(unsigned(B)), dim3(NMS_THREADS), lds, st, Nalloc,
+    static const int no_bitmask = [] {
+        const char* e = getenv("YM_NMS_BITMASK");
+        return e && e[0] == '0';
+    }();
+    if (w.mask && clamp_norm && !no_bitmask) {
+        const int Wn = int((Nalloc + 63) / 64);
+        const int64_t KP = pow2_at_least(Nalloc);
+        hipLaunchKernelGGL(nms_image_kernel<true>, dim3(unsigned(B)), dim3(NMS_THREADS), lds, st, Nalloc, KP, iou_thr,
+                           img_size, clamp_norm, w, out_count, out_boxes, out_scores, out_labels, out_index);
+        const unsigned nt = unsigned((Nalloc + 255) / 256);
+        hipLaunchKernelGGL(nms_rank_kernel, dim3(nt, nt, unsigned(B)), dim3(256), 0, st, Nalloc, w);
+        hipLaunchKernelGGL(nms_rank_scatter_kernel, dim3(nt, unsigned(B)), dim3(256), 0, st, Nalloc, KP, w);
+        hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn), unsigned(Wn), unsigned(B)), dim3(64), 0, st, Nalloc, Wn,
+                           iou_thr, w);
+        const size_t scan_lds = 0;
+        static const int stamps = getenv("YM_NMS_STAMPS") != nullptr;
+        hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), scan_lds, st, Nalloc, KP, Wn, img_size, w,
+                           out_count, out_boxes, out_scores, out_labels, out_index, stamps);
+        YM_LAUNCH_CHECK("nms bitmask path");
+        return YM_OK;
+    }
+    hipLaunchKernelGGL(nms_image_kernel<false>, dim3(unsigned(B)), dim3(NMS_THREADS), lds, st, Nalloc,
                        pow2_at_least(Nalloc), iou_thr, img_size,
                        clamp_norm, w, out_count, out_boxes, out_scores, out_labels, out_index);
     YM_LAUNCH_CHECK("nms_image_kernel");
@@ -360,6 +623,13 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
 using namespace ym;
 
 extern "C" size_t ym_nms_workspace_size(int64_t B, int64_t N) { return 2 * ws_bytes(B, N); }
+
+// diagnostics: segment cycle totals of the last bitmask-path scan (YM_NMS_STAMPS set):
+// [0] between chunks (load issue), [1] removed-bits reduction, [2] diagonal resolve, [3] keep update
+extern "C" int ym_debug_nms_stamps(unsigned long long* out4) {
+    return hipMemcpyFromSymbol(out4, HIP_SYMBOL(ym::g_nms_stamps), 4 * sizeof(unsigned long long)) == hipSuccess
+               ? YM_OK : YM_ERR_HIP;
+}
 
 __global__ void ym_iou_row_kernel(const float4* __restrict__ b1, const float4* __restrict__ b2, int64_t m,
                                   float* __restrict__ out) {
