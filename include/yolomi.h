@@ -102,6 +102,11 @@ int ym_eval_detections(const float* pred_boxes, const float* pred_scores, const 
 int ym_eval_ap(const float* scores, const uint8_t* is_tp, int64_t n, int64_t n_gt, void* workspace,
                size_t workspace_bytes, double* out, void* stream);
 
+/* Diagnostics: segment cycle totals (s_memtime) of the last small-batch NMS scan, recorded when
+ * YM_NMS_STAMPS is set in the environment: [0] between chunks, [1] removed-bits reduction,
+ * [2] diagonal resolve, [3] keep update. */
+int ym_debug_nms_stamps(unsigned long long* out4);
+
 /* calculate_iou_batch (utils/metrics.py:49-81): out[i*m+j] = IoU(boxes1[i], boxes2[j]),
  * xyxy fp32 in the reference's op order. */
 int ym_iou_matrix(const float* boxes1, const float* boxes2, int64_t n, int64_t m, float* out, void* stream);

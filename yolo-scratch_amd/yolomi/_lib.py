@@ -87,6 +87,7 @@ SIGNATURES = {
     "ym_eval_detections": (R, [P, P, P, P, P, I64, I64, I64, I64, P, INT, INT, INT, F32, P, SZ, P, P]),
     "ym_eval_ap": (R, [P, P, I64, I64, P, SZ, P, P]),
     "ym_iou_matrix": (R, [P, P, I64, I64, P, P]),
+    "ym_debug_nms_stamps": (R, [P]),
     "ym_resize_linear_u8": (R, [P, P, INT, INT, P, P]),
 }
 
