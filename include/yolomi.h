@@ -184,7 +184,9 @@ int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t tota
  * eps 1e-3 / momentum 0.03 from yolo11_model.py:183-185).  z is the dense (m, c) conv output in
  * fp16 (written by ym_conv_fwd with out_f32 = 2); dz (bf16) may overwrite it in place.
  */
-/* scratch for the two-level partial reductions of ym_bn_finalize / ym_bn_bwd_finalize */
+/* scratch for the two-level partial reductions of ym_bn_finalize / ym_bn_bwd_finalize: fp64 rows
+ * plus ticket counters.  Zero it once before first use (the library leaves the counters at zero
+ * after every call); calls sharing one workspace must be ordered (same stream). */
 size_t ym_bn_workspace_size(int c);
 int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,

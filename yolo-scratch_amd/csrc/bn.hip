@@ -19,6 +19,7 @@
 // and keeps its channels' parameters in registers; every activation view is a
 // whole (B, H, W, ld) buffer, so pixel m lives at m*ld (no integer division).
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -145,6 +146,96 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ p2, int R, int
     coef[c] = gamma[c] * rstd[c];               // k1
     coef[C + c] = float(s / count);             // k2 = mean(g)
     coef[2 * C + c] = float(q / count);         // k3 = mean(g * xhat)
+}
+
+// ---------------------------------------------------------------- one-launch finalize
+// Level 1 of the partials reduction (grid (ceil(C/64), R)) and the finalize in ONE launch: every
+// level-1 block publishes its fp64 row, takes a ticket on its channel group's counter, and the
+// block drawing the last ticket folds the R rows and runs the finalize (forward: scale / shift /
+// mean / rstd / running stats; backward: dgamma / dbeta / apply coefficients) and re-arms the
+// counter.  Hand-off per MI355X_MICROARCH.md (workgroup dispatch & inter-workgroup visibility):
+// stores -> every wave vmcnt(0) -> barrier -> lane 0 agent release fence -> vmcnt(0) -> relaxed
+// agent fetch_add; the last arriver: agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// Deterministic: the fold reads the rows in a fixed order whatever order the blocks finished in.
+template <bool BWD>
+__global__ void __launch_bounds__(256) bn_finalize_fused_kernel(
+    const float* __restrict__ a, const float* __restrict__ bsq, int G, int C, int R, double count, double* p2,
+    unsigned* counters, const float* __restrict__ gamma, const float* __restrict__ beta, float* running_mean,
+    float* running_var, int64_t* nbt, float momentum, float eps, float* scale, float* shift, float* mean_out,
+    float* rstd_out, const float* __restrict__ rstd_in, float* dgamma, float* dbeta, int accumulate, float* coef) {
+    __shared__ double sh[2][4][64];
+    __shared__ int last_sh;
+    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const int per = (G + R - 1) / R;
+    const int g0 = blockIdx.y * per, g1 = min(G, g0 + per);
+    double s = 0.0, q = 0.0;
+    if (c < C) {
+#pragma unroll 4
+        for (int g = g0 + rg; g < g1; g += 4) {
+            s += a[int64_t(g) * C + c];
+            q += bsq[int64_t(g) * C + c];
+        }
+    }
+    sh[0][rg][cl] = s;
+    sh[1][rg][cl] = q;
+    __syncthreads();
+    if (rg == 0 && c < C) {
+        p2[(int64_t(blockIdx.y) * 2 + 0) * C + c] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+        p2[(int64_t(blockIdx.y) * 2 + 1) * C + c] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned t = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sh = t == unsigned(R - 1);
+        if (last_sh) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!last_sh) return;
+    // fold the R rows in a fixed order (as fold(): row groups over the 4 waves, then in order)
+    s = 0.0;
+    q = 0.0;
+    if (c < C)
+        for (int r = rg; r < R; r += 4) {
+            s += p2[(int64_t(r) * 2 + 0) * C + c];
+            q += p2[(int64_t(r) * 2 + 1) * C + c];
+        }
+    sh[0][rg][cl] = s;
+    sh[1][rg][cl] = q;
+    __syncthreads();
+    if (threadIdx.x == 0) counters[blockIdx.x] = 0u;   // re-armed for the next launch (same stream)
+    if (rg != 0 || c >= C) return;
+    s = (sh[0][0][cl] + sh[0][1][cl]) + (sh[0][2][cl] + sh[0][3][cl]);
+    q = (sh[1][0][cl] + sh[1][1][cl]) + (sh[1][2][cl] + sh[1][3][cl]);
+    if constexpr (!BWD) {
+        if (nbt && blockIdx.x == 0 && cl == 0) *nbt += 1;
+        const double mu = s / count;
+        double var = q / count - mu * mu;
+        if (var < 0) var = 0;
+        const double rstd = 1.0 / sqrt(var + double(eps));
+        const float sc = float(double(gamma[c]) * rstd);
+        scale[c] = sc;
+        shift[c] = float(double(beta[c]) - mu * double(sc));
+        mean_out[c] = float(mu);
+        rstd_out[c] = float(rstd);
+        if (running_mean) {
+            const double unb = count > 1 ? var * count / (count - 1) : var;
+            running_mean[c] = float((1.0 - momentum) * running_mean[c] + momentum * mu);
+            running_var[c] = float((1.0 - momentum) * running_var[c] + momentum * unb);
+        }
+    } else {
+        if (dgamma) dgamma[c] = float(accumulate ? dgamma[c] + q : q);
+        if (dbeta) dbeta[c] = float(accumulate ? dbeta[c] + s : s);
+        coef[c] = gamma[c] * rstd_in[c];
+        coef[C + c] = float(s / count);
+        coef[2 * C + c] = float(q / count);
+    }
 }
 
 // eval: scale/shift from running stats
@@ -348,7 +439,18 @@ using namespace ym;
 #define CHECK_VIEW(bs, ld, hw) YM_CHECK_ARG((bs) == int64_t(hw) * (ld) && (ld) % 8 == 0, \
                                             "BN: views must be whole-image buffers with 16-B aligned rows")
 
-extern "C" size_t ym_bn_workspace_size(int c) { return size_t(RED_R) * 2 * c * sizeof(double); }
+// 256 B of ticket counters (one per 64-channel group, c <= 2048 -> at most 32) at a fixed offset,
+// then the [RED_R][2][c] fp64 level-1 rows: calls with different c share one workspace safely
+constexpr size_t BN_CNT_BYTES = 256;
+extern "C" size_t ym_bn_workspace_size(int c) { return BN_CNT_BYTES + size_t(RED_R) * 2 * c * sizeof(double); }
+
+static bool bn_fused() {
+    static const int on = [] {
+        const char* e = getenv("YM_BN_FUSED");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count,
                               const float* gamma, const float* beta, float* running_mean, float* running_var,
@@ -356,7 +458,16 @@ extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int p
                               float* mean, float* rstd, void* workspace, void* stream) {
     YM_CHECK_ARG(count > 0 && workspace, "ym_bn_finalize: count must be > 0, workspace required");
     hipStream_t st = as_stream(stream);
-    double* p2 = static_cast<double*>(workspace);
+    double* p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
+    if (bn_fused()) {
+        unsigned* cnt = static_cast<unsigned*>(workspace);
+        hipLaunchKernelGGL((bn_finalize_fused_kernel<false>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
+                           part_sq, parts, c, RED_R, count, p2, cnt, gamma, beta, running_mean, running_var,
+                           num_batches_tracked, momentum, eps, scale, shift, mean, rstd, nullptr, nullptr, nullptr, 0,
+                           nullptr);
+        YM_LAUNCH_CHECK("ym_bn_finalize");
+        return YM_OK;
+    }
     hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_sq, parts,
                        c, RED_R, p2);
     hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma, beta,
@@ -406,7 +517,15 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
                                   float* coef, void* workspace, void* stream) {
     YM_CHECK_ARG(workspace, "ym_bn_bwd_finalize: workspace required");
     hipStream_t st = as_stream(stream);
-    double* p2 = static_cast<double*>(workspace);
+    double* p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
+    if (bn_fused()) {
+        unsigned* cnt = static_cast<unsigned*>(workspace);
+        hipLaunchKernelGGL((bn_finalize_fused_kernel<true>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
+                           part_dot, parts, c, RED_R, count, p2, cnt, gamma, nullptr, nullptr, nullptr, nullptr, 0.f,
+                           0.f, nullptr, nullptr, nullptr, nullptr, rstd, dgamma, dbeta, accumulate, coef);
+        YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
+        return YM_OK;
+    }
     hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_dot, parts,
                        c, RED_R, p2);
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma,

@@ -670,7 +670,8 @@ class Plan:
         """BatchNorm reduction scratch of the stream the current op runs on (ops on different
         streams run concurrently, so each stream has its own)."""
         while len(self._bn_ws) <= self._cur:
-            self._bn_ws.append(torch.empty(lib().ym_bn_workspace_size(2048) // 4, dtype=F32, device=self.dev))
+            # zeroed once: the one-launch finalize's ticket counters live at its end
+            self._bn_ws.append(torch.zeros((lib().ym_bn_workspace_size(2048) + 3) // 4, dtype=F32, device=self.dev))
         return self._bn_ws[self._cur]
 
     def wgrad_ws(self):
