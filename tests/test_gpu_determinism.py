@@ -2,8 +2,8 @@
 
 Every reduction in the HIP path runs in a fixed order (per-block partial rows summed in row order,
 waves combined in wave order; no float atomics), so the same step on the same inputs gives
-bit-identical heads, loss and parameter gradients — across repeated runs and with the weight
-gradients on the side stream or in line.  (The reference is a single-process fp32 PyTorch loop;
+bit-identical heads, loss and parameter gradients — across repeated runs, one or three scheduler
+streams, the weight gradients on the side stream or in line, and eager vs HIP-graph replay.  (The reference is a single-process fp32 PyTorch loop;
 reproducibility is what lets tests/test_gpu_curve.py compare 20-step curves without run-to-run drift.)
 """
 import os
@@ -40,11 +40,24 @@ def test_train_step_bit_reproducible():
     # BatchNorm running statistics move every step; restore them so each step sees the same model
     bufs = {k: v.clone() for k, v in m.state_dict().items()}
     runs = []
-    for side in ("1", "1", "0"):
-        os.environ["YM_SIDE_STREAM"] = side
+    os.environ["YM_GRAPH"] = "0"
+    for side, streams in (("1", "3"), ("1", "3"), ("0", "3"), ("1", "1")):
+        os.environ["YM_SIDE_STREAM"], os.environ["YM_STREAMS"] = side, streams
         m.load_state_dict(bufs)
         runs.append(_step(m, crit, b))
-    os.environ.pop("YM_SIDE_STREAM", None)
+    for k in ("YM_SIDE_STREAM", "YM_STREAMS"):
+        os.environ.pop(k, None)
+    os.environ["YM_GRAPH"] = "1"
+    # HIP-graph mode on a fresh model: eager, capture, replay
+    m2 = build_yolo11(cfg, ch=1, nc=5)
+    m2.load_state_dict(P)
+    m2 = m2.cuda().train()
+    crit2 = v8DetectionLoss(m2)
+    for _ in range(3):
+        m2.load_state_dict(bufs)
+        # a fresh image tensor each step: the replay copies it into the graph's static input
+        runs.append(_step(m2, crit2, dict(b, img=b["img"].clone())))
+    os.environ.pop("YM_GRAPH", None)
     ref = runs[0]
     for other in runs[1:]:
         for a, c in zip(ref[0], other[0]):

@@ -21,7 +21,10 @@ def _port():
     return p
 
 
-def test_gradsync_rccl_single_rank_matches_plain_backward():
+@pytest.mark.parametrize("graph", ["0", "1"])
+def test_gradsync_rccl_single_rank_matches_plain_backward(graph, monkeypatch):
+    """YM_GRAPH=0: eager backward, bucketed all-reduces launched from the backward hook.
+    YM_GRAPH=1: the backward replays as a HIP graph (no hooks), one all-reduce after it."""
     import torch.distributed as dist
     from oracle import model as om
     from models import build_yolo11
@@ -29,6 +32,7 @@ def test_gradsync_rccl_single_rank_matches_plain_backward():
     from datasets.synthetic import synth_batch
     from yolomi import dist as ydist
 
+    monkeypatch.setenv("YM_GRAPH", graph)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
@@ -50,6 +54,9 @@ def test_gradsync_rccl_single_rank_matches_plain_backward():
             torch.cuda.synchronize()
             got = m.__dict__["_ym_last_plan"].grad_flat
             assert torch.equal(got, plain), step
-        assert len(sync.buckets.ranges) > 1
+        if graph == "0":
+            assert len(sync.buckets.ranges) > 1
+        else:
+            assert sync.buckets is None and m.__dict__["_ym_last_plan"].graph_active
     finally:
         dist.destroy_process_group()

@@ -134,7 +134,11 @@ class GradSync:
         self.plan, self.buckets = None, None
 
     def _attach(self, plan):
-        """Hook the plan's backward so the NEXT backward launches buckets as it goes."""
+        """Hook the plan's backward so the NEXT backward launches buckets as it goes.  A plan that
+        replays its backward as a HIP graph takes no hooks: its gradient is all-reduced in one
+        collective after the backward (sync's first-step path, every step)."""
+        if getattr(plan, "graph_active", False):
+            return
         self.plan = plan
         self.buckets = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
         self.buckets.streams = getattr(plan, "comm_streams", None)

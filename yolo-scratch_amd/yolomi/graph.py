@@ -665,13 +665,20 @@ class Plan:
         """Size the shared split-K workspace of ym_conv_wgrad (ops run in order on one stream)."""
         self._wg_bytes = max(getattr(self, "_wg_bytes", 0), int(lib().ym_conv_wgrad_workspace_size(ctypes.byref(desc))))
 
+    def _alloc_bn_ws(self, K):
+        """Allocate the BN scratch of K scheduler streams, zeroed once (the one-launch finalize's
+        ticket counters live at offset 0 and re-arm themselves).  Runs on the caller's stream
+        before the other streams fork from it, so the zero fill is ordered before every op that
+        takes a ticket."""
+        while len(self._bn_ws) < K:
+            self._bn_ws.append(torch.zeros((lib().ym_bn_workspace_size(2048) + 3) // 4, dtype=F32, device=self.dev))
+
     @property
     def bn_ws(self):
         """BatchNorm reduction scratch of the stream the current op runs on (ops on different
         streams run concurrently, so each stream has its own)."""
-        while len(self._bn_ws) <= self._cur:
-            # zeroed once: the one-launch finalize's ticket counters live at its end
-            self._bn_ws.append(torch.zeros((lib().ym_bn_workspace_size(2048) + 3) // 4, dtype=F32, device=self.dev))
+        if len(self._bn_ws) <= self._cur:
+            raise YolomiError("BN workspace of a scheduler stream used before _run allocated it")
         return self._bn_ws[self._cur]
 
     def wgrad_ws(self):
@@ -704,7 +711,12 @@ class Plan:
     # dependency, otherwise it takes a stream whose tail it depends on, or the least recently used
     # one.  YM_STREAMS sets the stream count (1 = everything in order on the caller's stream).
     def _nstreams(self):
-        return max(1, int(os.environ.get("YM_STREAMS", "3"))) if self.dev.type == "cuda" else 1
+        if self.dev.type != "cuda":
+            return 1
+        k = max(1, int(os.environ.get("YM_STREAMS", "3")))
+        # HIP graph capture of the 3-stream schedule segfaults in the ROCm 7.2 runtime (forward
+        # capture, reproducible; 1 and 2 streams capture and replay correctly): graphs use 2
+        return min(k, 2) if self._graph_ok() else k
 
     def _schedule(self, ops, phase, K):
         key = (phase, K, len(ops))
@@ -761,6 +773,7 @@ class Plan:
 
     def _run(self, ops, phase, after=None):
         K = self._nstreams()
+        self._alloc_bn_ws(K)
         if K == 1:
             st = stream_ptr(self.dev)
             self._cur = 0
@@ -803,14 +816,69 @@ class Plan:
             main.wait_stream(s)
         self._cur, self._cur_stream = 0, None
 
+    # --------------------------------------------------------------- HIP graphs
+    # After one eager run (which allocates every workspace, stream and event), the whole forward
+    # and the whole backward of a model plan are captured once each as HIP graphs (all streams,
+    # events and kernels) and replayed: the per-step host work drops from ~900 ctypes launches to
+    # two graph launches, so the GPU no longer waits on Python between kernels.  The captured
+    # launches point at fixed buffers: the input image and the head gradient are copied into the
+    # plan's own static tensors when the caller's differ.  Not used while the bench probe times a
+    # kernel with events, or for block plans.  Data parallelism in graph mode all-reduces the flat
+    # gradient once after the backward (yolomi/dist.py).  Opt-in (YM_GRAPH=1): measured on the
+    # s@640 bs64 step, replay is 1.5-2 ms SLOWER than eager launches (26.3-26.7 vs 24.7 ms/step at
+    # 1 and 2 streams): the eager host enqueue already runs ahead of the GPU, and the replayed
+    # graph runs its kernels with less overlap than the streams do.
+    def _graph_ok(self):
+        return (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
+                and os.environ.get("YM_GRAPH", "0") == "1")
+
+    @property
+    def graph_active(self):
+        return self._graph_ok()
+
+    def _replay(self, phase, body, static_in):
+        """Eager on the first call of a phase, capture on the second, replay afterwards.
+        static_in: list of (attribute name, tensor) inputs the captured kernels read by address."""
+        graphs = self.__dict__.setdefault("_graphs", {})
+        runs = self.__dict__.setdefault("_eager_runs", {})
+        if not self._graph_ok():
+            body()
+            return
+        if runs.get(phase, 0) < 1:
+            runs[phase] = runs.get(phase, 0) + 1
+            body()
+            return
+        ent = graphs.get(phase)
+        if ent is None:
+            statics = {}
+            for name, t in static_in:
+                statics[name] = torch.empty_like(t)
+                statics[name].copy_(t)
+                setattr(self, name, statics[name])
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize(self.dev)
+            with torch.cuda.graph(g):
+                body()
+            graphs[phase] = ent = (g, statics)
+        g, statics = ent
+        for name, t in static_in:
+            st_t = statics[name]
+            if t.data_ptr() != st_t.data_ptr():
+                st_t.copy_(t)
+            setattr(self, name, st_t)
+        g.replay()
+
     # --------------------------------------------------------------- run
     def forward(self):
-        st = stream_ptr(self.dev)
-        self.weights.refresh(st)
-        self._run(self.ops, "fwd")
+        def body():
+            st = stream_ptr(self.dev)
+            self.weights.refresh(st)
+            self._run(self.ops, "fwd")
+        self._replay("fwd", body, [("img", self.img)] if self.img is not None else [])
 
     def backward(self):
-        self._backward_ops(self.ops)
+        self._replay("bwd", lambda: self._backward_ops(self.ops),
+                     [("dhead", self.dhead)] if self.dhead is not None else [])
 
     def _backward_ops(self, ops):
         for a in self.acts:
@@ -818,7 +886,7 @@ class Plan:
         self.grad_flat.zero_()
         for t in self._scratch:
             t.zero_()
-        hook = self.grad_hook
+        hook = None if self._graph_ok() else self.grad_hook
         self._begin_side()
         self._run(list(reversed(ops)), "bwd", (lambda op: hook(op_params(op))) if hook is not None else None)
         self._join_side()
@@ -1120,6 +1188,7 @@ def run_model(model, img: torch.Tensor):
     if plan is None:
         plan = Plan(model, B, H, W, img.device, model.training)
         plan.input_requires_grad = False
+        plan.is_model = True
         lower_model(plan, model, (B, H, W))
         cache[key] = plan
     if model.training:
