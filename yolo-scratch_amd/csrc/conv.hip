@@ -53,6 +53,7 @@ struct GemmArgs {
     int out_f32, accumulate;
     int N;                                   // images
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
+    int ntl;                                 // channel tiles interleaved into grid x (0: they are grid y)
 };
 
 // LDS images are lane-linear (LDS-DMA writes lane l of a wave-instruction at base + 16*l): 128-B
@@ -107,7 +108,17 @@ conv_gemm_kernel(GemmArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave / WN, wc = wave % WN;
     const int fc = lane >> 4, fr = lane & 15;
-    const int n0 = blockIdx.y * BN;
+    // block -> (grid-x slot bx, channel tile): with ntl > 0 the channel tiles of one m-tile sequence
+    // are adjacent launches on the same XCD (linear ids 8 apart), so the input rows one of them
+    // stages are still in that XCD's L2 when the others stage them; bx keeps the stats row layout
+    int bx = blockIdx.x, gxx = gridDim.x, nt = blockIdx.y;
+    if (a.ntl > 0) {
+        const int s = int(blockIdx.x) >> 3;
+        nt = s % a.ntl;
+        bx = (s / a.ntl) * 8 + (int(blockIdx.x) & 7);
+        gxx = gridDim.x / a.ntl;
+    }
+    const int n0 = nt * BN;
     const int kc = (a.Kin + BK - 1) / BK;
     // output pixel mapping: oh = i*os + py, ow = j*os + px over a class grid OHc x OWc;
     // for the stride-2 data gradient only the taps kh = kh0 + 2i, kw = kw0 + 2j reach whole pixels
@@ -144,10 +155,10 @@ conv_gemm_kernel(GemmArgs a) {
 
     // m-tiles grouped per XCD (workgroups go to XCDs round-robin by linear id; gridDim.x % 8 == 0):
     // neighbouring tiles share input halo rows in that XCD's L2
-    const int xcd = blockIdx.x & 7, lstride = gridDim.x >> 3;
+    const int xcd = bx & 7, lstride = gxx >> 3;
     const int per_xcd = (mtiles + 7) >> 3;
     const int mt_end = min((xcd + 1) * per_xcd, mtiles);
-    for (int mt = xcd * per_xcd + (blockIdx.x >> 3); mt < mt_end; mt += lstride) {
+    for (int mt = xcd * per_xcd + (bx >> 3); mt < mt_end; mt += lstride) {
         const int64_t m0 = int64_t(mt) * BM;
         const uint32_t nfirst = uint32_t(m0 / OHW);
         const __amdgpu_buffer_rsrc_t xres =
@@ -362,8 +373,8 @@ conv_gemm_kernel(GemmArgs a) {
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = pq;
+                a.st_sum[int64_t(bx) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(bx) * a.Nout + ch] = pq;
             }
         }
     }
@@ -687,7 +698,13 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
         const char* e = getenv("YM_CONV_ABLATE");
         return !e ? 0 : std::string(e) == "nomma" ? 1 : std::string(e) == "nodma" ? 2 : 0;
     }();
-    const dim3 grid(gx, ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
+    // YM_CONV_NMAP=0: channel tiles as grid y (dispatched one after another) instead of interleaved
+    static const int nmap = [] {
+        const char* e = getenv("YM_CONV_NMAP");
+        return !(e && e[0] == '0');
+    }();
+    a.ntl = nmap && ntiles > 1 ? ntiles : 0;
+    const dim3 grid(a.ntl ? gx * ntiles : gx, a.ntl ? 1 : ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
     if (abl == 1)
         hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, 1>), grid, block, 0, st, a);
     else if (abl == 2)
