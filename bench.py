@@ -112,12 +112,15 @@ def main():
     torch.manual_seed(0)
     model = build_yolo11(cfg, ch=1, nc=5).to(dev).train()
     crit = v8DetectionLoss(model, tal_topk=10)
-    # same AdamW math as the reference (train_yolo11_cuda.py:440-451); the fused single-kernel
-    # implementation where PyTorch offers it for this device
-    try:
+    # the reference's clip_grad_norm_(10) + AdamW(lr 1e-3, wd 5e-4) (train_yolo11_cuda.py:58-62,
+    # 440-451) as yolomi.optim.FusedAdamW: the same update in three HIP launches (YM_OPT=torch: PyTorch's
+    # fused AdamW + clip_grad_norm_, for A/B runs)
+    if os.environ.get("YM_OPT", "fused") == "torch":
         opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=5e-4, fused=True)
-    except (RuntimeError, TypeError):
-        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=5e-4)
+    else:
+        from yolomi.optim import FusedAdamW
+        opt = FusedAdamW(model.parameters(), lr=1e-3, weight_decay=5e-4, max_grad_norm=10.0)
+    fuses_clip = getattr(opt, "fuses_clip", False)
     dp = ydist.GradSync(model, ctx) if ctx else None
     if dp:
         dp.broadcast_state()
@@ -137,7 +140,8 @@ def main():
         loss.backward()
         if dp:
             dp.sync()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
+        if not fuses_clip:
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
         opt.step()
         return loss
 

@@ -280,6 +280,27 @@ int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc, int nl, co
  * (datasets/crater_dataset_cuda.py:182-184, 253). */
 int ym_resize_linear_u8(const uint8_t* src, const int64_t* meta, int batch, int size, float* out, void* stream);
 
+/* ------------------------------------------------------------------ optimizer tail
+ * clip_grad_norm_(params, max_norm) + AdamW.step() over every parameter (train_yolo11_cuda.py:58-62,
+ * 440-451).  The parameters form one flat index space: entry e covers elements [offset, offset + n)
+ * of its own fp32 param / grad / exp_avg / exp_avg_sq tensors (offsets ascending from 0). */
+typedef struct {
+    float* p;
+    const float* g;
+    float* m;                  /* exp_avg */
+    float* v;                  /* exp_avg_sq */
+    int64_t offset, n;
+} ym_adamw_entry;
+/* Blocks (= fp32 partials) of ym_grad_norm over `total` elements. */
+int ym_grad_norm_blocks(int64_t total);
+/* norm[0] = ||all grads||_2 (deterministic two-level sum; partials: ym_grad_norm_blocks floats). */
+int ym_grad_norm(const ym_adamw_entry* table_dev, int n_entries, int64_t total, float* partials, float* norm,
+                 void* stream);
+/* torch.optim.AdamW update (amsgrad=False, maximize=False) at step `step` (>= 1, already incremented)
+ * on g * min(1, max_norm / (norm[0] + 1e-6)); max_norm <= 0: no clipping (norm may be NULL). */
+int ym_adamw(const ym_adamw_entry* table_dev, int n_entries, int64_t total, double lr, double beta1, double beta2,
+             double eps, double weight_decay, int64_t step, float max_norm, const float* norm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -133,3 +133,19 @@ def test_reference_layout_checkpoint_resumes(tmp_path):
     for k, v in sd.items():
         assert torch.equal(m.state_dict()[k], v), k
     assert len(opt.state_dict()["state"]) == len(opt_ref.state_dict()["state"])
+
+
+def test_fused_adamw_refuses_cpu_parameters():
+    """The fused optimizer has no CPU path: CPU parameters raise instead of silently stepping,
+    and its state_dict layout is torch.optim.AdamW's (checkpoint interop)."""
+    import torch
+    from yolomi import YolomiError
+    from yolomi.optim import FusedAdamW
+    p = torch.nn.Parameter(torch.randn(4))
+    p.grad = torch.randn(4)
+    opt = FusedAdamW([p], lr=1e-3, weight_decay=5e-4, max_grad_norm=10.0)
+    import pytest
+    with pytest.raises(YolomiError):
+        opt.step()
+    ref = torch.optim.AdamW([torch.nn.Parameter(torch.randn(4))], lr=1e-3, weight_decay=5e-4)
+    assert set(opt.state_dict()["param_groups"][0]) == set(ref.state_dict()["param_groups"][0])

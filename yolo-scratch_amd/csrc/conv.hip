@@ -653,22 +653,32 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
 }
 
 // ------------------------------------------------------------------ weight preparation
-// fp32 OIHW master weights -> fp16 [Cout][KH][KW][Cin] (fwd) and bf16 [Cin][KH][KW][Cout] (dgrad)
+// fp32 OIHW master weights -> fp16 [Cout][KH][KW][Cin] (fwd, blockIdx.y 0) and bf16
+// [Cin][KH][KW][Cout_t] (dgrad, blockIdx.y 1).  A thread owns one DESTINATION element (coalesced
+// 2-B stores; the fp32 gathers hit L2), its table entry found by binary search over the offsets.
 __global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int n_entries, int64_t total) {
-    int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= total) return;
-    int e = 0;
-    while (e + 1 < n_entries && tab[e + 1].elem_offset <= i) ++e;
-    const ym_wprep_entry t = tab[e];
-    int64_t j = i - t.elem_offset;                 // index in OIHW
-    int T = t.kh * t.kw;
-    int tap = int(j % T);
-    int64_t r = j / T;
-    int ci = int(r % t.cin);
-    int co = int(r / t.cin);
-    const float v = t.src[j];
-    if (t.dst_fwd) t.dst_fwd[(int64_t(co) * T + tap) * t.cin + ci] = f2h(v);     // fp16 (forward operand)
-    if (t.dst_t) t.dst_t[(int64_t(ci) * T + tap) * t.cout_t + co] = f2bf(v);     // bf16 (dgrad operand)
+    int lo = 0, hi = n_entries - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[mid].elem_offset <= i) lo = mid;
+        else hi = mid - 1;
+    }
+    const ym_wprep_entry t = tab[lo];
+    const int j = int(i - t.elem_offset);
+    const int T = t.kh * t.kw;
+    if (blockIdx.y == 0) {
+        if (!t.dst_fwd) return;
+        const int ci = j % t.cin, r = j / t.cin;
+        const int tap = r % T, co = r / T;
+        t.dst_fwd[j] = f2h(t.src[(int64_t(co) * t.cin + ci) * T + tap]);
+    } else {
+        if (!t.dst_t) return;
+        const int co = j % t.cout, r = j / t.cout;
+        const int tap = r % T, ci = r / T;
+        t.dst_t[(int64_t(ci) * T + tap) * t.cout_t + co] = f2bf(t.src[(int64_t(co) * t.cin + ci) * T + tap]);
+    }
 }
 
 // grid x: a multiple of 8 (the kernel groups m-tiles per XCD); with BatchNorm statistics the
@@ -944,7 +954,7 @@ extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
 
 extern "C" int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream) {
     if (total_elems == 0) return YM_OK;
-    hipLaunchKernelGGL(prep_weights_kernel, dim3(unsigned((total_elems + 255) / 256)), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(prep_weights_kernel, dim3(unsigned((total_elems + 255) / 256), 2), dim3(256), 0, as_stream(stream),
                        table_dev, n_entries, total_elems);
     YM_LAUNCH_CHECK("ym_prep_weights");
     return YM_OK;

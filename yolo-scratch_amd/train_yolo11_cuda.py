@@ -57,7 +57,8 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, epoch, epoc
         loss.backward()
         if dp is not None:
             dp.sync()
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
+        if not getattr(optimizer, "fuses_clip", False):    # FusedAdamW clips on the device itself
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
         optimizer.step()
         sums[0] += loss.detach()
         sums[1:] += loss_items.detach()
@@ -239,11 +240,12 @@ def main():
         n_params = sum(p.numel() for p in model.parameters())
         print(f"Total parameters: {n_params:,} ({n_params / 1e6:.2f}M)")
     criterion = v8DetectionLoss(model, tal_topk=10)
-    # the reference's AdamW (:440-451); PyTorch's fused single-kernel form on the GPU
-    try:
-        optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay,
-                                      fused=device.type == "cuda")
-    except (RuntimeError, TypeError):
+    # the reference's AdamW (:440-451) + clip_grad_norm_(10) (:58-62): on the GPU as yolomi's
+    # FusedAdamW (a torch.optim.AdamW with the same state_dict; clipping fused into its step)
+    if device.type == "cuda":
+        from yolomi.optim import FusedAdamW
+        optimizer = FusedAdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay, max_grad_norm=10.0)
+    else:
         optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
     dp = ydist.GradSync(model, dp_ctx) if dp_ctx else None
     start_epoch, best_loss, best_mAP50 = 0, float("inf"), 0.0

@@ -27,6 +27,11 @@ class ConvDesc(ctypes.Structure):
                 ("y_ld", I64), ("out_f32", I32), ("accumulate", I32)]
 
 
+class AdamWEntry(ctypes.Structure):
+    """ym_adamw_entry (include/yolomi.h)."""
+    _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("offset", I64), ("n", I64)]
+
+
 class WPrepEntry(ctypes.Structure):
     """ym_wprep_entry (include/yolomi.h)."""
     _fields_ = [("src", P), ("dst_fwd", P), ("dst_t", P), ("elem_offset", I64), ("cout", I32), ("cin", I32),
@@ -89,6 +94,9 @@ SIGNATURES = {
     "ym_iou_matrix": (R, [P, P, I64, I64, P, P]),
     "ym_debug_nms_stamps": (R, [P]),
     "ym_resize_linear_u8": (R, [P, P, INT, INT, P, P]),
+    "ym_grad_norm_blocks": (R, [I64]),
+    "ym_grad_norm": (R, [P, INT, I64, P, P, P]),
+    "ym_adamw": (R, [P, INT, I64, F64, F64, F64, F64, F64, I64, F32, P, P]),
 }
 
 _LIB = None
