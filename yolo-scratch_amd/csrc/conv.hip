@@ -486,26 +486,39 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
         for (int t = 0; t < 9; ++t) acc[r][t] = 0.f;
     const int M = N * OH * OW, OHW = OH * OW;
     const int step = gridDim.x * (256 / G);
-    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
-        const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
-        const uint4 d = *reinterpret_cast<const uint4*>(dz + size_t(m) * Cout + g * 8);
-        const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
-        float gv[8];
+    // two pixels per iteration (loads of both first); accumulation order unchanged (m, m + step, ...)
+    for (int m0 = (blockIdx.x * 256 + threadIdx.x) / G; m0 < M; m0 += 2 * step) {
+        uint4 d[2];
+        float xv[2][9];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            gv[2 * e] = bf2f(bf16_t(dd[e] & 0xffff));
-            gv[2 * e + 1] = bf2f(bf16_t(dd[e] >> 16));
+        for (int u = 0; u < 2; ++u) {
+            const int m = m0 + u * step < M ? m0 + u * step : m0;
+            const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
+            d[u] = *reinterpret_cast<const uint4*>(dz + size_t(m) * Cout + g * 8);
+#pragma unroll
+            for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                for (int kw = 0; kw < 3; ++kw) {
+                    const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+                    xv[u][kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
+                                             ? img[(n * H + ih) * W + iw] : 0.f;
+                }
         }
 #pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
+        for (int u = 0; u < 2; ++u) {
+            if (m0 + u * step >= M) break;
+            const uint32_t dd[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+            float gv[8];
 #pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                const float xv = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
-                                     ? img[(n * H + ih) * W + iw] : 0.f;
-#pragma unroll
-                for (int r = 0; r < 8; ++r) acc[r][kh * 3 + kw] += gv[r] * xv;
+            for (int e = 0; e < 4; ++e) {
+                gv[2 * e] = bf2f(bf16_t(dd[e] & 0xffff));
+                gv[2 * e + 1] = bf2f(bf16_t(dd[e] >> 16));
             }
+#pragma unroll
+            for (int t = 0; t < 9; ++t)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) acc[r][t] += gv[r] * xv[u][t];
+        }
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r)

@@ -80,24 +80,32 @@ __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x))
 
 // ---------------------------------------------------------------- preprocess (:501-527)
 // gt_box[b][j] pixel xyxy (bbox * [ih, iw, ih, iw] as imgsz.repeat(2)), gt_lab, valid; stable per-image order
-__global__ void gt_prep_kernel(const int64_t* __restrict__ bidx, const int64_t* __restrict__ cls,
-                               const float* __restrict__ boxes, int64_t N, int B, int M, float ih, float iw,
-                               float4* __restrict__ gt_box, float* __restrict__ gt_lab, int* __restrict__ gt_valid) {
-    int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+// one wave per image: the targets are scanned 64 at a time, each image's rows keep the batch order
+// (ballot + prefix popcount), the first M of them are kept
+__global__ void __launch_bounds__(64) gt_prep_kernel(const int64_t* __restrict__ bidx, const int64_t* __restrict__ cls,
+                                                     const float* __restrict__ boxes, int64_t N, int B, int M, float ih,
+                                                     float iw, float4* __restrict__ gt_box, float* __restrict__ gt_lab,
+                                                     int* __restrict__ gt_valid) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const unsigned long long below = (1ull << lane) - 1ull;
     int j = 0;
-    for (int64_t t = 0; t < N && j < M; ++t) {
-        if (bidx[t] != b) continue;
-        const float* r = boxes + 4 * t;
-        gt_box[b * M + j] = make_float4(r[0] * ih, r[1] * iw, r[2] * ih, r[3] * iw);
-        gt_lab[b * M + j] = float(cls[t]);
-        gt_valid[b * M + j] = 1;
-        ++j;
+    for (int64_t t0 = 0; t0 < N && j < M; t0 += 64) {
+        const int64_t t = t0 + lane;
+        const bool mine = t < N && bidx[t] == b;
+        const unsigned long long mask = __ballot(mine);
+        const int slot = j + int(__popcll(mask & below));
+        if (mine && slot < M) {
+            const float* r = boxes + 4 * t;
+            gt_box[b * M + slot] = make_float4(r[0] * ih, r[1] * iw, r[2] * ih, r[3] * iw);
+            gt_lab[b * M + slot] = float(cls[t]);
+            gt_valid[b * M + slot] = 1;
+        }
+        j += int(__popcll(mask));
     }
-    for (; j < M; ++j) {
-        gt_box[b * M + j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        gt_lab[b * M + j] = 0.f;
-        gt_valid[b * M + j] = 0;
+    for (int s = min(j, M) + lane; s < M; s += 64) {
+        gt_box[b * M + s] = make_float4(0.f, 0.f, 0.f, 0.f);
+        gt_lab[b * M + s] = 0.f;
+        gt_valid[b * M + s] = 0;
     }
 }
 
@@ -128,7 +136,11 @@ __global__ void __launch_bounds__(256) assign_scan_kernel(const float* __restric
     for (int g = threadIdx.x; g < M; g += blockDim.x) { s_amax[g] = 0ull; s_cnt[g] = 0; }
     __syncthreads();
     const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (a < A) {
+    const bool live = a < A;
+    // every lane runs the gt loop (dead lanes with zero keys) so the per-gt argmax and in-box counts
+    // reduce over the wave first (shuffles / ballot) and take one LDS atomic per wave, not per lane
+    float px1 = 0.f, py1 = 0.f, px2 = 0.f, py2 = 0.f, cx = 0.f, cy = 0.f;
+    if (live) {
         const float* x = head + (int64_t(b) * A + a) * no;
         float ax, ay, s;
         anchor_of(L, a, ax, ay, s);
@@ -137,27 +149,37 @@ __global__ void __launch_bounds__(256) assign_scan_kernel(const float* __restric
         for (int k = 0; k < 4; ++k) d[k] = dfl_expect(x + k * REG, p);
         float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
         w.pbox[int64_t(b) * A + a] = make_float4(x1, y1, x2, y2);
-        float px1 = x1 * s, py1 = y1 * s, px2 = x2 * s, py2 = y2 * s;
-        float cx = ax * s, cy = ay * s;                  // anchor_points * stride_tensor
-        int cnt = 0, first = -1, gm = 0;
-        float best = -1.f;
-        for (int g = 0; g < M; ++g) {
-            float4 gb = gt_box[b * M + g];
-            float iou = iou_xyxy(px1, py1, px2, py2, gb.x, gb.y, gb.z, gb.w);
-            iou = iou < 0.f ? 0.f : iou;                 // .clamp_(0) (:199)
-            if (iou > best) { best = iou; gm = g; }
-            // select_candidates_in_gts (:210-224): min(l, t, r, b) > eps
-            float l = cx - gb.x, t = cy - gb.y, r = gb.z - cx, bo = gb.w - cy;
-            float mn = fminf(fminf(l, t), fminf(r, bo));
-            bool inb = mn > EPS_TAL;
-            if (inb && gt_valid[b * M + g]) {
-                ++cnt;
-                if (first < 0) first = g;
-                atomicAdd(&s_cnt[g], 1);
-            }
-            unsigned long long key = (uint64_t(__float_as_uint(iou)) << 32) | uint64_t(0xffffffffu - uint32_t(a));
-            atomicMax(&s_amax[g], key);
+        px1 = x1 * s; py1 = y1 * s; px2 = x2 * s; py2 = y2 * s;
+        cx = ax * s; cy = ay * s;                        // anchor_points * stride_tensor
+    }
+    int cnt = 0, first = -1, gm = 0;
+    float best = -1.f;
+    const int lane = threadIdx.x & 63;
+    for (int g = 0; g < M; ++g) {
+        const float4 gb = gt_box[b * M + g];
+        float iou = iou_xyxy(px1, py1, px2, py2, gb.x, gb.y, gb.z, gb.w);
+        iou = iou < 0.f ? 0.f : iou;                     // .clamp_(0) (:199)
+        if (iou > best) { best = iou; gm = g; }
+        // select_candidates_in_gts (:210-224): min(l, t, r, b) > eps
+        const float l = cx - gb.x, t = cy - gb.y, r = gb.z - cx, bo = gb.w - cy;
+        const float mn = fminf(fminf(l, t), fminf(r, bo));
+        const bool inb = live && mn > EPS_TAL && gt_valid[b * M + g];
+        if (inb) {
+            ++cnt;
+            if (first < 0) first = g;
         }
+        const unsigned long long pos = __ballot(inb);
+        if (lane == 0 && pos) atomicAdd(&s_cnt[g], int(__popcll(pos)));
+        // wave max of the packed (iou, ~a) key: the first anchor of the best IoU
+        uint32_t hi = live ? __float_as_uint(iou) : 0u, lo = live ? 0xffffffffu - uint32_t(a) : 0u;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint32_t h2 = __shfl_xor(hi, o, 64), l2 = __shfl_xor(lo, o, 64);
+            if (h2 > hi || (h2 == hi && l2 > lo)) { hi = h2; lo = l2; }
+        }
+        if (lane == 0) atomicMax(&s_amax[g], (uint64_t(hi) << 32) | uint64_t(lo));
+    }
+    if (live) {
         w.cnt0[int64_t(b) * A + a] = cnt;
         w.g0[int64_t(b) * A + a] = first;
         w.gmax[int64_t(b) * A + a] = gm;
@@ -569,7 +591,7 @@ extern "C" int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int 
     if (hipMemsetAsync(workspace, 0, zero_bytes(B, A, M), st) != hipSuccess) return YM_ERR_HIP;
     dim3 ga(unsigned((A + 255) / 256), unsigned(B));
     if (M > 0) {
-        hipLaunchKernelGGL(gt_prep_kernel, dim3(unsigned((B + 63) / 64)), dim3(64), 0, st, batch_idx, cls, bboxes,
+        hipLaunchKernelGGL(gt_prep_kernel, dim3(unsigned(B)), dim3(64), 0, st, batch_idx, cls, bboxes,
                            n_targets, int(B), M, imgsz_h, imgsz_w, reinterpret_cast<float4*>(gt_box), gt_lab, gt_valid);
         hipLaunchKernelGGL(assign_scan_kernel, ga, dim3(256), size_t(M) * 12, st, head, A, no, nc, L,
                            reinterpret_cast<const float4*>(gt_box), gt_valid, M, w);
