@@ -97,6 +97,7 @@ def main():
     from models import build_yolo11
     from losses import v8DetectionLoss
     from datasets.synthetic import synth_batch
+    from datasets import prepare_batch
     import yaml
 
     ctx = ydist.init_from_env()
@@ -130,7 +131,10 @@ def main():
     batches = []
     for i in range(n_batches):
         b = synth_batch(args.batch, args.imgsz, seed=1000 * rank + i)
-        batches.append({k: v.to(dev) for k, v in b.items()})
+        b = prepare_batch(b, dev)                  # the data path's H2D (records max_gt on the host)
+        if os.environ.get("YM_LOSS_SYNC") == "1":      # A/B: the loss counts M with a device sync
+            b.pop("max_gt", None)
+        batches.append(b)
 
     def step(i):
         b = batches[i % n_batches]

@@ -63,3 +63,15 @@ def test_resize_restatement_sanity():
     blocks = a.reshape(32, 2, 32, 2).astype(np.int64)
     r = resize_linear_u8(a, 32).astype(np.int64)
     assert np.abs(r - blocks.mean((1, 3))).max() <= 1
+
+
+def test_prepare_batch_records_max_gt_on_host():
+    """prepare_batch counts the max GTs per image on the host (the loss then needs no device sync)."""
+    import torch
+    from datasets import max_gt_count, prepare_batch
+    from datasets.synthetic import synth_batch
+    b = synth_batch(6, 64, seed=5)
+    want = int(torch.bincount(b["batch_idx"].long(), minlength=6).max())
+    out = prepare_batch(b, "cpu")
+    assert out["max_gt"] == want == max_gt_count(b["batch_idx"])
+    assert max_gt_count(torch.zeros(0)) == 0

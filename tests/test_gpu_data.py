@@ -40,7 +40,8 @@ def test_dataset_to_device_batch(tmp_path):
     seen = 0
     for b in dl:
         d = prepare_batch(b, torch.device("cuda"))
-        assert set(d) == {"img", "batch_idx", "cls", "bboxes"}
+        assert set(d) == {"img", "batch_idx", "cls", "bboxes", "max_gt"}
+        assert d["max_gt"] == int(torch.bincount(d["batch_idx"].long().cpu()).max()) if len(d["batch_idx"]) else 0
         assert d["img"].shape == (len(d["img"]), 1, 640, 640) and d["img"].dtype == torch.float32
         for j in range(d["img"].shape[0]):
             path, anns = ref[seen + j]

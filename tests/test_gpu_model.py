@@ -303,3 +303,32 @@ def test_network_backward_fixed_head_grads_vs_oracle():
         worst.append((err / bound, k, err, err_emu))
         assert err < bound, (k, err, err_emu)
     print("worst err/bound", sorted(worst)[-3:])
+
+
+def test_loss_with_host_max_gt_matches_synced_count():
+    """The loss sized by the data path's host-side max_gt equals the one that syncs to count it."""
+    from oracle import model as om
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets import prepare_batch
+    from datasets.synthetic import synth_batch
+    cfg = om.load_cfg("n")
+    _, _, P = om.build(cfg)
+    m = build_yolo11(cfg, ch=1, nc=5)
+    m.load_state_dict(P)
+    m = m.cuda().train()
+    crit = v8DetectionLoss(m)
+    raw = synth_batch(3, 256, seed=8)
+    b1 = prepare_batch(raw, "cuda")
+    assert "max_gt" in b1
+    b0 = {k: v for k, v in b1.items() if k != "max_gt"}
+    heads = [h.detach().clone().requires_grad_(True) for h in m(b1["img"])]
+    outs = []
+    for b in (b0, b1):
+        hs = [h.detach().clone().requires_grad_(True) for h in heads]
+        loss, items = crit(hs, b)
+        loss.backward()
+        outs.append((loss.detach(), items, [h.grad for h in hs]))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for a, c in zip(outs[0][2], outs[1][2]):
+        assert torch.equal(a, c)

@@ -5,7 +5,7 @@ CraterDatasetCUDA mirrors /root/reference/yolo_scratch_cuda/datasets/crater_data
 :289-346; prepare_batch is the device transfer of train_yolo11_cuda.py:43-45.
 """
 from .collate import collate_fn_cuda  # noqa: F401
-from .crater import CraterDatasetCUDA, prepare_batch, resize_batch  # noqa: F401
+from .crater import CraterDatasetCUDA, max_gt_count, prepare_batch, resize_batch  # noqa: F401
 
 collate_fn = collate_fn_cuda
 CraterDatasetYOLO = CraterDatasetCUDA

@@ -139,10 +139,22 @@ def resize_batch(img_u8: torch.Tensor, meta: torch.Tensor, img_size: int) -> tor
     return out
 
 
+def max_gt_count(batch_idx: torch.Tensor, batch_size: int | None = None) -> int:
+    """max over images of the number of GT rows (0 for an empty batch), on a host tensor."""
+    if batch_idx.numel() == 0:
+        return 0
+    return int(torch.bincount(batch_idx.long().reshape(-1), minlength=batch_size or 0).max())
+
+
 def prepare_batch(batch: dict, device) -> dict:
     """Device transfer of a collated batch (train_yolo11_cuda.py:43-45), running the GPU resize when
     the batch carries raw images.  Tensors are copied non_blocking from pinned memory."""
     out = {}
+    bidx = batch.get("batch_idx")
+    if isinstance(bidx, torch.Tensor) and not bidx.is_cuda and "max_gt" not in batch:
+        # the loss sizes its assigner by the max GT count per image: counted here on the host, it
+        # spares the training step its mid-step device sync (losses/yolo_v8_loss.py)
+        out["max_gt"] = max_gt_count(bidx)
     for k, v in batch.items():
         out[k] = v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v
     if "img_u8" in out:

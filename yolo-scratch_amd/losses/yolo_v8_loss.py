@@ -135,7 +135,12 @@ class _LossFn(torch.autograd.Function):
         cls = batch["cls"].to(dev, torch.int64).reshape(-1).contiguous()
         boxes = batch["bboxes"].to(dev, torch.float32).reshape(-1, 4).contiguous()
         n = int(boxes.shape[0])
-        M = int(torch.bincount(bidx, minlength=B).max().item()) if n else 0     # the one host sync
+        # M = max GTs per image (sizes the assigner): from the batch's host-side "max_gt" when the data
+        # path recorded it before the H2D copy (datasets.prepare_batch), else the one host sync
+        M = batch.get("max_gt")
+        if M is None:
+            M = int(torch.bincount(bidx, minlength=B).max().item()) if n else 0
+        M = int(M) if n else 0
         key = (B, A, M)
         lc = crit._ctx.get(key)
         if lc is None:
