@@ -424,6 +424,22 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
 
 constexpr int RED_R = 32;   // level-1 row splits of the partials reduction
 
+// grid caps of the streaming kernels (measured in the training step: 2048 / 512 with the conv
+// forward's 1024 stat rows, +0.3 % over 4096 / 1024 / 2048); YM_BN_APPLY_BLOCKS /
+// YM_BN_REDUCE_BLOCKS override them (A/B runs)
+int env_cap(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? std::max(8, atoi(e)) : dflt;
+}
+int apply_cap() {
+    static const int v = env_cap("YM_BN_APPLY_BLOCKS", 2048);
+    return v;
+}
+int reduce_cap() {
+    static const int v = env_cap("YM_BN_REDUCE_BLOCKS", 512);
+    return v;
+}
+
 int stream_blocks(int64_t M, int C, int cap) {
     int rows = 256 / (C / 8);
     int64_t g = (M + rows - 1) / rows;
@@ -491,13 +507,13 @@ extern "C" int ym_bn_apply(const uint16_t* z, int64_t m, int c, int hw, const fl
     CHECK_VIEW(o_bs, o_ld, hw);
     if (res) CHECK_VIEW(r_bs, r_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(m, c, 4096)), dim3(256), 0, as_stream(stream), z, m, c,
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0, as_stream(stream), z, m, c,
                        scale, shift, act, res, r_ld, out, o_ld, out32);
     YM_LAUNCH_CHECK("ym_bn_apply");
     return YM_OK;
 }
 
-extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, 1024); }
+extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, reduce_cap()); }
 
 extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
                                 int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
@@ -540,7 +556,7 @@ extern "C" int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, c
     CHECK_C(c);
     CHECK_VIEW(d_bs, d_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(m, c, 4096)), dim3(256), 0, as_stream(stream), dy, d_ld,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0, as_stream(stream), dy, d_ld,
                        z, m, c, scale, shift, mean, rstd, act, coef, dz);
     YM_LAUNCH_CHECK("ym_bn_bwd_apply");
     return YM_OK;

@@ -696,6 +696,15 @@ __global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int 
 
 // grid x: a multiple of 8 (the kernel groups m-tiles per XCD); with BatchNorm statistics the
 // partials are one row per grid-x block, so the grid is bounded and blocks loop over tiles
+// grid-x bound of the forward with BN statistics (rows of its partials); YM_CONV_FWD_BLOCKS overrides
+static int fwd_stat_blocks() {
+    static const int v = [] {
+        const char* e = getenv("YM_CONV_FWD_BLOCKS");
+        return e ? std::max(64, atoi(e)) : 1024;
+    }();
+    return v;
+}
+
 static int grid_x(int mtiles, int ntiles, bool stats, int max_blocks) {
     int gx = (mtiles + 7) & ~7;
     if (stats) gx = std::min(gx, std::max(8, (max_blocks / ntiles) & ~7));
@@ -802,7 +811,7 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     // grid-x used for the stats partials by ym_conv_fwd (callers size the partial buffers with it)
     const Tile t = pick_tile(M, 1, Cout);
     const int mtiles = int((M + t.bm - 1) / t.bm);
-    return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, 2048);
+    return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, fwd_stat_blocks());
 }
 
 extern "C" int ym_conv_set_halo(int mode) {
@@ -855,7 +864,7 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
-    pick_and_launch(a, MODE_FWD, 2048, as_stream(stream));
+    pick_and_launch(a, MODE_FWD, fwd_stat_blocks(), as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
 }
