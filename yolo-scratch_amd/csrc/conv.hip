@@ -781,16 +781,17 @@ static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t 
     return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
 }
 
-// K-stage depth x ring depth; YM_CONV_CFG=32x4 / 32x3 / 64x3 selects the alternatives (A/B runs)
+// K-stage depth x ring depth; YM_CONV_CFG=32x4 / 32x3 / 64x3 / 32x2 selects the alternatives (A/B runs)
 template <int MODE>
 static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
     static const int cfg = [] {
         const char* e = getenv("YM_CONV_CFG");
         if (!e) return 0;
         const std::string v(e);
-        return v == "32x4" ? 1 : v == "32x3" ? 2 : v == "64x3" ? 3 : 0;
+        return v == "32x4" ? 1 : v == "32x3" ? 2 : v == "64x3" ? 3 : v == "32x2" ? 4 : 0;
     }();
     switch (cfg) {
+        case 4: return launch_tile_k<32, 2, MODE>(a, t, max_blocks, st);
         case 1: return launch_tile_k<32, 4, MODE>(a, t, max_blocks, st);
         case 2: return launch_tile_k<32, 3, MODE>(a, t, max_blocks, st);
         case 3: return launch_tile_k<64, 3, MODE>(a, t, max_blocks, st);
