@@ -447,7 +447,13 @@ WgPlan wg_plan(const ym_conv_desc* d) {
         p.units = int64_t(d->n) * ((d->oh + 7) / 8) * ((d->ow + 7) / 8);
     } else if (d->k == 1 && d->stride == 1 && d->pad == 0 && whole) {
         p.kind = 1;
-        p.T = (d->cout >= 128 && d->cin >= 128) ? 128 : 64;
+        // 128-wide tiles once both channel counts reach t128 (YM_WGRAD1_T128, default 128): fewer
+        // tiles re-read dz and x fewer times, at the cost of padding a channel count below 128
+        static const int t128 = [] {
+            const char* e = getenv("YM_WGRAD1_T128");
+            return e ? atoi(e) : 128;
+        }();
+        p.T = (d->cout >= t128 && d->cin >= t128) ? 128 : 64;
         p.units = (M + 63) / 64;
     } else {
         p.kind = 0;
