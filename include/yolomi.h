@@ -208,6 +208,13 @@ int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, 
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                     const float* coef, uint16_t* dz, void* stream);
+/* ym_bn_bwd_apply that also writes the residual branch's gradient from the same dy read:
+ * dres (+)= dy into the bf16 view (r_bs, r_ld) — the shortcut of Bottleneck (yolo11_modules.py:47)
+ * and Attention.pe (:134); replaces a separate ym_view_axpy pass. */
+int ym_bn_bwd_apply_res(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
+                        const float* scale, const float* shift, const float* mean, const float* rstd, int act,
+                        const float* coef, uint16_t* dz, uint16_t* dres, int64_t r_bs, int64_t r_ld,
+                        int r_accumulate, void* stream);
 
 /* ------------------------------------------------------------------ graph ops
  * SPPF max-pool (yolo11_modules.py:92-105), nearest 2x upsample (yaml head rows 11, 14),

@@ -376,13 +376,17 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
 }
 
 // dz[m][c] = k1*(g - k2 - xhat*k3), dz dense [M][C] (may alias z)
+// RES: also the residual branch's gradient, dres (+)= dy (the Bottleneck / Attention.pe shortcut),
+// from the dy this kernel reads anyway (replaces a ym_view_axpy pass)
+template <bool RES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restrict__ dy, int64_t d_ld,
                                                            const bf16_t* z, int64_t M, int C,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, int act,
-                                                           const float* __restrict__ coef, bf16_t* dz) {
+                                                           const float* __restrict__ coef, bf16_t* dz,
+                                                           bf16_t* __restrict__ dres, int64_t r_ld, int r_acc) {
     const Lanes L = lanes(C);
     if (!L.on) return;
     const int c0 = L.g * 8;
@@ -418,6 +422,18 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                 o[k] = k1[k] * (gg - k2[k] - xh * k3[k]);
             }
             *reinterpret_cast<uint4*>(dz + (u ? m2 : m) * C + c0) = pack8(o);
+            if constexpr (RES) {
+                uint4* rp = reinterpret_cast<uint4*>(dres + (u ? m2 : m) * r_ld + c0);
+                if (r_acc) {
+                    float rv[8];
+                    unpack8(*rp, rv);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) rv[k] += dv[k];
+                    *rp = pack8(rv);
+                } else {
+                    *rp = dr[u];
+                }
+            }
         }
     }
 }
@@ -556,8 +572,24 @@ extern "C" int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, c
     CHECK_C(c);
     CHECK_VIEW(d_bs, d_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0, as_stream(stream), dy, d_ld,
-                       z, m, c, scale, shift, mean, rstd, act, coef, dz);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0,
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, coef, dz, nullptr, 0, 0);
     YM_LAUNCH_CHECK("ym_bn_bwd_apply");
+    return YM_OK;
+}
+
+extern "C" int ym_bn_bwd_apply_res(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m,
+                                   int c, int hw, const float* scale, const float* shift, const float* mean,
+                                   const float* rstd, int act, const float* coef, uint16_t* dz, uint16_t* dres,
+                                   int64_t r_bs, int64_t r_ld, int r_accumulate, void* stream) {
+    CHECK_C(c);
+    CHECK_VIEW(d_bs, d_ld, hw);
+    CHECK_VIEW(r_bs, r_ld, hw);
+    YM_CHECK_ARG(dres, "ym_bn_bwd_apply_res: null residual gradient");
+    if (m == 0) return YM_OK;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0,
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, coef, dz, dres, r_ld,
+                       r_accumulate);
+    YM_LAUNCH_CHECK("ym_bn_bwd_apply_res");
     return YM_OK;
 }

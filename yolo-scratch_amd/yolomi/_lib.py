@@ -70,6 +70,7 @@ SIGNATURES = {
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
+    "ym_bn_bwd_apply_res": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, I64, I64, INT, P]),
     "ym_maxpool5_f32_fwd": (R, [P, P, P, P, I64, I64, INT, INT, INT, INT, P]),
     "ym_maxpool5_f32_bwd": (R, [P, P, P, I64, I64, P, P, I64, I64, INT, INT, INT, INT, INT, P]),
     "ym_upsample2_fwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, P]),

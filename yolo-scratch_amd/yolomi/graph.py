@@ -252,13 +252,16 @@ class ConvBN:
         call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
              _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
         dz = self.z  # reuse the z buffer? no: z is needed by nobody after this op -> in-place dz
-        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
-             self.act, self.coef.data_ptr(), dz.data_ptr(), st)
         if self.res is not None:
+            # the shortcut's gradient (dres (+)= dy) comes out of the same pass over dy
             acc = self.res.grad_for_write(st)
-            call("ym_view_axpy", dy, self.y.bs, self.y.ld, self.res.gptr(), self.res.bs, self.res.ld, self.M, self.co,
-                 self.HW, acc, 0, st)
+            call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                 mu, rs, self.act, self.coef.data_ptr(), dz.data_ptr(), self.res.gptr(), self.res.bs, self.res.ld,
+                 acc, st)
             self.res.mark()
+        else:
+            call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu,
+                 rs, self.act, self.coef.data_ptr(), dz.data_ptr(), st)
         # weight gradient: on the side stream, beside this layer's data gradient and the next BN backward
         ws = plan.wgrad_ws()
         call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
@@ -374,11 +377,9 @@ class DWConvBN(ConvBN):
              0, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
         call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.C, float(self.M),
              _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
-             0, self.coef.data_ptr(), self.z.data_ptr(), st)
         acc = self.res.grad_for_write(st)
-        call("ym_view_axpy", dy, self.y.bs, self.y.ld, self.res.gptr(), self.res.bs, self.res.ld, self.M, self.C,
-             self.HW, acc, 0, st)
+        call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu,
+             rs, 0, self.coef.data_ptr(), self.z.data_ptr(), self.res.gptr(), self.res.bs, self.res.ld, acc, st)
         self.res.mark()
         # dx into the v channels of dqkv (accumulate if the attention core wrote them already)
         hd, hs, goff = self.map
