@@ -817,9 +817,10 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
 
 extern "C" int ym_conv_set_halo(int mode) {
     // selection policy of the halo-staged 3x3 kernel: -1 env/default, 0 never, 1 wherever it applies,
-    // 2 where it measured faster (the default); returns the previous setting
+    // 2 where it measured faster in the step (the default), 3 the wider per-layer rule; returns the
+    // previous setting
     const int prev = g_halo_force;
-    g_halo_force = mode < -1 || mode > 2 ? -1 : mode;
+    g_halo_force = mode < -1 || mode > 3 ? -1 : mode;
     return prev;
 }
 

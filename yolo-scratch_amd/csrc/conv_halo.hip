@@ -45,7 +45,13 @@ struct HaloArgs {
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
 };
 
-__device__ __forceinline__ int fsw64(int r) { return (0x1E4 >> (((r >> 2) & 3) * 2)) & 3; }   // F = {0,3,2,1}
+// 64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1).
+// A ds_read_b128 lane group reads 16 rows s + fr at chunks c (fr in {0-3, 12-15}) and c ^ 1
+// (fr in {4-11}) (or the reverse); rows s+k, s+k+4, s+k+8, s+k+12 share bank quads and land on
+// chunks {c, c^3, c^1, c^2} for EVERY start s — the halo fragments start at arbitrary rows (tap
+// shifts, tile rows), where the earlier F = {0,3,2,1}[(r>>2)&3] conflicted 1.8-2.4x
+// (bank-conflict model over the kernel's fragment rows: 7.3-9.4 LDS cycles per read -> 4.0-6.4).
+__device__ __forceinline__ int fsw64(int r) { return ((r >> 2) & 1) << 1; }
 
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -367,15 +373,19 @@ int g_halo_force = -1;
 
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
     HaloPlan p{};
-    // YM_CONV_HALO=0: never, =1: wherever it applies, unset: where it measured faster than the
-    // implicit GEMM (maps <= 24 wide: the 20x20 layers; 40x40 and 80x80 maps are 2-20 % slower)
+    // YM_CONV_HALO=0: never, =1: wherever it applies, unset (2): maps <= 24 wide (the 20x20 layers).
+    // With the conflict-free swizzle the halo kernel also wins most 40x40 layers and the <= 64-channel
+    // 80x80 ones in isolation (tools/layer_bench.py: -2..-25 %), but selecting it there measured
+    // 0.5 % slower on the whole step (=3: that wider rule, for A/B runs)
     static const int mode = [] {
         const char* e = getenv("YM_CONV_HALO");
-        return !e ? 2 : (e[0] == '0' ? 0 : 1);
+        return !e ? 2 : (e[0] == '0' ? 0 : e[0] == '3' ? 3 : 1);
     }();
     const int force = g_halo_force >= 0 ? g_halo_force : mode;
     if (force == 0) return p;
-    if (force == 2 && (dgrad ? d->w : d->ow) > 24) return p;
+    const int ow_ = dgrad ? d->w : d->ow, cout_ = dgrad ? d->cin : d->cout;
+    if (force == 2 && ow_ > 24) return p;
+    if (force == 3 && ow_ > 48 && cout_ > 64) return p;
     // 3x3, stride 1, pad 1, channels in whole 16-B chunks
     const int cin = dgrad ? d->cout : d->cin, cout = dgrad ? d->cin : d->cout;
     const int GH = dgrad ? d->oh : d->h, GW = dgrad ? d->ow : d->w;
