@@ -35,7 +35,6 @@
 namespace ym {
 namespace {
 
-
 constexpr int MODE_FWD = 0;
 constexpr int MODE_DGRAD = 1;
 
@@ -61,12 +60,13 @@ struct GemmArgs {
 // lives on the global (source) side: a DMA lane that fills slot s of row r loads chunk s ^ f(r), so
 // each 8-lane group still reads one whole 128-B row.  A ds_read_b128 lane group (rows {0-3,12-15}
 // at chunk c, rows {4-11} at chunk c^1) then covers 16 distinct (row parity, slot) bank quads.
-// 64-B rows (32-deep K stages, 4 slots): slot c ^ F[(r >> 2) & 3], F = {0, 3, 2, 1} — for each
-// row residue mod 4 a read group's four rows then land on four distinct slots.
+// 64-B rows (32-deep K stages, 4 slots): slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1) — measured
+// conflict-free (SQ_LDS_BANK_CONFLICT 0; the earlier F = {0, 3, 2, 1}[(r >> 2) & 3] cost 45-50 %
+// extra LDS cycles in the 128x64 tiles, tools/pmc_conv.sh).
 template <int RB>
 __device__ __forceinline__ int fsw(int r) {
     if constexpr (RB == 128) return (r >> 1) & 7;
-    else return (0x1E4 >> (((r >> 2) & 3) * 2)) & 3;   // F = {0, 3, 2, 1}
+    else return ((r >> 2) & 1) << 1;                    // F(r) = 2 * ((r >> 2) & 1)
 }
 
 template <int N>
