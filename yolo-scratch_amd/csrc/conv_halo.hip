@@ -13,7 +13,7 @@
 // K loop: steps k = (32-channel chunk cc, kernel row kh), each step = the row's 3 taps.  LDS: two halo images (chunk cc and cc+1) and an
 // NW-deep ring of weight slices, all filled by LDS-DMA (buffer_load ... lds) with source-side
 // swizzle, counted vmcnt waits (the halo of the next chunk and NW-2 weight slices stay in flight)
-// and raw barriers.  64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F[(r>>2)&3].
+// and raw barriers.  64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r) (fsw64 below).
 // Pixels of a fragment map to halo rows through a per-lane base (row-major tile, any TW), so tile
 // rectangles need not be powers of two (40x40 maps use 40 x 6 tiles); pixels past the map edge are
 // computed on zero-padded halo rows and masked in the epilogue.
