@@ -753,6 +753,7 @@ using namespace ym;
 
 struct Tile {
     int bm, bn;
+    int deep = 0;    // 256x128 on 4 waves of 64 channels x 128 pixels (YM_CONV_TILE=2564)
 };
 
 // Large problems: 256 x 128 tiles on 8 waves (a quarter fewer operand bytes per FLOP than 128x128,
@@ -763,9 +764,12 @@ struct Tile {
 static Tile pick_tile(int64_t Mc, int classes, int nout) {
     static const int use256 = [] {
         const char* e = getenv("YM_CONV_TILE");
-        return e && atoi(e) == 256;
+        return e ? atoi(e) : 0;
     }();
-    if (nout >= 128 && use256 && ((Mc + 255) / 256) * classes * ((nout + 127) / 128) >= 512) return {256, 128};
+    // YM_CONV_TILE=256: 8 waves of 64x64; YM_CONV_TILE=2564: 4 waves of 64 channels x 128 pixels
+    // (32-deep stages, 3-stage ring, 72 KB: two workgroups per CU)
+    if (nout >= 128 && use256 && ((Mc + 255) / 256) * classes * ((nout + 127) / 128) >= 512)
+        return {256, 128, use256 == 2564};
     const int64_t blocks_per_ntile = ((Mc + 127) / 128) * classes;
     int bn = nout >= 128 ? 128 : (nout >= 64 ? 64 : 32);
     while (bn > 32 && blocks_per_ntile * ((nout + bn - 1) / bn) < 384) bn >>= 1;
@@ -774,6 +778,7 @@ static Tile pick_tile(int64_t Mc, int classes, int nout) {
 
 template <int KB, int NS, int MODE>
 static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
+    if (t.bm == 256 && t.deep) return launch_gemm<256, 128, 2, 2, 32, 3, MODE>(a, max_blocks, st);
     if (t.bm == 256) return launch_gemm<256, 128, 2, 4, KB, NS, MODE>(a, max_blocks, st);
     if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
     if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
