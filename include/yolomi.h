@@ -11,7 +11,11 @@
  * Conventions
  *  - All pointers are DEVICE pointers unless stated; buffers are allocated by
  *    the caller (PyTorch caching allocator); the library never allocates or
- *    frees caller memory and keeps no state between calls.
+ *    frees caller memory and keeps no TENSOR state between calls.  The only
+ *    process-wide state is configuration and diagnostics: the halo-kernel
+ *    selection policy (ym_conv_set_halo / YM_CONV_HALO, read once) and the
+ *    NMS segment counters (ym_debug_nms_stamps, written when YM_NMS_STAMPS is
+ *    set); neither changes a result.
  *  - `stream` is a hipStream_t (0 = legacy default stream); every call is
  *    asynchronous on it and performs no device-wide synchronisation.
  *  - Activations are NHWC.  An "activation view" is (base pointer, batch
@@ -250,6 +254,11 @@ int ym_attn_bwd(const uint16_t* qkv, int64_t q_bs, int64_t q_ld, const uint16_t*
                 const uint16_t* dout, int64_t d_bs, int64_t d_ld, const float* lse, int b, int heads, int n,
                 float scale, float* workspace, uint16_t* dqkv, int64_t g_bs, int64_t g_ld, int acc_q, int acc_k,
                 int acc_v, void* stream);
+/* Concat.forward (models/yolo11_modules.py:284-285) of contiguous tensors along one dimension, and
+ * its backward: `rows` runs of `width_bytes`, source pitch `src_pitch`, destination pitch `dst_pitch`
+ * (bytes).  A device-to-device strided copy on the stream. */
+int ym_copy2d(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t width_bytes, int64_t rows,
+              void* stream);
 /* dst_view = src_view (+ dst_view when accumulate); src NULL zero-fills dst */
 int ym_view_axpy(const uint16_t* x, int64_t x_bs, int64_t x_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int64_t m,
                  int c, int hw, int accumulate, int half, void* stream);   /* half: 1 fp16 data, 0 bf16 */
@@ -276,6 +285,29 @@ int ym_loss_bwd(const float* head, int64_t B, int64_t A, int nc, int nl, const i
 /* Device pointers to the assignment (target_gt_idx, fg_mask, target-score magnitude) in the workspace. */
 int ym_loss_assignment(void* workspace, int64_t B, int64_t A, int M, const int** tgi, const int** fg,
                        const float** norm);
+/* TaskAlignedAssigner.forward (losses/yolo_v8_loss.py:78-180) on explicit tensors, for M >= 1 (the
+ * M = 0 early return :100-108 is the caller's): pd_scores (B,A,nc) probabilities, pd_bboxes (B,A,4)
+ * pixel xyxy, anc_points (A,2) pixels, gt_labels (B,M) float, gt_bboxes (B,M,4) (16-B aligned),
+ * mask_gt (B,M) float.  Outputs: target_labels (B,A) float, target_bboxes (B,A,4), target_scores
+ * (B,A,nc), fg_mask (B,A) uint8, target_gt_idx (B,A) int64 — the reference's 5-tuple.  Same kernels
+ * (and quirks Q1-Q3) as ym_loss_fwd's fused assignment. */
+size_t ym_tal_assign_workspace_size(int64_t B, int64_t A, int M);
+int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, const float* anc_points, const float* gt_labels,
+                  const float* gt_bboxes, const float* mask_gt, int64_t B, int64_t A, int nc, int M, void* workspace,
+                  size_t workspace_bytes, float* target_labels, float* target_bboxes, float* target_scores,
+                  uint8_t* fg_mask, int64_t* target_gt_idx, void* stream);
+/* BboxLoss.forward (losses/yolo_v8_loss.py:280-324): pred_dist (B,A,64), pred_bboxes / target_bboxes
+ * (B,A,4) grid units, anchor_points (A,2), target_scores (B,A,nc), tss device scalar (target_scores_sum),
+ * fg_mask (B,A) uint8.  out[0] = loss_iou, out[1] = loss_dfl.  The backward writes
+ * d(grad_out[0] * loss_iou + grad_out[1] * loss_dfl) / d pred_dist, d pred_bboxes (zero off foreground). */
+size_t ym_bbox_loss_workspace_size(int64_t B, int64_t A);
+int ym_bbox_loss_fwd(const float* pred_dist, const float* pred_bboxes, const float* anchor_points,
+                     const float* target_bboxes, const float* target_scores, const float* tss, const uint8_t* fg_mask,
+                     int64_t B, int64_t A, int nc, void* workspace, size_t workspace_bytes, float* out, void* stream);
+int ym_bbox_loss_bwd(const float* pred_dist, const float* pred_bboxes, const float* anchor_points,
+                     const float* target_bboxes, const float* target_scores, const float* tss, const uint8_t* fg_mask,
+                     int64_t B, int64_t A, int nc, const float* grad_out, float* dpred_dist, float* dpred_bboxes,
+                     void* stream);
 /* y (B, 4+nc, A): xywh * stride from the DFL projection with weights dfl_w[16], sigmoid(cls). */
 int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h,
                      const int* level_w, const float* strides, const float* dfl_w, float* y, void* stream);

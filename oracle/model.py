@@ -293,6 +293,18 @@ def build(cfg: dict, ch: int = 1, nc: int = 5, seeded: bool = True):
     return layers, save, P
 
 
+def block_params(layer: dict, prefix: str = "blk", seeded: bool = True) -> dict:
+    """Parameters of ONE building block (layer dict as parse() makes it, e.g. {"type": "C2PSA",
+    "c1": 512, "c2": 512, "n": 1}) under `prefix.`, key-seeded as the standalone module's
+    state_dict would be (oracle/weights.py)."""
+    from .weights import apply_seeded_weights
+    P = init_params([{**layer, "i": 0}])
+    P = {prefix + k[len("model.0"):]: v for k, v in P.items()}
+    if seeded:
+        apply_seeded_weights(P, prefix + ".")
+    return P
+
+
 def load_cfg(scale: str) -> dict:
     import yaml
     from pathlib import Path

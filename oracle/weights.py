@@ -28,9 +28,11 @@ def seeded_tensor(key: str, shape) -> torch.Tensor:
     return torch.randn(tuple(shape), generator=g, dtype=torch.float32) * math.sqrt(2.0 / fan_out)
 
 
-def apply_seeded_weights(state: dict) -> dict:
-    """In-place: overwrite every 4-D '*.weight' entry of a state_dict."""
+def apply_seeded_weights(state: dict, prefix: str = "") -> dict:
+    """In-place: overwrite every 4-D '*.weight' entry of a state_dict.  Keys are seeded without
+    `prefix`, so a block's parameters held under 'blk.' in the oracle draw the same values as the
+    standalone module's state_dict (keys 'cv1.conv.weight', ...)."""
     for k, v in state.items():
         if k.endswith(".weight") and v.dim() == 4:
-            v.copy_(seeded_tensor(k, v.shape))
+            v.copy_(seeded_tensor(k[len(prefix):] if k.startswith(prefix) else k, v.shape))
     return state

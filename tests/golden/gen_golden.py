@@ -41,6 +41,7 @@ from losses.yolo_v8_loss import v8DetectionLoss  # noqa: E402
 from models.yolo11_model import build_yolo11  # noqa: E402
 from utils.metrics import evaluate_detections  # noqa: E402
 import models.yolo11_modules as ref_mods  # noqa: E402
+import losses.yolo_v8_loss as ref_loss_mod  # noqa: E402
 import yaml  # noqa: E402
 
 
@@ -233,6 +234,103 @@ def gen_s_small():
     save("model_s128.npz", **arrs)
 
 
+def gen_m_small():
+    """m-scale graph (1024-channel layers, C2PSA heads=8) pinned at 256x256 bs1."""
+    m = build("m")
+    m.train()
+    batch = synth.synth_batch(1, 256, seed=9)
+    preds = m(batch["img"])
+    crit = v8DetectionLoss(m, tal_topk=10)
+    loss, items = crit(preds, batch)
+    loss.backward()
+    arrs = dict(img=batch["img"], batch_idx=batch["batch_idx"], cls=batch["cls"], bboxes=batch["bboxes"],
+                loss=loss.detach().reshape(1), items=items)
+    for i, h in enumerate(preds):
+        arrs[f"head{i}"] = h
+    arrs["grad_names"] = np.asarray([k for k, _ in m.named_parameters()])
+    arrs["grad_norm"] = np.asarray([float(p.grad.norm()) if p.grad is not None else -1.0 for p in m.parameters()],
+                                   np.float64)
+    for k in ("model.0.conv.weight", "model.10.m.0.attn.qkv.conv.weight", "model.23.cv2.2.2.weight"):
+        arrs["grad:" + k] = dict(m.named_parameters())[k].grad
+    save("model_m256.npz", **arrs)
+
+
+def gen_detect():
+    """Detect called on its own (yolo11_modules.py:195-266): train-mode maps + backward, then the
+    eval-mode (y, maps) after the BN running-stat update; and Concat (:277-285)."""
+    torch.manual_seed(3)
+    det = ref_mods.Detect(5, (32, 64, 128))
+    det.stride = torch.tensor([8.0, 16.0, 32.0])
+    for k, v in det.state_dict().items():
+        if k.endswith(".weight") and v.dim() == 4:
+            v.copy_(torch.randn(v.shape) * (2.0 / (v.shape[0] * v.shape[2] * v.shape[3])) ** 0.5)
+    det.bias_init()
+    det.apply(lambda m: setattr(m, "eps", 1e-3) if isinstance(m, torch.nn.BatchNorm2d) else None)
+    det.apply(lambda m: setattr(m, "momentum", 0.03) if isinstance(m, torch.nn.BatchNorm2d) else None)
+    arrs = {f"p:{k}": v.clone() for k, v in det.state_dict().items()}
+    g = torch.Generator().manual_seed(61)
+    shapes = [(2, 32, 16, 16), (2, 64, 8, 8), (2, 128, 4, 4)]
+    xs = [torch.randn(s, generator=g).requires_grad_(True) for s in shapes]
+    det.train()
+    ys = det([x for x in xs])
+    dys = [torch.randn(y.shape, generator=g) for y in ys]
+    torch.autograd.backward(ys, dys)
+    for i in range(3):
+        arrs[f"x{i}"], arrs[f"y{i}"], arrs[f"dy{i}"], arrs[f"dx{i}"] = xs[i], ys[i], dys[i], xs[i].grad
+    for k, p in det.named_parameters():
+        if p.grad is not None:
+            arrs[f"g:{k}"] = p.grad
+    for k, v in det.state_dict().items():
+        if "running" in k:
+            arrs[f"s:{k}"] = v.clone()
+    det.eval()
+    with torch.no_grad():
+        y, maps = det([x.detach() for x in xs])
+    arrs["eval_y"] = y
+    for i in range(3):
+        arrs[f"eval_map{i}"] = maps[i]
+    # Concat along dim 1 and dim 2
+    cat = ref_mods.Concat(1)
+    a, b = torch.randn(2, 3, 4, 5, generator=g), torch.randn(2, 6, 4, 5, generator=g)
+    arrs.update(cat_a=a, cat_b=b, cat_out1=cat([a, b]), cat_out2=ref_mods.Concat(2)([a, a[:, :, :2]]))
+    save("detect.npz", **arrs)
+
+
+def _fingerprint(t: torch.Tensor, n: int = 16384) -> np.ndarray:
+    """A fixed strided subsample of a large tensor (element-wise comparison on a subset)."""
+    flat = t.detach().reshape(-1)
+    step = max(1, flat.numel() // n)
+    return flat[::step][:n].numpy().copy()
+
+
+def gen_attn_big():
+    """C2PSA at the attention shapes of the s@640 (heads=4, N=400) and m@1280 (heads=8, N=1600)
+    configs.  Weights are key-seeded (oracle/weights.py), inputs and output gradients drawn from
+    seeded CPU generators, so the fixture holds only outputs: per-tensor fingerprints (strided
+    subsamples), norms and parameter-gradient norms."""
+    arrs = {}
+    cases = {"h4n400": (512, (2, 512, 20, 20), 51), "h8n1600": (1024, (1, 1024, 40, 40), 52)}
+    for name, (c, shape, seed) in cases.items():
+        mod = ref_mods.C2PSA(c, c, 1)
+        apply_seeded_weights(mod.state_dict())
+        mod.apply(lambda m: setattr(m, "eps", 1e-3) if isinstance(m, torch.nn.BatchNorm2d) else None)
+        mod.apply(lambda m: setattr(m, "momentum", 0.03) if isinstance(m, torch.nn.BatchNorm2d) else None)
+        mod.train()
+        g = torch.Generator().manual_seed(seed)
+        x = torch.randn(shape, generator=g).requires_grad_(True)
+        dy = torch.randn(shape, generator=g)
+        y = mod(x)
+        y.backward(dy)
+        arrs[f"{name}/y_fp"] = _fingerprint(y)
+        arrs[f"{name}/dx_fp"] = _fingerprint(x.grad)
+        arrs[f"{name}/y_norm"] = np.float64(y.detach().double().norm())
+        arrs[f"{name}/dx_norm"] = np.float64(x.grad.double().norm())
+        arrs[f"{name}/grad_names"] = np.asarray([k for k, _ in mod.named_parameters()])
+        arrs[f"{name}/grad_norm"] = np.asarray([float(p.grad.norm()) for p in mod.parameters()], np.float64)
+        arrs[f"{name}/qkv_grad_fp"] = _fingerprint(mod.m[0].attn.qkv.conv.weight.grad)
+    save("attn_big.npz", **arrs)
+
+
 # --------------------------------------------------------------------------- per-block
 def _block_case(mod, x, seed):
     mod.train()
@@ -326,14 +424,37 @@ def gen_assigner():
     orig = crit.assigner.forward
 
     def spy(*a, **k):
+        captured["as_in"] = [t.detach().clone() for t in a]
         r = orig(*a, **k)
-        captured["r"] = r
+        captured["r"] = tuple(t.clone() for t in r)       # the loss divides target_bboxes in place (:479)
         return r
 
     crit.assigner.forward = spy
+    orig_bl = crit.bbox_loss.forward
+
+    def spy_bl(*a, **k):
+        captured["bl_in"] = [t.detach().clone() if isinstance(t, torch.Tensor) else t for t in a]
+        r = orig_bl(*a, **k)
+        captured["bl_out"] = [t.detach().clone() for t in r]
+        return r
+
+    crit.bbox_loss.forward = spy_bl
     loss, items = crit(feats_in, batch)
     loss.backward()
     tl, tb, ts, fg, tgi = captured["r"]
+    # the assigner's own inputs (TaskAlignedAssigner.forward, yolo_v8_loss.py:78-180)
+    for nm, t in zip(("pd_scores", "pd_bboxes", "anc_points", "gt_labels", "gt_bboxes", "mask_gt"), captured["as_in"]):
+        arrs["as_" + nm] = t
+    # BboxLoss.forward (:280-310) inputs / outputs, and its gradient w.r.t. pred_dist and pred_bboxes for
+    # the seed 1.3 * d loss_iou + 0.7 * d loss_dfl
+    pd, pb, ap, tbb, tsc, tss, fgm = captured["bl_in"]
+    arrs.update(bl_pred_dist=pd, bl_pred_bboxes=pb, bl_anchor_points=ap, bl_target_bboxes=tbb,
+                bl_target_scores=tsc, bl_tss=np.float32(float(tss)), bl_fg_mask=fgm,
+                bl_loss_iou=captured["bl_out"][0], bl_loss_dfl=captured["bl_out"][1])
+    pdl, pbl = pd.clone().requires_grad_(True), pb.clone().requires_grad_(True)
+    li, ld = ref_loss_mod.BboxLoss(16)(pdl, pbl, ap, tbb.clone(), tsc, tss, fgm)
+    (1.3 * li + 0.7 * ld).backward()
+    arrs.update(bl_dpred_dist=pdl.grad, bl_dpred_bboxes=pbl.grad)
     for i, f in enumerate(feats):
         arrs[f"feat{i}"] = f
         arrs[f"dfeat{i}"] = feats_in[i].grad
@@ -375,7 +496,8 @@ def gen_curve(steps=20):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["structure", "nms", "decode", "metrics", "model", "s_small", "blocks", "assigner", "curve"]
+    which = sys.argv[1:] or ["structure", "nms", "decode", "metrics", "model", "s_small", "m_small", "attn_big",
+                             "detect", "blocks", "assigner", "curve"]
     if "structure" in which:
         gen_structure()
     if "nms" in which:
@@ -389,6 +511,12 @@ if __name__ == "__main__":
                               "model.10.m.0.attn.qkv.conv.weight", "model.2.m.0.cv1.bn.weight"))
     if "s_small" in which:
         gen_s_small()
+    if "m_small" in which:
+        gen_m_small()
+    if "attn_big" in which:
+        gen_attn_big()
+    if "detect" in which:
+        gen_detect()
     if "blocks" in which:
         gen_blocks()
     if "assigner" in which:

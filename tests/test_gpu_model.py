@@ -3,7 +3,7 @@
 Tolerances (BASELINE.json north_star: 1e-2 for 16-bit tensors): activations are fp16 and
 gradients bf16, so single blocks are held to relative-L2 <= 1e-2 (outputs) / 2e-2 (input and
 parameter gradients); the full n@320 network's head maps to <= 1e-2; loss items <= 1e-2;
-per-parameter gradients within 10%, or within 2x the distance of the oracle run under the
+EVERY parameter gradient within 10%, or within 2x the distance of the oracle run under the
 HIP storage-rounding model (oracle/precision.py) where that is larger: backbone gradients are
 discontinuous in the activations through SPPF's max-pool routing — stated per assert.  The loss
 on fp32 head maps is an fp32 path: assignment decisions (fg mask, target_gt_idx) are bit-exact
@@ -87,53 +87,22 @@ def _seeded_model(scale):
 
 
 def test_model_n320_train_step_vs_reference(golden):
+    """n@320 bs2: heads, loss / items, every parameter gradient (test_gpu_network.check_network) and
+    the BN running statistics after the step, against the reference's own run."""
     from losses import v8DetectionLoss
+    from test_gpu_network import check_network
     d = golden("model_n320.npz")
     m = _seeded_model("n").train()
     batch = _batch(d)
     heads = m(batch["img"])
-    # 1e-2 (north star, 16-bit), or 1.2x the error the fp16 storage model alone produces on this
-    # input where that is larger: at n@320 bs2 the P5 map sits at 0.97 % by rounding alone
-    from oracle import model as om
-    from oracle.precision import hip_storage_rounding
-    layers, save, P = om.build(om.load_cfg("n"))
-    with torch.no_grad(), hip_storage_rounding():
-        emu = om.forward(P, layers, save, torch.from_numpy(d["img"]), training=True)
-    for i in range(3):
-        r = rel(heads[i], d[f"head{i}"])
-        assert r < max(1e-2, 1.2 * rel(emu[i], d[f"head{i}"])), (i, r)
     crit = v8DetectionLoss(m)
     loss, items = crit(heads, batch)
-    assert abs(float(loss) - float(d["loss"][0])) / float(d["loss"][0]) < 1e-2
-    assert rel(items, d["items"]) < 1e-2, (items.tolist(), d["items"].tolist())
-    loss.backward()
-    # backbone gradients of this network are discontinuous in the activations (SPPF max-pool
-    # routing, oracle/precision.py): each gradient is held to 10%, or to 2x the distance of the
-    # oracle run under the HIP storage-rounding model from the fp32 reference, whichever is larger
-    from oracle import loss as ol
-    cpu_batch = {k: v.cpu() for k, v in batch.items() if k != "img"}
-    emu = _emulated_oracle_grads("n", torch.from_numpy(d["img"]), lambda h: ol.v8_loss(h, cpu_batch)[0])
-    names = list(d["grad_names"])
-    ref = dict(zip(names, d["grad_norm"]))
-    bad = []
-    gmax = max(ref.values())
-    for k, p in m.named_parameters():
-        if not p.requires_grad or ref[k] < 1e-6 * gmax:      # true gradient ~0 (BN-invariant biases)
-            continue
-        g = float(p.grad.norm())
-        tol = max(0.1, 2.0 * abs(float(emu[k].norm()) - ref[k]) / ref[k])
-        if abs(g - ref[k]) > tol * ref[k] + 1e-6:
-            bad.append((k, g, ref[k]))
-    # the P5-branch gradients of this tiny batch hinge on a handful of stride-32 anchors whose
-    # assignment follows the predicted boxes, so ulp-level forward changes (e.g. the SiLU
-    # reciprocal) move a few of them discretely; the continuous parts are held exactly by
-    # test_assigner_and_loss_exact_fp32 (loss on identical heads) and
-    # test_network_backward_fixed_head_grads_vs_oracle (network backward on identical head grads)
-    assert len(bad) <= len(names) // 10, bad[:10]
-    for k in [n for n in d.files if n.startswith("grad:")]:
-        p = dict(m.named_parameters())[k[5:]]
-        tol = max(1e-1, 2.0 * rel(emu[k[5:]], d[k]))
-        assert rel(p.grad, d[k]) < tol, (k, rel(p.grad, d[k]), tol)
+    ref_norm = dict(zip(list(d["grad_names"]), d["grad_norm"]))
+    full = {k[5:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("grad:")}
+    worst = check_network("n", heads, loss, items, m, [torch.from_numpy(d[f"head{i}"]) for i in range(3)],
+                          d["loss"][0], d["items"], ref_norm, full, d["img"],
+                          {k: v.cpu() for k, v in batch.items() if k != "img"})
+    print("worst err/tol", worst)
     sd = m.state_dict()
     for k in [n for n in d.files if n.startswith("state:")]:
         assert rel(sd[k[6:]], d[k]) < 2e-2, (k, rel(sd[k[6:]], d[k]))
@@ -184,11 +153,28 @@ def test_model_eval_decode_vs_reference(golden):
     loss, _ = crit(m(batch["img"]), batch)      # one train forward (BN running stats update)
     loss.backward()
     m.eval()
+    # 1e-2, or 1.2x the error of the oracle under the HIP storage-rounding model (the same train
+    # step, then the eval forward on the updated running statistics) where that is larger: the eval
+    # y carries the DFL projection with random weights (Q5), which amplifies head-map rounding
+    from oracle import model as om
+    from oracle import loss as ol
+    from oracle.precision import hip_storage_rounding
+    layers, save, P = om.build(om.load_cfg("n"))
+    img = torch.from_numpy(d["img"])
+    with hip_storage_rounding():
+        P = {k: (v.requires_grad_(True) if v.is_floating_point() and "running" not in k else v) for k, v in P.items()}
+        ol.v8_loss(om.forward(P, layers, save, img, training=True),
+                   {k: v.cpu() for k, v in batch.items() if k != "img"})[0].backward()
+        with torch.no_grad():
+            emu_y, emu_f = om.forward(P, layers, save, img, training=False)
+            emu_vi = ol.v8_loss(emu_f, {k: v.cpu() for k, v in batch.items() if k != "img"})[1]
     with torch.no_grad():
         y, feats = m(batch["img"])
-        assert rel(y, d["eval_y"]) < 5e-2, rel(y, d["eval_y"])
+        bound = max(1e-2, 1.2 * rel(emu_y, d["eval_y"]))
+        assert rel(y, d["eval_y"]) < bound, (rel(y, d["eval_y"]), bound)
         vl, vi = crit((y, feats), batch)
-        assert rel(vi, d["eval_items"]) < 5e-2
+        bound = max(1e-2, 1.2 * rel(emu_vi, d["eval_items"]))
+        assert rel(vi, d["eval_items"]) < bound, (rel(vi, d["eval_items"]), bound)
 
 
 @pytest.mark.parametrize("H,W,C", [(9, 7, 16), (20, 20, 12), (48, 44, 8)])
@@ -250,6 +236,14 @@ def test_sppf_pool_chain_exact(H, W, C):
              H * W * C, C, nxt.data_ptr(), None, 0, 0, 0, B, H, W, C, st)
         cur_chk = nxt
     torch.testing.assert_close(cur_chk.cpu().view(B, H, W, C), xr2.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
+
+
+def _emulated_heads(scale, img):
+    from oracle import model as om
+    from oracle.precision import hip_storage_rounding
+    layers, save, P = om.build(om.load_cfg(scale))
+    with torch.no_grad(), hip_storage_rounding():
+        return om.forward(P, layers, save, torch.as_tensor(img), training=True)
 
 
 def _emulated_oracle_grads(scale, img, loss_fn):

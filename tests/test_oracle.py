@@ -156,3 +156,96 @@ def test_metrics_oracle_ap_tie_order():
     assert omet.calculate_ap([0.5], [0.5], 1) == pytest.approx(1.0 / (1 + 1e-6))
     assert omet.calculate_ap([], [0.9], 3) == 0.0
     assert omet.calculate_ap([0.9], [], 0) == 0.0
+
+
+def _grads_vs_golden(d, P, params, rtol_norm=1e-3):
+    names = list(d["grad_names"])
+    ref_norm = dict(zip(names, d["grad_norm"]))
+    for k, p in params.items():
+        if k.endswith("dfl.conv.weight") or k not in ref_norm:
+            continue
+        r = ref_norm[k]
+        assert abs(float(p.grad.norm()) - r) <= rtol_norm * max(r, 1e-3), (k, float(p.grad.norm()), r)
+    for k in [n for n in d.files if n.startswith("grad:")]:
+        torch.testing.assert_close(params[k[5:]].grad, torch.from_numpy(d[k]), rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("scale,name", [("s", "model_s128.npz"), ("m", "model_m256.npz")])
+def test_model_s_m_forward_loss_grads(golden, scale, name):
+    """The s (C2PSA heads=4) and m (1024-channel layers, heads=8) graphs at small resolution."""
+    d = golden(name)
+    layers, save, P = om.build(om.load_cfg(scale))
+    params = {k: v.requires_grad_(True) for k, v in P.items() if v.is_floating_point() and "running" not in k}
+    heads = om.forward(P, layers, save, torch.from_numpy(d["img"]), training=True)
+    for i in range(3):
+        torch.testing.assert_close(heads[i], torch.from_numpy(d[f"head{i}"]), rtol=1e-4, atol=1e-4)
+    loss, items = ol.v8_loss(heads, _batch(d))
+    torch.testing.assert_close(loss.detach().reshape(1), torch.from_numpy(d["loss"]), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(items, torch.from_numpy(d["items"]), rtol=1e-5, atol=1e-5)
+    loss.backward()
+    if "grad_names" not in d.files:          # model_s128: norms in parameter order
+        names = [k for k in P if P[k].is_floating_point() and "running" not in k]
+        ref = dict(zip(names, d["grad_norm"]))
+        for k, p in params.items():
+            if not k.endswith("dfl.conv.weight"):
+                assert abs(float(p.grad.norm()) - ref[k]) <= 1e-3 * max(ref[k], 1e-3), k
+        for k in [n for n in d.files if n.startswith("grad:")]:
+            torch.testing.assert_close(params[k[5:]].grad, torch.from_numpy(d[k]), rtol=1e-3, atol=1e-5)
+    else:
+        _grads_vs_golden(d, P, params)
+
+
+def attn_big_case(name):
+    """(P, x, dy) of the attn_big.npz cases: C2PSA(c, c, 1) with key-seeded weights."""
+    c, shape, seed = {"h4n400": (512, (2, 512, 20, 20), 51), "h8n1600": (1024, (1, 1024, 40, 40), 52)}[name]
+    P = om.block_params({"type": "C2PSA", "c1": c, "c2": c, "n": 1})
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(shape, generator=g)
+    dy = torch.randn(shape, generator=g)
+    return P, x, dy
+
+
+def fingerprint(t, n=16384):
+    flat = t.detach().reshape(-1)
+    step = max(1, flat.numel() // n)
+    return flat[::step][:n]
+
+
+@pytest.mark.parametrize("name", ["h4n400", "h8n1600"])
+def test_c2psa_big_heads_oracle(golden, name):
+    """C2PSA at the s@640 (heads 4, N 400) and m@1280 (heads 8, N 1600) attention shapes."""
+    d = golden("attn_big.npz")
+    P, x, dy = attn_big_case(name)
+    params = {k: v.requires_grad_(True) for k, v in P.items() if v.is_floating_point() and "running" not in k}
+    x.requires_grad_(True)
+    y = om.c2psa(P, "blk", x, 1)
+    y.backward(dy)
+    torch.testing.assert_close(fingerprint(y), torch.from_numpy(d[f"{name}/y_fp"]), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(fingerprint(x.grad), torch.from_numpy(d[f"{name}/dx_fp"]), rtol=1e-4, atol=1e-4)
+    ref = dict(zip(d[f"{name}/grad_names"], d[f"{name}/grad_norm"]))
+    for k, v in ref.items():
+        assert abs(float(params["blk." + k].grad.norm()) - v) <= 1e-3 * max(v, 1e-3), k
+    torch.testing.assert_close(fingerprint(params["blk.m.0.attn.qkv.conv.weight"].grad),
+                               torch.from_numpy(d[f"{name}/qkv_grad_fp"]), rtol=1e-3, atol=1e-5)
+
+
+def test_detect_standalone_oracle(golden):
+    """oracle.model.detect against the reference's Detect called on its own (detect.npz)."""
+    d = golden("detect.npz")
+    P = {"d." + k[2:]: torch.from_numpy(d[k]).clone() for k in d.files if k.startswith("p:")}
+    params = {k: v.requires_grad_(True) for k, v in P.items()
+              if v.is_floating_point() and "running" not in k and "dfl" not in k}
+    xs = [torch.from_numpy(d[f"x{i}"]).clone().requires_grad_(True) for i in range(3)]
+    ys = om.detect(P, "d", xs, 5, (8.0, 16.0, 32.0), tr=True)
+    for i in range(3):
+        torch.testing.assert_close(ys[i], torch.from_numpy(d[f"y{i}"]), rtol=1e-4, atol=1e-4)
+    torch.autograd.backward(ys, [torch.from_numpy(d[f"dy{i}"]) for i in range(3)])
+    for i in range(3):
+        torch.testing.assert_close(xs[i].grad, torch.from_numpy(d[f"dx{i}"]), rtol=1e-4, atol=1e-4)
+    for k, p in params.items():
+        torch.testing.assert_close(p.grad, torch.from_numpy(d["g:" + k[2:]]), rtol=1e-3, atol=1e-4)
+    for k in [n for n in d.files if n.startswith("s:")]:
+        torch.testing.assert_close(P["d." + k[2:]], torch.from_numpy(d[k]), rtol=1e-5, atol=1e-6)
+    with torch.no_grad():
+        y, maps = om.detect(P, "d", [x.detach() for x in xs], 5, (8.0, 16.0, 32.0), tr=False)
+    torch.testing.assert_close(y, torch.from_numpy(d["eval_y"]), rtol=1e-4, atol=1e-3)

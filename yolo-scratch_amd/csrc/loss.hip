@@ -126,21 +126,18 @@ struct AssignWs {
     float* out;          // [8] loss, items[3], tss, num_fg ...
 };
 
-// ---------------------------------------------------------------- assignment, pass 1
-__global__ void __launch_bounds__(256) assign_scan_kernel(const float* __restrict__ head, int64_t A, int no, int nc,
-                                                          Levels L, const float4* __restrict__ gt_box,
-                                                          const int* __restrict__ gt_valid, int M, AssignWs w) {
-    extern __shared__ unsigned long long s_amax[];    // [M]
-    int* s_cnt = reinterpret_cast<int*>(s_amax + M);   // [M]
-    const int b = blockIdx.y;
-    for (int g = threadIdx.x; g < M; g += blockDim.x) { s_amax[g] = 0ull; s_cnt[g] = 0; }
-    __syncthreads();
-    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const bool live = a < A;
-    // every lane runs the gt loop (dead lanes with zero keys) so the per-gt argmax and in-box counts
-    // reduce over the wave first (shuffles / ballot) and take one LDS atomic per wave, not per lane
-    float px1 = 0.f, py1 = 0.f, px2 = 0.f, py2 = 0.f, cx = 0.f, cy = 0.f;
-    if (live) {
+// ---------------------------------------------------------------- assignment inputs
+// The assigner reads its predictions through one of two sources: the fused loss's (B, A, 64+nc) head rows
+// (boxes decoded here, v8DetectionLoss.__call__ :408-422), or the explicit tensors a direct
+// TaskAlignedAssigner.forward call passes (pd_scores already sigmoided, pd_bboxes / anc_points in pixels).
+struct HeadSrc {
+    const float* head;
+    int64_t A;
+    int no;
+    Levels L;
+    // pixel-space predicted box + anchor centre; stores the grid-unit box the loss re-reads
+    __device__ void box(int b, int64_t a, AssignWs& w, float& px1, float& py1, float& px2, float& py2, float& cx,
+                        float& cy) const {
         const float* x = head + (int64_t(b) * A + a) * no;
         float ax, ay, s;
         anchor_of(L, a, ax, ay, s);
@@ -152,6 +149,49 @@ __global__ void __launch_bounds__(256) assign_scan_kernel(const float* __restric
         px1 = x1 * s; py1 = y1 * s; px2 = x2 * s; py2 = y2 * s;
         cx = ax * s; cy = ay * s;                        // anchor_points * stride_tensor
     }
+    __device__ float4 pixbox(int b, int64_t a, const AssignWs& w) const {
+        float ax, ay, s;
+        anchor_of(L, a, ax, ay, s);
+        float4 pb = w.pbox[int64_t(b) * A + a];
+        return make_float4(pb.x * s, pb.y * s, pb.z * s, pb.w * s);
+    }
+    __device__ float score(int b, int64_t a, int lab) const { return sigm(head[(int64_t(b) * A + a) * no + 64 + lab]); }
+};
+
+struct PlainSrc {
+    const float* scores;    // (B, A, nc) probabilities
+    const float* boxes;     // (B, A, 4) xyxy pixels
+    const float* anc;       // (A, 2) pixels
+    int64_t A;
+    int nc;
+    __device__ void box(int b, int64_t a, AssignWs&, float& px1, float& py1, float& px2, float& py2, float& cx,
+                        float& cy) const {
+        const float* r = boxes + (int64_t(b) * A + a) * 4;
+        px1 = r[0]; py1 = r[1]; px2 = r[2]; py2 = r[3];
+        cx = anc[2 * a]; cy = anc[2 * a + 1];
+    }
+    __device__ float4 pixbox(int b, int64_t a, const AssignWs&) const {
+        const float* r = boxes + (int64_t(b) * A + a) * 4;
+        return make_float4(r[0], r[1], r[2], r[3]);
+    }
+    __device__ float score(int b, int64_t a, int lab) const { return scores[(int64_t(b) * A + a) * nc + lab]; }
+};
+
+// ---------------------------------------------------------------- assignment, pass 1
+template <class Src>
+__global__ void __launch_bounds__(256) assign_scan_kernel(Src src, int64_t A, const float4* __restrict__ gt_box,
+                                                          const int* __restrict__ gt_valid, int M, AssignWs w) {
+    extern __shared__ unsigned long long s_amax[];    // [M]
+    int* s_cnt = reinterpret_cast<int*>(s_amax + M);   // [M]
+    const int b = blockIdx.y;
+    for (int g = threadIdx.x; g < M; g += blockDim.x) { s_amax[g] = 0ull; s_cnt[g] = 0; }
+    __syncthreads();
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const bool live = a < A;
+    // every lane runs the gt loop (dead lanes with zero keys) so the per-gt argmax and in-box counts
+    // reduce over the wave first (shuffles / ballot) and take one LDS atomic per wave, not per lane
+    float px1 = 0.f, py1 = 0.f, px2 = 0.f, py2 = 0.f, cx = 0.f, cy = 0.f;
+    if (live) src.box(b, a, w, px1, py1, px2, py2, cx, cy);
     int cnt = 0, first = -1, gm = 0;
     float best = -1.f;
     const int lane = threadIdx.x & 63;
@@ -269,23 +309,21 @@ __global__ void __launch_bounds__(RES_THREADS) assign_resolve_kernel(const float
 }
 
 // target-score magnitude: align = sigmoid(cls[label])^0.5 * IoU^4 (:206), norm = align*IoU/(align+eps)
-__global__ void assign_norm_kernel(const float* __restrict__ head, int64_t A, int no, Levels L,
-                                   const float4* __restrict__ gt_box, const float* __restrict__ gt_lab, int M,
-                                   AssignWs w) {
+template <class Src>
+__global__ void assign_norm_kernel(Src src, int64_t A, const float4* __restrict__ gt_box,
+                                   const float* __restrict__ gt_lab, int M, AssignWs w) {
     const int b = blockIdx.y;
     const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (a >= A) return;
     const int64_t i = int64_t(b) * A + a;
     if (!w.fg[i]) { w.norm[i] = 0.f; return; }
-    float ax, ay, s;
-    anchor_of(L, a, ax, ay, s);
-    float4 pb = w.pbox[i];
+    float4 pb = src.pixbox(b, a, w);
     int t = w.tgi[i];
     float4 gb = gt_box[b * M + t];
-    float iou = iou_xyxy(pb.x * s, pb.y * s, pb.z * s, pb.w * s, gb.x, gb.y, gb.z, gb.w);
+    float iou = iou_xyxy(pb.x, pb.y, pb.z, pb.w, gb.x, gb.y, gb.z, gb.w);
     iou = iou < 0.f ? 0.f : iou;
     int lab = int(gt_lab[b * M + t]);
-    float sc = sigm(head[i * no + 64 + lab]);
+    float sc = src.score(b, a, lab);
     float align = sqrtf(sc) * powf(iou, 4.0f);
     w.norm[i] = align * iou / (align + EPS_TAL);
 }
@@ -513,6 +551,157 @@ __global__ void detect_decode_kernel(const float* __restrict__ head, int64_t A, 
     for (int c = 0; c < nc; ++c) yb[(4 + c) * A + a] = sigm(x[64 + c]);
 }
 
+// ---------------------------------------------------------------- TaskAlignedAssigner.forward on explicit tensors
+// mask_gt (float, the reference's `if mask_gt[b, g]` truthiness) -> int valid flags
+__global__ void mask_valid_kernel(const float* __restrict__ mask_gt, int64_t n, int* __restrict__ valid) {
+    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) valid[i] = mask_gt[i] != 0.f;
+}
+
+// get_targets (:246-270) + target_scores normalisation (:172-178) on the final assignment:
+// labels = gt_labels[b, tgi] clamped to [0, nc] (float, like gt_labels), boxes = gt_bboxes[b, tgi],
+// scores = one-hot(label) * norm on foreground rows, fg (bool) and tgi (int64)
+__global__ void assign_targets_kernel(int64_t A, int nc, const float4* __restrict__ gt_box,
+                                      const float* __restrict__ gt_lab, int M, AssignWs w, float* __restrict__ t_lab,
+                                      float4* __restrict__ t_box, float* __restrict__ t_sc, uint8_t* __restrict__ fg_out,
+                                      int64_t* __restrict__ tgi_out) {
+    const int b = blockIdx.y;
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (a >= A) return;
+    const int64_t i = int64_t(b) * A + a;
+    const int t = w.tgi[i], f = w.fg[i];
+    float lab = gt_lab[b * M + t];
+    lab = fminf(fmaxf(lab, 0.f), float(nc));
+    t_lab[i] = lab;
+    t_box[i] = gt_box[b * M + t];
+    const int li = int(lab);
+    const float nm = w.norm[i];
+    for (int c = 0; c < nc; ++c) t_sc[i * nc + c] = (f && c == li) ? nm : 0.f;
+    fg_out[i] = uint8_t(f);
+    tgi_out[i] = int64_t(t);
+}
+
+// ---------------------------------------------------------------- BboxLoss.forward on explicit tensors (:280-324)
+// one thread per anchor; partials (double) of the CIoU and DFL sums over foreground anchors
+struct BoxIn {
+    const float* pdist;     // (B, A, 64)
+    const float* pbox;      // (B, A, 4) grid units
+    const float* anc;       // (A, 2) grid units
+    const float* tbox;      // (B, A, 4) grid units
+    const float* tsc;       // (B, A, nc)
+    const uint8_t* fg;      // (B, A)
+    int64_t A;
+    int nc;
+};
+
+__device__ __forceinline__ float box_weight(const BoxIn& in, int64_t i) {
+    float wsum = 0.f;                                    // target_scores.sum(-1) (:298)
+    for (int c = 0; c < in.nc; ++c) wsum += in.tsc[i * in.nc + c];
+    return wsum;
+}
+
+__global__ void __launch_bounds__(256) bbox_loss_partial_kernel(BoxIn in, double* __restrict__ part) {
+    __shared__ double red[2][256];
+    const int b = blockIdx.y;
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    double li = 0, ld = 0;
+    if (a < in.A) {
+        const int64_t i = int64_t(b) * in.A + a;
+        if (in.fg[i]) {
+            const float wt = box_weight(in, i);
+            const float* pb = in.pbox + i * 4;
+            const float* tb = in.tbox + i * 4;
+            CiouOut ci = ciou_grad(pb[0], pb[1], pb[2], pb[3], tb[0], tb[1], tb[2], tb[3], false);
+            li = double((1.0f - ci.ciou) * wt);
+            const float ax = in.anc[2 * a], ay = in.anc[2 * a + 1];
+            float tgt[4] = {ax - tb[0], ay - tb[1], tb[2] - ax, tb[3] - ay};
+            float acc = 0.f;
+            for (int k = 0; k < 4; ++k) {
+                float t = fminf(fmaxf(tgt[k], 0.f), REG - 1 - 0.01f);
+                int tl = int(t);
+                float wl = float(tl + 1) - t, wr = 1.0f - wl;
+                const float* xs = in.pdist + i * 64 + k * REG;
+                float m = xs[0];
+                for (int j = 1; j < REG; ++j) m = fmaxf(m, xs[j]);
+                float se = 0.f;
+                for (int j = 0; j < REG; ++j) se += expf(xs[j] - m);
+                float lse = m + logf(se);
+                acc += (lse - xs[tl]) * wl + (lse - xs[tl + 1]) * wr;
+            }
+            ld = double(acc / 4.0f * wt);
+        }
+    }
+    red[0][threadIdx.x] = li;
+    red[1][threadIdx.x] = ld;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 2) part[(int64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 2 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// out[0] = loss_iou, out[1] = loss_dfl (each sum / target_scores_sum)
+__global__ void bbox_loss_final_kernel(const double* __restrict__ part, int nparts, const float* __restrict__ tss,
+                                       float* __restrict__ out) {
+    __shared__ double red[2][256];
+    double s0 = 0, s1 = 0;
+    for (int p = threadIdx.x; p < nparts; p += blockDim.x) { s0 += part[2 * p]; s1 += part[2 * p + 1]; }
+    red[0][threadIdx.x] = s0;
+    red[1][threadIdx.x] = s1;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + o];
+            red[1][threadIdx.x] += red[1][threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out[0] = float(red[0][0]) / tss[0];
+        out[1] = float(red[1][0]) / tss[0];
+    }
+}
+
+// d(g0 * loss_iou + g1 * loss_dfl) / d pred_bboxes and / d pred_dist (zero on background rows)
+__global__ void __launch_bounds__(256) bbox_loss_bwd_kernel(BoxIn in, const float* __restrict__ tss,
+                                                            const float* __restrict__ gout, float* __restrict__ dpdist,
+                                                            float* __restrict__ dpbox) {
+    const int b = blockIdx.y;
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (a >= in.A) return;
+    const int64_t i = int64_t(b) * in.A + a;
+    float* gd = dpdist + i * 64;
+    float* gb = dpbox + i * 4;
+    if (!in.fg[i]) {
+        for (int j = 0; j < 64; ++j) gd[j] = 0.f;
+        for (int j = 0; j < 4; ++j) gb[j] = 0.f;
+        return;
+    }
+    const float wt = box_weight(in, i);
+    const float* pb = in.pbox + i * 4;
+    const float* tb = in.tbox + i * 4;
+    CiouOut ci = ciou_grad(pb[0], pb[1], pb[2], pb[3], tb[0], tb[1], tb[2], tb[3], true);
+    const float kiou = -gout[0] * wt / tss[0];
+    for (int j = 0; j < 4; ++j) gb[j] = kiou * ci.g[j];
+    const float ax = in.anc[2 * a], ay = in.anc[2 * a + 1];
+    float tgt[4] = {ax - tb[0], ay - tb[1], tb[2] - ax, tb[3] - ay};
+    const float kdfl = gout[1] * wt / (4.0f * tss[0]);
+    for (int k = 0; k < 4; ++k) {
+        float t = fminf(fmaxf(tgt[k], 0.f), REG - 1 - 0.01f);
+        int tl = int(t);
+        float wl = float(tl + 1) - t, wr = 1.0f - wl;
+        const float* xs = in.pdist + i * 64 + k * REG;
+        float p[REG];
+        dfl_expect(xs, p);
+        for (int j = 0; j < REG; ++j)
+            gd[k * REG + j] = kdfl * ((wl + wr) * p[j] - (j == tl ? wl : 0.f) - (j == tl + 1 ? wr : 0.f));
+    }
+}
+
 inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct Carve {
@@ -593,11 +782,12 @@ extern "C" int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int 
     if (M > 0) {
         hipLaunchKernelGGL(gt_prep_kernel, dim3(unsigned(B)), dim3(64), 0, st, batch_idx, cls, bboxes,
                            n_targets, int(B), M, imgsz_h, imgsz_w, reinterpret_cast<float4*>(gt_box), gt_lab, gt_valid);
-        hipLaunchKernelGGL(assign_scan_kernel, ga, dim3(256), size_t(M) * 12, st, head, A, no, nc, L,
+        HeadSrc src{head, A, no, L};
+        hipLaunchKernelGGL(assign_scan_kernel<HeadSrc>, ga, dim3(256), size_t(M) * 12, st, src, A,
                            reinterpret_cast<const float4*>(gt_box), gt_valid, M, w);
         hipLaunchKernelGGL(assign_resolve_kernel, dim3(unsigned(B)), dim3(RES_THREADS), size_t(M) * 5 * sizeof(int),
                            st, head, A, no, nc, reinterpret_cast<const float4*>(gt_box), gt_lab, gt_valid, M, w);
-        hipLaunchKernelGGL(assign_norm_kernel, ga, dim3(256), 0, st, head, A, no, L,
+        hipLaunchKernelGGL(assign_norm_kernel<HeadSrc>, ga, dim3(256), 0, st, src, A,
                            reinterpret_cast<const float4*>(gt_box), gt_lab, M, w);
     } else {
         // no targets in the batch (:100-108 early return): all background
@@ -647,5 +837,74 @@ extern "C" int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc,
     dim3 ga(unsigned((A + 255) / 256), unsigned(B));
     hipLaunchKernelGGL(detect_decode_kernel, ga, dim3(256), 0, as_stream(stream), head, A, 64 + nc, nc, L, dfl_w, y);
     YM_LAUNCH_CHECK("ym_detect_decode");
+    return YM_OK;
+}
+
+// TaskAlignedAssigner.forward (yolo_v8_loss.py:78-180) on explicit tensors; M >= 1 (the M = 0 early return
+// :100-108 is the caller's).  Outputs: target_labels (B,A) f32, target_bboxes (B,A,4), target_scores
+// (B,A,nc), fg_mask (B,A) u8, target_gt_idx (B,A) i64.
+extern "C" size_t ym_tal_assign_workspace_size(int64_t B, int64_t A, int M) {
+    return ym_loss_workspace_size(B, A, M) + 256 + size_t(B) * std::max(M, 1) * 4;
+}
+
+extern "C" int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, const float* anc_points,
+                             const float* gt_labels, const float* gt_bboxes, const float* mask_gt, int64_t B,
+                             int64_t A, int nc, int M, void* workspace, size_t workspace_bytes, float* target_labels,
+                             float* target_bboxes, float* target_scores, uint8_t* fg_mask, int64_t* target_gt_idx,
+                             void* stream) {
+    YM_CHECK_ARG(M >= 1 && M <= 4096, "ym_tal_assign: M=%d out of range (1..4096)", M);
+    YM_CHECK_ARG(nc >= 1 && nc <= 64, "ym_tal_assign: nc");
+    YM_CHECK_ARG((reinterpret_cast<uintptr_t>(gt_bboxes) & 15) == 0, "ym_tal_assign: gt_bboxes not 16-B aligned");
+    YM_CHECK_ARG((reinterpret_cast<uintptr_t>(target_bboxes) & 15) == 0, "ym_tal_assign: target_bboxes not 16-B aligned");
+    hipStream_t st = as_stream(stream);
+    const int64_t nparts = B * ((A + 255) / 256);
+    Carve c = carve(workspace, B, A, M, nparts);
+    const size_t vbytes = size_t(B) * M * 4;
+    YM_CHECK_ARG(workspace_bytes >= c.bytes + vbytes, "ym_tal_assign: workspace too small");
+    int* valid = reinterpret_cast<int*>(static_cast<char*>(workspace) + c.bytes);
+    AssignWs w = c.w;
+    if (hipMemsetAsync(workspace, 0, zero_bytes(B, A, M), st) != hipSuccess) return YM_ERR_HIP;
+    hipLaunchKernelGGL(mask_valid_kernel, dim3(unsigned((B * M + 255) / 256)), dim3(256), 0, st, mask_gt, B * M, valid);
+    dim3 ga(unsigned((A + 255) / 256), unsigned(B));
+    PlainSrc src{pd_scores, pd_bboxes, anc_points, A, nc};
+    const float4* gb = reinterpret_cast<const float4*>(gt_bboxes);
+    hipLaunchKernelGGL(assign_scan_kernel<PlainSrc>, ga, dim3(256), size_t(M) * 12, st, src, A, gb, valid, M, w);
+    hipLaunchKernelGGL(assign_resolve_kernel, dim3(unsigned(B)), dim3(RES_THREADS), size_t(M) * 5 * sizeof(int), st,
+                       nullptr, A, 0, nc, gb, gt_labels, valid, M, w);
+    hipLaunchKernelGGL(assign_norm_kernel<PlainSrc>, ga, dim3(256), 0, st, src, A, gb, gt_labels, M, w);
+    hipLaunchKernelGGL(assign_targets_kernel, ga, dim3(256), 0, st, A, nc, gb, gt_labels, M, w, target_labels,
+                       reinterpret_cast<float4*>(target_bboxes), target_scores, fg_mask, target_gt_idx);
+    YM_LAUNCH_CHECK("ym_tal_assign");
+    return YM_OK;
+}
+
+// BboxLoss.forward (yolo_v8_loss.py:280-324): out[0] = loss_iou, out[1] = loss_dfl; tss is a device scalar
+extern "C" size_t ym_bbox_loss_workspace_size(int64_t B, int64_t A) { return size_t(B) * ((A + 255) / 256) * 16; }
+
+extern "C" int ym_bbox_loss_fwd(const float* pred_dist, const float* pred_bboxes, const float* anchor_points,
+                                const float* target_bboxes, const float* target_scores, const float* tss,
+                                const uint8_t* fg_mask, int64_t B, int64_t A, int nc, void* workspace,
+                                size_t workspace_bytes, float* out, void* stream) {
+    YM_CHECK_ARG(nc >= 1 && nc <= 64, "ym_bbox_loss_fwd: nc");
+    YM_CHECK_ARG(workspace_bytes >= ym_bbox_loss_workspace_size(B, A), "ym_bbox_loss_fwd: workspace too small");
+    hipStream_t st = as_stream(stream);
+    BoxIn in{pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, fg_mask, A, nc};
+    dim3 ga(unsigned((A + 255) / 256), unsigned(B));
+    double* part = static_cast<double*>(workspace);
+    hipLaunchKernelGGL(bbox_loss_partial_kernel, ga, dim3(256), 0, st, in, part);
+    hipLaunchKernelGGL(bbox_loss_final_kernel, dim3(1), dim3(256), 0, st, part, int(ga.x * ga.y), tss, out);
+    YM_LAUNCH_CHECK("ym_bbox_loss_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_bbox_loss_bwd(const float* pred_dist, const float* pred_bboxes, const float* anchor_points,
+                                const float* target_bboxes, const float* target_scores, const float* tss,
+                                const uint8_t* fg_mask, int64_t B, int64_t A, int nc, const float* grad_out,
+                                float* dpred_dist, float* dpred_bboxes, void* stream) {
+    BoxIn in{pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, fg_mask, A, nc};
+    dim3 ga(unsigned((A + 255) / 256), unsigned(B));
+    hipLaunchKernelGGL(bbox_loss_bwd_kernel, ga, dim3(256), 0, as_stream(stream), in, tss, grad_out, dpred_dist,
+                       dpred_bboxes);
+    YM_LAUNCH_CHECK("ym_bbox_loss_bwd");
     return YM_OK;
 }

@@ -535,3 +535,17 @@ extern "C" int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, 
     return YM_OK;
 }
 
+
+extern "C" int ym_copy2d(void* dst, int64_t dst_pitch, const void* src, int64_t src_pitch, int64_t width_bytes,
+                         int64_t rows, void* stream) {
+    YM_CHECK_ARG(width_bytes >= 0 && rows >= 0 && dst_pitch >= width_bytes && src_pitch >= width_bytes,
+                 "ym_copy2d: bad pitches");
+    if (width_bytes == 0 || rows == 0) return YM_OK;
+    if (hipMemcpy2DAsync(dst, size_t(dst_pitch), src, size_t(src_pitch), size_t(width_bytes), size_t(rows),
+                         hipMemcpyDeviceToDevice, as_stream(stream)) != hipSuccess)
+    {
+        ym::set_error("ym_copy2d: hipMemcpy2DAsync failed");
+        return YM_ERR_HIP;
+    }
+    return YM_OK;
+}

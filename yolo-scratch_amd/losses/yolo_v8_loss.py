@@ -11,9 +11,10 @@ The host synchronises once per call (the largest per-image box count sizes
 the GT table) instead of 2*B*M+4 times.
 
 The helper functions (bbox_iou, bbox2dist, make_anchors, dist2bbox) are the
-reference's tensor utilities with identical semantics; TaskAlignedAssigner and
-BboxLoss carry the reference's hyper-parameters for API compatibility — their
-arithmetic lives in the fused kernels.
+reference's tensor utilities with identical semantics.  TaskAlignedAssigner and
+BboxLoss are callable on their own with the reference's signatures and return
+conventions; they run the same HIP kernels on explicit tensors (ym_tal_assign,
+ym_bbox_loss_fwd / _bwd).
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ import math
 import torch
 import torch.nn as nn
 
-from yolomi._lib import YolomiError, call, lib, stream_ptr
+from yolomi._lib import YolomiError, call, lib, require_device, stream_ptr
 
 
 def bbox_iou(box1, box2, xywh=True, GIoU=False, DIoU=False, CIoU=False, eps=1e-7):
@@ -88,27 +89,103 @@ def dist2bbox(distance, anchor_points, xywh=True, dim=-1):
     return torch.cat((x1y1, x2y2), dim)
 
 
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    return t.detach().to(torch.float32).contiguous()
+
+
 class TaskAlignedAssigner(nn.Module):
-    """Hyper-parameters of the task-aligned assigner (reference :64-76).  As in the reference,
-    `topk` is stored but never applied; the assignment runs fused in ym_loss_fwd."""
+    """Task-aligned assigner (reference :64-270).  As in the reference, `topk` is stored but never
+    applied.  `forward` runs the HIP assignment kernels of the fused loss (ym_tal_assign)
+    on explicit tensors and returns the reference's 5-tuple; inside v8DetectionLoss the same kernels
+    run fused on the head buffer (ym_loss_fwd)."""
 
     def __init__(self, topk=13, num_classes=80, alpha=1.0, beta=6.0, eps=1e-9):
         super().__init__()
         self.topk, self.num_classes, self.alpha, self.beta, self.eps = topk, num_classes, alpha, beta, eps
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("the MI355X assigner runs fused inside v8DetectionLoss (ym_loss_fwd)")
+    @torch.no_grad()
+    def forward(self, pd_scores, pd_bboxes, anc_points, gt_labels, gt_bboxes, mask_gt):
+        """-> (target_labels (B,A), target_bboxes (B,A,4), target_scores (B,A,nc), fg_mask (B,A) bool,
+        target_gt_idx (B,A) int64), reference :78-180 (including its M = 0 early return :100-108)."""
+        require_device(pd_scores, pd_bboxes, anc_points, gt_labels, gt_bboxes, mask_gt)
+        if (self.alpha, self.beta, self.eps) != (0.5, 4.0, 1e-9):
+            raise YolomiError("the HIP assigner is specialised for alpha=0.5, beta=4.0, eps=1e-9 "
+                              "(v8DetectionLoss's TaskAlignedAssigner(topk=50, alpha=0.5, beta=4.0))")
+        self.bs = B = pd_scores.shape[0]
+        self.n_max_boxes = M = gt_bboxes.shape[1]
+        A, nc = pd_scores.shape[1], pd_scores.shape[2]
+        if nc != self.num_classes:
+            raise YolomiError(f"pd_scores has {nc} classes, assigner built for {self.num_classes}")
+        dev = pd_scores.device
+        if M == 0:
+            return (torch.full_like(pd_scores[..., 0], self.num_classes).long(), torch.zeros_like(pd_bboxes),
+                    torch.zeros_like(pd_scores), torch.zeros_like(pd_scores[..., 0]),
+                    torch.zeros_like(pd_scores[..., 0]))
+        sc, pb, an = _f32(pd_scores), _f32(pd_bboxes), _f32(anc_points)
+        gl, gb = _f32(gt_labels).reshape(B, M), _f32(gt_bboxes).reshape(B, M, 4).clone()   # clone: 16-B aligned
+        mg = _f32(mask_gt).reshape(B, M)
+        ws_n = lib().ym_tal_assign_workspace_size(B, A, M)
+        ws = torch.empty(ws_n, dtype=torch.uint8, device=dev)
+        t_lab = torch.empty(B, A, dtype=torch.float32, device=dev)
+        t_box = torch.empty(B, A, 4, dtype=torch.float32, device=dev)
+        t_sc = torch.empty(B, A, nc, dtype=torch.float32, device=dev)
+        fg = torch.empty(B, A, dtype=torch.bool, device=dev)
+        tgi = torch.empty(B, A, dtype=torch.int64, device=dev)
+        call("ym_tal_assign", sc.data_ptr(), pb.data_ptr(), an.data_ptr(), gl.data_ptr(), gb.data_ptr(), mg.data_ptr(),
+             B, A, nc, M, ws.data_ptr(), ws_n, t_lab.data_ptr(), t_box.data_ptr(), t_sc.data_ptr(), fg.data_ptr(),
+             tgi.data_ptr(), stream_ptr(dev))
+        return t_lab.to(gt_labels.dtype), t_box, t_sc, fg, tgi
+
+
+class _BboxLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, tss, fg_mask):
+        B, A = fg_mask.shape
+        nc = target_scores.shape[-1]
+        dev = pred_dist.device
+        ins = [_f32(pred_dist).reshape(B, A, 64), _f32(pred_bboxes).reshape(B, A, 4), _f32(anchor_points).reshape(A, 2),
+               _f32(target_bboxes).reshape(B, A, 4), _f32(target_scores).reshape(B, A, nc), tss,
+               fg_mask.to(torch.uint8).contiguous()]
+        ws_n = lib().ym_bbox_loss_workspace_size(B, A)
+        ws = torch.empty(max(ws_n, 8), dtype=torch.uint8, device=dev)
+        out = torch.empty(2, dtype=torch.float32, device=dev)
+        call("ym_bbox_loss_fwd", *[t.data_ptr() for t in ins], B, A, nc, ws.data_ptr(), ws_n, out.data_ptr(),
+             stream_ptr(dev))
+        ctx.save_for_backward(*ins)
+        ctx.meta = (B, A, nc, pred_dist.shape, pred_bboxes.shape)
+        return out[0].clone(), out[1].clone()
+
+    @staticmethod
+    def backward(ctx, g_iou, g_dfl):
+        ins = ctx.saved_tensors
+        B, A, nc, sd, sb = ctx.meta
+        dev = ins[0].device
+        z = torch.zeros((), dtype=torch.float32, device=dev)
+        g = torch.stack([(g_iou if g_iou is not None else z).float().reshape(()),
+                         (g_dfl if g_dfl is not None else z).float().reshape(())]).contiguous()
+        dd = torch.empty(B, A, 64, dtype=torch.float32, device=dev)
+        db = torch.empty(B, A, 4, dtype=torch.float32, device=dev)
+        call("ym_bbox_loss_bwd", *[t.data_ptr() for t in ins], B, A, nc, g.data_ptr(), dd.data_ptr(), db.data_ptr(),
+             stream_ptr(dev))
+        return dd.view(sd), db.view(sb), None, None, None, None, None
 
 
 class BboxLoss(nn.Module):
-    """CIoU + DFL box loss hyper-parameters (reference :273-324); computed in ym_loss_fwd/bwd."""
+    """CIoU + DFL box loss (reference :273-324).  `forward` runs ym_bbox_loss_fwd/bwd (the fused
+    loss's CIoU and DFL terms on explicit tensors; differentiable in pred_dist and pred_bboxes)."""
 
     def __init__(self, reg_max=16):
         super().__init__()
         self.reg_max = reg_max
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("the MI355X box loss runs fused inside v8DetectionLoss (ym_loss_fwd)")
+    def forward(self, pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, target_scores_sum, fg_mask):
+        """-> (loss_iou, loss_dfl), reference :280-310."""
+        require_device(pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, fg_mask)
+        if self.reg_max != 16:
+            raise YolomiError("the HIP box loss is specialised for reg_max=16")
+        tss = torch.as_tensor(target_scores_sum, dtype=torch.float32, device=pred_dist.device).detach().reshape(1)
+        return _BboxLossFn.apply(pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores,
+                                 tss.contiguous(), fg_mask)
 
 
 class _LossCtx:

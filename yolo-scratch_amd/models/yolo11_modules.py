@@ -179,7 +179,27 @@ class Detect(nn.Module):
         self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
 
     def forward(self, x):
-        raise NotImplementedError("Detect runs as part of the YOLOv11 plan (call the model)")
+        """Train: list of (B, 64+nc, h, w) maps; eval: (y (B, 4+nc, A), maps) (reference :237-266).
+        Inside a YOLOv11 the head runs as part of the model's plan; called on its own it lowers its
+        six conv chains and bias convs into a plan of its own (yolomi.graph.run_detect)."""
+        from yolomi.graph import run_detect
+        from yolomi import head as yhead
+        head, plan = run_detect(self, x)
+        maps = yhead.level_views(head, plan.level_hw)
+        if self.training:
+            return maps
+        return yhead.inference(self, head, plan.level_hw), maps
+
+    def inference(self, x):
+        """Decode a list of level maps to y (B, 4+nc, A): DFL projection with this module's weights
+        (Q5), ltrb -> xywh * stride, sigmoid(cls) (reference :248-266) — ym_detect_decode."""
+        from yolomi import head as yhead
+        h = getattr(x[0], "_ym_head", None)
+        if h is not None and all(getattr(f, "_ym_head", None) is h for f in x):
+            return yhead.inference(self, h, list(x[0]._ym_levels))
+        B = x[0].shape[0]
+        head = torch.cat([t.reshape(B, self.no, -1) for t in x], 2).permute(0, 2, 1).float().contiguous()
+        return yhead.inference(self, head, [tuple(t.shape[2:]) for t in x])
 
     def bias_init(self):
         """Reference :268-274; called while stride is still zero."""
@@ -199,7 +219,11 @@ class Concat(nn.Module):
         self.d = dimension
 
     def forward(self, x):
-        raise NotImplementedError("Concat runs as part of the YOLOv11 plan (call the model)")
+        """torch.cat(x, self.d) (reference :284-285).  Inside a YOLOv11 a concat is free (producers
+        write channel slices of one buffer); called on its own it is a strided device copy per input
+        (ym_copy2d), differentiable."""
+        from yolomi.concat import concat
+        return concat(list(x), self.d)
 
 
 def make_anchors(feats, strides, grid_cell_offset=0.5):

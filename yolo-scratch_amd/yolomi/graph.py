@@ -1176,6 +1176,69 @@ def run_block(module, x: torch.Tensor):
     return _BlockFn.apply(x, anchor, plan)
 
 
+class _DetectFn(torch.autograd.Function):
+    """Detect on its own: three NCHW fp32 level maps -> the (B, A, 64+nc) fp32 head buffer."""
+
+    @staticmethod
+    def forward(ctx, anchor, plan, *xs):
+        for v, x in zip(plan.inputs, xs):
+            v.act.t.copy_(x.permute(0, 2, 3, 1))
+        plan.forward()
+        ctx.plan = plan
+        ctx.needs = [x.requires_grad for x in xs]
+        return plan.head.clone()
+
+    @staticmethod
+    def backward(ctx, dhead):
+        plan = ctx.plan
+        plan.dhead = dhead.contiguous()
+        plan.backward_from_head()
+        plan.install_grads()
+        dxs = [v.act.grad().permute(0, 3, 1, 2).float() if need else None for v, need in zip(plan.inputs, ctx.needs)]
+        return (None, None, *dxs)
+
+
+def run_detect(det, xs):
+    """Detect.forward on standalone level maps (yolo11_modules.py:237-266): the head's six conv
+    chains and bias convs as one plan; returns (head (B, A, 64+nc) fp32, plan)."""
+    xs = list(xs)
+    if not xs or not all(x.is_cuda for x in xs):
+        raise YolomiError("yolomi kernels run on the MI355X only (got a CPU tensor)")
+    if len(xs) != det.nl:
+        raise YolomiError(f"Detect expects {det.nl} level maps, got {len(xs)}")
+    B = xs[0].shape[0]
+    key = ("detect", tuple(tuple(x.shape) for x in xs), det.training, tuple(x.requires_grad for x in xs))
+    cache = det.__dict__.setdefault("_ym_plans", {})
+    plan = cache.get(key)
+    if plan is None:
+        plan = Plan(det, B, xs[0].shape[2], xs[0].shape[3], xs[0].device, det.training)
+        plan.inputs = [plan.act(x.shape[1], x.shape[2], x.shape[3], name=f"level{i}") for i, x in enumerate(xs)]
+        plan.input = None
+        plan.input_requires_grad = any(x.requires_grad for x in xs)
+        A = sum(x.shape[2] * x.shape[3] for x in xs)
+        plan.head = torch.empty(B, A, det.no, dtype=F32, device=plan.dev)
+        plan.dhead = torch.empty_like(plan.head)
+        _detect(plan, det, plan.inputs, plan.head)
+        plan.level_hw = [(x.shape[2], x.shape[3]) for x in xs]
+
+        def backward_from_head():
+            plan._backward_ops(plan.ops)
+        plan.backward_from_head = backward_from_head
+        cache[key] = plan
+    # every level input takes part in the backward (needs_grad checks plan.input only)
+    plan.needs_grad = lambda v: v.act is not None
+    anchor = det.__dict__.setdefault("_ym_anchor", torch.zeros(1, device=xs[0].device, requires_grad=True))
+    xs32 = [x.float().contiguous() for x in xs]
+    if torch.is_grad_enabled() and det.training:
+        head = _DetectFn.apply(anchor, plan, *xs32)
+    else:
+        for v, x in zip(plan.inputs, xs32):
+            v.act.t.copy_(x.permute(0, 2, 3, 1))
+        plan.forward()
+        head = plan.head.clone()
+    return head, plan
+
+
 def run_model(model, img: torch.Tensor):
     """Training-mode / eval-mode forward of the whole YOLOv11; returns the (B, A, 64+nc) fp32 head buffer."""
     if not img.is_cuda:
