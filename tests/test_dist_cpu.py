@@ -105,7 +105,7 @@ def _bucket_worker(rank, world, port, q):
             plan.backward(rank, step)
             sync.sync()
             res.append([float(plan.grad_views[id(p)].mean()) for p in plan.params])
-        q.put((rank, res, len(sync.buckets.ranges)))
+        q.put((rank, res, len(sync.buckets[id(plan)].ranges)))
         ydist.shutdown()
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e)))
@@ -131,3 +131,150 @@ def test_bucketed_overlap_world2_gloo():
         for step, means in enumerate(res[r][1]):
             for i, g in enumerate(means):
                 assert g == pytest.approx(1.5 * (i + 1) * (step + 1)), (r, step, i)
+
+
+def _spawn(target, world=2, extra=()):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, *extra)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r = q.get(timeout=180)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=60)
+    for r in res.values():
+        assert r[1] != "error", r[2]
+    return res
+
+
+def _alternate_worker(rank, world, port, q):
+    """Two plans (two batch sizes: a partial last batch) used alternately, the ADVICE r1 case: each
+    plan's own hook must launch its own buckets and sync() must never reduce twice."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from yolomi import dist as ydist
+        ctx = ydist.init_from_env("gloo")
+        m = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(6)])
+        plans = [_FakePlan(m), _FakePlan(m)]
+        sync = ydist.GradSync(m, ctx, bucket_mb=0.02)
+        res = []
+        for step, which in enumerate((0, 1, 0, 1, 0, 0, 1, 1)):
+            plan = plans[which]
+            m.__dict__["_ym_last_plan"] = plan
+            plan.backward(rank, step)
+            sync.sync()
+            res.append([float(plan.grad_views[id(p)].mean()) for p in plan.params])
+        q.put((rank, res, None))
+        ydist.shutdown()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_gradsync_alternating_plans_world2_gloo():
+    res = _spawn(_alternate_worker)
+    for r in range(2):
+        for step, means in enumerate(res[r][1]):
+            for i, g in enumerate(means):
+                assert g == pytest.approx(1.5 * (i + 1) * (step + 1)), (r, step, i, g)
+
+
+class _Toy(torch.utils.data.Dataset):
+    def __init__(self, n):
+        self.n = n
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        return i
+
+
+def _loader_worker(rank, world, port, q, n, batch):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        import torch.distributed as dist
+        from yolomi import dist as ydist
+        import train_yolo11_cuda as T
+        ctx = ydist.init_from_env("gloo")
+        out = {}
+        for epoch in range(2):
+            tl, vl, sampler = T.make_loaders(_Toy(n), 0.2, batch, 0, 64, ctx, collate=lambda b: torch.tensor(b))
+            sampler.set_epoch(epoch)
+            steps = torch.tensor([0])
+            seen = []
+            for b in tl:
+                steps += 1
+                seen += b.tolist()
+                t = torch.ones(1)
+                dist.all_reduce(t)            # one collective per step, like GradSync: must never hang
+            out[epoch] = (int(steps), seen, [int(i) for b in vl for i in b.tolist()])
+        q.put((rank, out, None))
+        ydist.shutdown()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+@pytest.mark.parametrize("n,batch", [(101, 8), (37, 4)])
+def test_train_loader_equal_steps_and_val_shards_world2(n, batch):
+    """make_loaders (train_yolo11_cuda.py) with an odd dataset size: every rank takes the same number of
+    steps, the train shards are disjoint and reshuffled per epoch, the val shards cover the val set once."""
+    res = _spawn(_loader_worker, extra=(n, batch))
+    val_size = int(n * 0.2)
+    for epoch in range(2):
+        s0, s1 = res[0][1][epoch], res[1][1][epoch]
+        assert s0[0] == s1[0] > 0
+        assert not set(s0[1]) & set(s1[1])                      # disjoint train shards
+        assert len(s0[1]) == len(s1[1]) == (n - val_size) // 2
+        assert sorted(s0[2] + s1[2]) == sorted(set(s0[2] + s1[2])) and len(s0[2] + s1[2]) == val_size
+    assert res[0][1][0][1] != res[0][1][1][1]                 # set_epoch reshuffles
+
+
+def _gather_worker(rank, world, port, q, preds, targets):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from yolomi import dist as ydist
+        ctx = ydist.init_from_env("gloo")
+        mine = list(range(rank, len(preds), world))           # the ValShard of this rank
+        gp, gt = ydist.gather_detections([preds[i] for i in mine], [targets[i] for i in mine], ctx)
+        # numpy across the queue (torch tensors would travel as shared memory the exiting child owns)
+        npy = (lambda L: None if L is None else [{k: v.numpy() for k, v in d.items()} for d in L])
+        q.put((rank, (npy(gp), npy(gt)), None))
+        ydist.shutdown()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_gather_detections_world2_equals_single_process():
+    """Per-rank detections gathered to rank 0 reproduce the single-process list (order included), so
+    evaluate_detections (oracle restatement here, CPU) gives identical metrics."""
+    from oracle import metrics as omet
+    g = torch.Generator().manual_seed(4)
+    preds, targets = [], []
+    for i in range(11):                                  # odd image count, some empty images
+        k = int(torch.randint(0, 6, (1,), generator=g)) if i % 4 else 0
+        t = int(torch.randint(0, 4, (1,), generator=g))
+        c = torch.rand(t, 2, generator=g) * 0.8
+        tb = torch.cat((c, c + 0.1 + 0.1 * torch.rand(t, 2, generator=g)), 1)
+        src = tb[torch.randint(0, max(t, 1), (k,), generator=g)] if t else torch.rand(k, 4, generator=g)
+        preds.append({"boxes": (src + 0.01 * torch.randn(k, 4, generator=g)).clamp(0, 1),
+                      "scores": torch.rand(k, generator=g), "labels": torch.randint(0, 5, (k,), generator=g)})
+        targets.append({"boxes": tb, "labels": torch.randint(0, 5, (t,), generator=g)})
+    res = _spawn(_gather_worker, extra=(preds, targets))
+    assert res[1][1] == (None, None)
+    gp, gt = res[0][1]
+    gp = [{k: torch.from_numpy(v) for k, v in d.items()} for d in gp]
+    gt = [{k: torch.from_numpy(v) for k, v in d.items()} for d in gt]
+    assert len(gp) == len(preds) and len(gt) == len(targets)
+    for a, b in zip(gp, preds):
+        for k in ("boxes", "scores", "labels"):
+            assert torch.equal(a[k], b[k].reshape(a[k].shape)), k
+    for a, b in zip(gt, targets):
+        assert torch.equal(a["boxes"], b["boxes"]) and torch.equal(a["labels"], b["labels"])
+    assert omet.evaluate_detections(gp, gt, 0.25, 0.5) == omet.evaluate_detections(preds, targets, 0.25, 0.5)

@@ -1,0 +1,130 @@
+"""The entry point's functions end to end on the GPU (reference train_yolo11_cuda.py:31-262,
+440-451, 454-661): train_one_epoch against a hand-stepped loop of the same steps, validate against
+the loss and the metrics recomputed from its own inputs (evaluate_detections restated by the oracle),
+the cosine schedule, main --synthetic with checkpoint + resume, and the single-in-flight contract."""
+import copy
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _model():
+    from test_gpu_model import _seeded_model
+    return _seeded_model("n").train()
+
+
+def test_train_one_epoch_matches_hand_stepped_loop():
+    import train_yolo11_cuda as T
+    from losses import v8DetectionLoss
+    from yolomi.optim import FusedAdamW
+    from datasets import prepare_batch
+    loader = T._SyntheticLoader(3, 2, 256, seed=40)
+    m1 = _model()
+    m2 = copy.deepcopy(m1)
+    o1 = FusedAdamW(m1.parameters(), lr=1e-3, weight_decay=5e-4, max_grad_norm=10.0)
+    o2 = FusedAdamW(m2.parameters(), lr=1e-3, weight_decay=5e-4, max_grad_norm=10.0)
+    c1, c2 = v8DetectionLoss(m1), v8DetectionLoss(m2)
+    got = T.train_one_epoch(m1, loader, o1, c1, torch.device("cuda"), 1, 1)
+    assert set(got) == {"loss", "box_loss", "cls_loss", "dfl_loss"}
+    rows = []
+    for b in loader:                                  # the reference's loop body (:41-91), by hand
+        b = prepare_batch(b, torch.device("cuda"))
+        o2.zero_grad(set_to_none=True)
+        loss, items = c2(m2(b["img"]), b)
+        loss.backward()
+        o2.step()
+        rows.append([float(loss), *items.tolist()])
+    want = torch.tensor(rows, dtype=torch.float64).mean(0).tolist()
+    for k, w in zip(("loss", "box_loss", "cls_loss", "dfl_loss"), want):
+        assert got[k] == pytest.approx(w, rel=1e-6), (k, got[k], w)
+    for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.equal(a, b), k
+
+
+def test_validate_metrics_and_loss_from_its_own_predictions():
+    import train_yolo11_cuda as T
+    from losses import v8DetectionLoss
+    from datasets import prepare_batch
+    from oracle import metrics as omet
+    m = _model()
+    crit = v8DetectionLoss(m)
+    loader = T._SyntheticLoader(2, 3, 256, seed=50)
+    conf = 1e-7                      # the untrained head scores ~1e-6 (cls bias log(1e-6), Q4): keep candidates
+    vm = T.validate(m, loader, crit, torch.device("cuda"), conf_threshold=conf, iou_threshold=0.45)
+    assert not m.training
+    preds, tgts, rows = [], [], []
+    with torch.no_grad():
+        for b in loader:
+            b = prepare_batch(b, torch.device("cuda"))
+            y, feats = m(b["img"])
+            loss, items = crit((y, feats), b)
+            rows.append([float(loss), *items.tolist()])
+            preds += T.decode_predictions_for_metrics(y, b["img"].shape[-1], conf, 0.45, torch.device("cuda"))
+            for i in range(b["img"].shape[0]):
+                sel = b["batch_idx"] == i
+                tgts.append({"boxes": b["bboxes"][sel].cpu(), "labels": b["cls"][sel].reshape(-1).cpu()})
+    want = torch.tensor(rows, dtype=torch.float64).mean(0).tolist()
+    for k, w in zip(("loss", "box_loss", "cls_loss", "dfl_loss"), want):
+        assert vm[k] == pytest.approx(w, rel=1e-6), (k, vm[k], w)
+    assert sum(len(p["scores"]) for p in preds) > 0
+    ref = omet.evaluate_detections([{k: v.cpu() for k, v in p.items()} for p in preds], tgts, conf, 0.5)
+    for k in ("precision", "recall"):
+        assert vm[k] == ref[k], (k, vm[k], ref[k])
+    for k in ("mAP50", "mAP50-95"):
+        assert vm[k] == pytest.approx(ref[k], rel=1e-12, abs=1e-15), (k, vm[k], ref[k])
+
+
+def test_cosine_lr_schedule_reference_formula():
+    import math
+    import train_yolo11_cuda as T
+    opt = torch.optim.SGD([torch.nn.Parameter(torch.zeros(1))], lr=0.5)
+    for epoch in range(10):
+        lr = T.cosine_lr_schedule(opt, epoch, 10, lr_min=1e-5, lr_max=1e-3, warmup_epochs=3)
+        if epoch < 3:                                  # reference :440-451
+            want = 1e-5 + (1e-3 - 1e-5) * (epoch / 3)
+        else:
+            want = 1e-5 + (1e-3 - 1e-5) * 0.5 * (1 + math.cos(math.pi * (epoch - 3) / 7))
+        assert lr == want and opt.param_groups[0]["lr"] == want
+
+
+def test_main_synthetic_checkpoint_and_resume(tmp_path):
+    script = ROOT / "yolo-scratch_amd" / "train_yolo11_cuda.py"
+    args = [sys.executable, str(script), "--synthetic", "2", "--batch", "2", "--imgsz", "256", "--scale", "n",
+            "--save-dir", str(tmp_path), "--val-conf", "0.001"]
+    r = subprocess.run(args + ["--epochs", "1", "--resume", str(tmp_path / "none.pt")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Epoch 1/1" in r.stdout and (tmp_path / "last.pt").exists()
+    ck = torch.load(tmp_path / "last.pt", map_location="cpu", weights_only=True)
+    assert ck["epoch"] == 0 and set(ck["val_metrics"]) >= {"loss", "mAP50", "mAP50-95", "precision", "recall"}
+    r = subprocess.run(args + ["--epochs", "2", "--resume", str(tmp_path / "last.pt")], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Resumed from epoch 1" in r.stdout and "Epoch 2/2" in r.stdout
+    assert torch.load(tmp_path / "last.pt", map_location="cpu", weights_only=True)["epoch"] == 1
+
+
+def test_second_forward_before_backward_is_refused():
+    """Single-in-flight contract of a plan (yolomi.graph.Plan.check_generation)."""
+    from losses import v8DetectionLoss
+    from yolomi import YolomiError
+    from datasets.synthetic import synth_batch
+    m = _model()
+    crit = v8DetectionLoss(m)
+    b = {k: v.cuda() for k, v in synth_batch(2, 256, seed=3).items()}
+    l1, _ = crit(m(b["img"]), b)
+    l2, _ = crit(m(b["img"]), b)
+    with pytest.raises(YolomiError):
+        l1.backward()
+    m.eval()
+    with torch.no_grad():
+        y1, _ = m(b["img"])
+        keep = y1.clone()
+        m(b["img"] * 0.5)
+    assert torch.equal(y1, keep)                       # eval outputs are not overwritten by the next forward

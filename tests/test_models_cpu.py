@@ -124,12 +124,16 @@ def test_reference_layout_checkpoint_resumes(tmp_path):
             sd[k] = torch.randn(shape, generator=g)
     m = _model("s")
     opt_ref = _adamw_steps(_model("s"), n=1, seed=9)        # same module tree => same param indices
+    # the reference's evaluate_detections returns numpy scalars (np.sum / np.mean, utils/metrics.py:264-274)
+    # and they end up in val_metrics and best_mAP50 (train_yolo11_cuda.py:612-653)
+    import numpy as np
+    vm = {"loss": 3.5, "precision": 0.5, "recall": 0.25, "mAP50": np.float64(0.375), "mAP50-95": np.float64(0.125)}
     ck = {"epoch": 11, "model_state_dict": sd, "optimizer_state_dict": opt_ref.state_dict(),
-          "train_metrics": {"loss": 3.0}, "val_metrics": {"loss": 3.5}, "best_loss": 3.5, "best_mAP50": 0.0}
+          "train_metrics": {"loss": 3.0}, "val_metrics": vm, "best_loss": 3.5, "best_mAP50": np.float64(0.375)}
     torch.save(ck, tmp_path / "ref_last.pt")
     opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=5e-4)
     ep, bl, bm = T.resume_checkpoint(tmp_path / "ref_last.pt", m, opt, torch.device("cpu"))
-    assert (ep, bl, bm) == (12, 3.5, 0.0)
+    assert (ep, bl, bm) == (12, 3.5, 0.375)
     for k, v in sd.items():
         assert torch.equal(m.state_dict()[k], v), k
     assert len(opt.state_dict()["state"]) == len(opt_ref.state_dict()["state"])

@@ -71,8 +71,13 @@ def train_one_epoch(model, dataloader, optimizer, criterion, device, epoch, epoc
 
 
 @torch.no_grad()
-def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_threshold=0.45, max_batches=None):
-    """Validation + metrics (reference :101-262)."""
+def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_threshold=0.45, max_batches=None,
+             dp=None):
+    """Validation + metrics (reference :101-262).  Under data parallelism (`dp`, a GradSync) each
+    rank evaluates its ValShard of the val set (decode + NMS on its own GPU), the per-image
+    detections are gathered to rank 0 in the global image order and evaluate_detections runs there
+    (SURVEY §8(e)); the loss sums are all-reduced and the metrics broadcast, so every rank returns
+    the same dict."""
     model.eval()
     sums = torch.zeros(4, device=device)
     all_predictions, all_targets = [], []
@@ -98,10 +103,25 @@ def validate(model, dataloader, criterion, device, conf_threshold=0.25, iou_thre
         batches += 1
         if max_batches is not None and batches >= max_batches:
             break
-    # predictions and targets stay in HBM: the metrics run on the GPU (utils/metrics.py)
-    metrics = evaluate_detections(all_predictions, all_targets, conf_threshold=conf_threshold, iou_threshold=0.5)
-    nb = batches if max_batches else len(dataloader)
-    s = (sums / max(nb, 1)).tolist()
+    nb = torch.tensor([float(batches)], device=device)
+    world = dp.ctx.world if dp is not None else 1
+    if world > 1:
+        import torch.distributed as tdist
+        from yolomi.dist import gather_detections
+        tdist.all_reduce(sums)
+        tdist.all_reduce(nb)
+        all_predictions, all_targets = gather_detections(all_predictions, all_targets, dp.ctx, device)
+    keys = ("precision", "recall", "mAP50", "mAP50-95")
+    if all_predictions is not None:
+        # predictions and targets stay in HBM: the metrics run on the GPU (utils/metrics.py)
+        metrics = evaluate_detections(all_predictions, all_targets, conf_threshold=conf_threshold, iou_threshold=0.5)
+    if world > 1:
+        mt = torch.tensor([float(metrics[k]) for k in keys] if all_predictions is not None else [0.0] * 4,
+                          dtype=torch.float64, device=device)
+        tdist.broadcast(mt, 0)
+        metrics = dict(zip(keys, mt.tolist()))
+    nbatch = float(nb) if (max_batches or world > 1) else len(dataloader)
+    s = (sums / max(nbatch, 1)).tolist()
     return {"loss": s[0], "box_loss": s[1], "cls_loss": s[2], "dfl_loss": s[3], **metrics}
 
 
@@ -152,17 +172,66 @@ def make_checkpoint(epoch, model, optimizer, train_metrics, val_metrics, best_lo
             "best_mAP50": best_mAP50}
 
 
+def _np_safe_globals():
+    """numpy scalar reconstructors a reference-written checkpoint needs: its evaluate_detections
+    returns np.float64 mAP values (utils/metrics.py:264-274) that end up in val_metrics and
+    best_mAP50.  These rebuild plain numbers; nothing else is allowed through the restricted loader."""
+    import numpy as np
+    out = [np.dtype, type(np.dtype(np.float64)), type(np.dtype(np.float32)), type(np.dtype(np.int64))]
+    for mod in ("numpy._core.multiarray", "numpy.core.multiarray"):
+        try:
+            m = __import__(mod, fromlist=["scalar"])
+            out.append(m.scalar)
+            break
+        except (ImportError, AttributeError):
+            continue
+    return out
+
+
+
+def _load_np_safe(path, device):
+    with torch.serialization.safe_globals(_np_safe_globals()):
+        return torch.load(path, map_location=device, weights_only=True)
+
+
 def resume_checkpoint(path, model, optimizer, device):
     """Resume as the reference does (:576-586) -> (start_epoch, best_loss, best_mAP50).  Loaded with
-    weights_only=True (the dict holds tensors, numbers and metric dicts only); the optimizer keeps
-    this process's fused/foreach implementation choice across a reference-written state."""
-    ckpt = torch.load(path, map_location=device, weights_only=True)
+    weights_only=True plus the numpy scalar types a reference-written checkpoint holds (its metrics
+    are np.float64); the optimizer keeps this process's fused/foreach implementation choice across a
+    reference-written state."""
+    ckpt = _load_np_safe(path, device)
     model.load_state_dict(ckpt["model_state_dict"])
     impl = [{k: g.get(k) for k in ("fused", "foreach")} for g in optimizer.param_groups]
     optimizer.load_state_dict(ckpt["optimizer_state_dict"])
     for g, kv in zip(optimizer.param_groups, impl):
         g.update(kv)
     return ckpt["epoch"] + 1, ckpt.get("best_loss", float("inf")), ckpt.get("best_mAP50", 0.0)
+
+
+def make_loaders(dataset, val_split, batch, workers, imgsz, dp_ctx=None, collate=None):
+    """The reference's split and loaders (:491-543): seed-42 permutation, Subset train / val,
+    shuffled train loader, ordered val loader, drop_last=False.  Under data parallelism the train set
+    is sharded by a DistributedSampler(shuffle=True, drop_last=True): every rank gets the same number
+    of samples and so the same number of batches (a rank with one batch more would enter the gradient
+    all-reduce alone and hang), reshuffled every epoch (set_epoch); the val set by ValShard (no
+    padding: no image counted twice).  -> (train_loader, val_loader, train_sampler or None)."""
+    import functools
+    from torch.utils.data import DataLoader, DistributedSampler, Subset
+    n = len(dataset)
+    val_size = int(n * val_split)
+    idx = torch.randperm(n, generator=torch.Generator().manual_seed(42)).tolist()
+    tr, va = Subset(dataset, idx[: n - val_size]), Subset(dataset, idx[n - val_size:])
+    nw = min(workers, 4)
+    col = collate or functools.partial(collate_fn, img_size=imgsz)
+    kw = dict(batch_size=batch, num_workers=nw, collate_fn=col, pin_memory=torch.cuda.is_available(),
+              persistent_workers=nw > 0, prefetch_factor=2 if nw > 0 else None, drop_last=False)
+    if dp_ctx is not None and dp_ctx.world > 1:
+        from yolomi.dist import ValShard
+        sampler = DistributedSampler(tr, num_replicas=dp_ctx.world, rank=dp_ctx.rank, shuffle=True, seed=0,
+                                     drop_last=True)
+        return (DataLoader(tr, sampler=sampler, **kw),
+                DataLoader(va, sampler=ValShard(len(va), dp_ctx.rank, dp_ctx.world), **kw), sampler)
+    return DataLoader(tr, shuffle=True, **kw), DataLoader(va, shuffle=False, **kw), None
 
 
 class _SyntheticLoader:
@@ -214,22 +283,12 @@ def main():
         seed = 1000 * (dp_ctx.rank if dp_ctx else 0)
         train_loader = _SyntheticLoader(args.synthetic, args.batch, args.imgsz, seed)
         val_loader = _SyntheticLoader(max(1, args.synthetic // 5), args.batch, args.imgsz, seed + 10 ** 6)
+        train_sampler = None
     else:
         from datasets import CraterDatasetCUDA
-        from torch.utils.data import DataLoader, Subset
         dataset = CraterDatasetCUDA(args.data, img_size=args.imgsz, cache_images=False, augment=True)
-        val_size = int(len(dataset) * args.val_split)
-        idx = torch.randperm(len(dataset), generator=torch.Generator().manual_seed(42)).tolist()
-        tr, va = Subset(dataset, idx[: len(dataset) - val_size]), Subset(dataset, idx[len(dataset) - val_size:])
-        if dp_ctx:
-            tr = Subset(tr, list(range(dp_ctx.rank, len(tr), dp_ctx.world)))
-        nw = min(args.workers, 4)
-        import functools
-        kw = dict(batch_size=args.batch, num_workers=nw, collate_fn=functools.partial(collate_fn, img_size=args.imgsz),
-                  pin_memory=True,
-                  persistent_workers=nw > 0, prefetch_factor=2 if nw > 0 else None, drop_last=False)
-        train_loader = DataLoader(tr, shuffle=True, **kw)
-        val_loader = DataLoader(va, shuffle=False, **kw)
+        train_loader, val_loader, train_sampler = make_loaders(dataset, args.val_split, args.batch, args.workers,
+                                                               args.imgsz, dp_ctx)
 
     import yaml
     with open(args.cfg) as f:
@@ -259,9 +318,13 @@ def main():
     for epoch in range(start_epoch, args.epochs):
         lr = cosine_lr_schedule(optimizer, epoch, args.epochs, lr_min=args.lr * 0.01, lr_max=args.lr, warmup_epochs=3)
         criterion.epoch = epoch
+        if train_sampler is not None:
+            train_sampler.set_epoch(epoch)
         tm = train_one_epoch(model, train_loader, optimizer, criterion, device, epoch + 1, args.epochs, dp)
+        if dp:
+            dp.sync_buffers()          # rank 0's BN running statistics for validation and the checkpoint
         vm = validate(model, val_loader, criterion, device, conf_threshold=args.val_conf, iou_threshold=0.45,
-                      max_batches=args.max_val_batches)
+                      max_batches=args.max_val_batches, dp=dp)
         if not rank0:
             continue
         print(f"\nEpoch {epoch + 1}/{args.epochs} | LR: {lr:.6f}")

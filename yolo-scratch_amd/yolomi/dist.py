@@ -126,24 +126,30 @@ class Buckets:
 
 
 class GradSync:
-    """Average the model's gradients across ranks; bucketed and overlapped with the backward."""
+    """Average the model's gradients across ranks; bucketed and overlapped with the backward.
+
+    One Buckets object (and one backward hook) per plan: a model runs one plan per input shape
+    (e.g. a partial last batch), and each plan's hook launches that plan's buckets only."""
 
     def __init__(self, model: torch.nn.Module, ctx: DPContext, bucket_mb: float = 8.0):
         self.model, self.ctx = model, ctx
         self.cap = int(bucket_mb * (1 << 20))
-        self.plan, self.buckets = None, None
+        self.buckets = {}          # id(plan) -> Buckets (None: plan replays a HIP graph, no hooks)
+        self._plans = {}           # id(plan) -> plan (keeps the ids valid)
 
     def _attach(self, plan):
-        """Hook the plan's backward so the NEXT backward launches buckets as it goes.  A plan that
+        """Hook the plan's backward so its NEXT backward launches buckets as it goes.  A plan that
         replays its backward as a HIP graph takes no hooks: its gradient is all-reduced in one
-        collective after the backward (sync's first-step path, every step)."""
+        collective after the backward, every step."""
+        self._plans[id(plan)] = plan
         if getattr(plan, "graph_active", False):
+            self.buckets[id(plan)] = None
             return
-        self.plan = plan
-        self.buckets = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
-        self.buckets.streams = getattr(plan, "comm_streams", None)
+        b = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
+        b.streams = getattr(plan, "comm_streams", None)
+        self.buckets[id(plan)] = b
 
-        def hook(params, _b=self.buckets):
+        def hook(params, _b=b):
             if not _b.remaining:
                 _b.begin()
             _b.ready(params)
@@ -152,14 +158,17 @@ class GradSync:
     def sync(self):
         plan = self.model.__dict__.get("_ym_last_plan")
         if plan is not None:
-            if plan is self.plan and self.buckets.remaining:
-                self.buckets.finish(self.ctx.world)
-                self.buckets.remaining = []       # the next backward starts a new round
+            b = self.buckets.get(id(plan))
+            if b is not None and b.remaining:
+                # this plan's backward launched its buckets: wait for them, never reduce twice
+                b.finish(self.ctx.world)
+                b.remaining = []           # the next backward of this plan starts a new round
                 return
-            # first step on this plan: one collective now, buckets from the next step on
+            # first step on this plan (or a graph-replayed backward): one collective now
             dist.all_reduce(plan.grad_flat, op=dist.ReduceOp.SUM)
             plan.grad_flat.div_(self.ctx.world)
-            self._attach(plan)
+            if id(plan) not in self.buckets:
+                self._attach(plan)
             return
         # gradients not produced by a yolomi plan (CPU / gloo tests): bucket them in one flat tensor
         grads = [p.grad for p in self.model.parameters() if p.grad is not None]
@@ -179,3 +188,104 @@ class GradSync:
         with torch.no_grad():
             for t in list(self.model.parameters()) + list(self.model.buffers()):
                 dist.broadcast(t.data, src)
+
+    def sync_buffers(self, src: int = 0):
+        """Rank 0's BatchNorm running statistics everywhere.  Each rank's BN normalises with its own
+        batch statistics (plain BatchNorm2d under DDP) and updates its own running buffers; DDP's
+        default broadcast_buffers=True makes rank 0's the ones that count.  Called before every
+        validation and checkpoint (main), it gives every rank exactly rank 0's buffers — what DDP
+        leaves on rank 0 — at the only points the running statistics are read."""
+        with torch.no_grad():
+            for t in self.model.buffers():
+                dist.broadcast(t.data, src)
+
+
+# ----------------------------------------------------------------------------- data sharding
+class ValShard(torch.utils.data.Sampler):
+    """Validation shard without padding: rank r takes samples r, r + world, ... in order (a
+    DistributedSampler pads by repeating samples, which would count images twice in the mAP).
+    gather_detections() restores the global order on rank 0."""
+
+    def __init__(self, n: int, rank: int, world: int):
+        self.n, self.rank, self.world = n, rank, world
+
+    def __iter__(self):
+        return iter(range(self.rank, self.n, self.world))
+
+    def __len__(self):
+        return len(range(self.rank, self.n, self.world))
+
+
+def _pack(items, keys, widths):
+    """list of per-image dicts -> (counts (n,), {key: concatenated (rows, width) blocks})"""
+    counts = torch.tensor([len(it[keys[0]]) for it in items], dtype=torch.int64)
+    cols = {}
+    for k, w in zip(keys, widths):
+        parts = [it[k].reshape(len(it[keys[0]]), w) for it in items]
+        cols[k] = torch.cat(parts) if parts else None
+    return counts, cols
+
+
+def _all_gather_var(t: torch.Tensor, world: int):
+    """all_gather of a tensor whose first dimension differs per rank (padded to the max)."""
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x) for x in ns]
+    mx = max(ns)
+    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad)
+    return [o[:k] for o, k in zip(outs, ns)]
+
+
+def gather_detections(preds, targets, ctx: DPContext, device=None):
+    """Per-image prediction / target dicts of every rank's ValShard -> rank 0, in the global image
+    order (image i came from rank i % world, position i // world).  Non-zero ranks get (None, None).
+    SURVEY §8(e): AP is not decomposable across ranks, so the matching runs on rank 0."""
+    world, rank = ctx.world, ctx.rank
+    dev = device or (preds[0]["boxes"].device if preds else torch.device("cpu"))
+    pk = ("boxes", "scores", "labels")
+    tk = ("boxes", "labels")
+
+    def norm(items, keys):
+        out = []
+        for it in items:
+            d = {}
+            for k in keys:
+                v = it[k].to(dev)
+                d[k] = v.float() if k != "labels" else v.long()
+            out.append(d)
+        return out
+    preds, targets = norm(preds, pk), norm(targets, tk)
+    res = {}
+    for name, items, keys in (("p", preds, pk), ("t", targets, tk)):
+        widths = (4, 1, 1) if name == "p" else (4, 1)
+        counts, cols = _pack(items, keys, widths)
+        counts = counts.to(dev)
+        g_counts = _all_gather_var(counts, world)
+        g_cols = {}
+        for k, w in zip(keys, widths):
+            col = cols[k] if cols[k] is not None else torch.zeros(0, w, device=dev,
+                                                                 dtype=torch.int64 if k == "labels" else torch.float32)
+            g_cols[k] = _all_gather_var(col.reshape(-1, w), world)
+        res[name] = (g_counts, g_cols, keys)
+    if rank != 0:
+        return None, None
+
+    def unpack(g_counts, g_cols, keys):
+        per_rank = []
+        for r in range(world):
+            offs = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), g_counts[r].cumsum(0)]).tolist()
+            imgs = []
+            for j in range(len(g_counts[r])):
+                d = {}
+                for k in keys:
+                    v = g_cols[k][r][offs[j]:offs[j + 1]]
+                    d[k] = v if k == "boxes" else v.reshape(-1)
+                imgs.append(d)
+            per_rank.append(imgs)
+        n = sum(len(x) for x in per_rank)
+        return [per_rank[i % world][i // world] for i in range(n)]
+    return unpack(*res["p"]), unpack(*res["t"])

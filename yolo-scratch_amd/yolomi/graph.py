@@ -892,6 +892,21 @@ class Plan:
         self._run(list(reversed(ops)), "bwd", (lambda op: hook(op_params(op))) if hook is not None else None)
         self._join_side()
 
+    # --------------------------------------------------------------- single-in-flight contract
+    # A plan owns ONE set of activation buffers per input shape: a second forward of the same shape
+    # overwrites what the first one's backward needs.  Each forward takes a generation number and the
+    # backward refuses to run on a plan that has since run a newer forward (the reference's autograd
+    # graph would keep both sets alive; this path keeps one and says so instead of returning wrong
+    # gradients).
+    def new_generation(self):
+        self.gen = getattr(self, "gen", 0) + 1
+        return self.gen
+
+    def check_generation(self, gen):
+        if gen != getattr(self, "gen", 0):
+            raise YolomiError("backward of a forward whose activations a newer forward of the same input shape has "
+                              "overwritten: run backward (or detach the outputs) before the next forward")
+
     def install_grads(self):
         """Expose the flat buffer as parameter .grad (accumulating if a grad already exists)."""
         for p in self.params:
@@ -1097,12 +1112,13 @@ class _ModelFn(torch.autograd.Function):
     def forward(ctx, img, anchor, plan):
         plan.img = img.contiguous()
         plan.forward()
-        ctx.plan = plan
+        ctx.plan, ctx.gen = plan, plan.new_generation()
         return plan.head.detach()
 
     @staticmethod
     def backward(ctx, dhead):
         plan = ctx.plan
+        plan.check_generation(ctx.gen)
         plan.dhead = dhead.contiguous()
         plan.backward()
         plan.install_grads()
@@ -1119,13 +1135,14 @@ class _BlockFn(torch.autograd.Function):
         else:
             plan.input.act.t.copy_(x.permute(0, 2, 3, 1))
         plan.forward()
-        ctx.plan = plan
+        ctx.plan, ctx.gen = plan, plan.new_generation()
         out = plan.output.act.t[..., plan.output.c0:plan.output.c0 + plan.output.c]
         return out.permute(0, 3, 1, 2).float().contiguous()
 
     @staticmethod
     def backward(ctx, dy):
         plan = ctx.plan
+        plan.check_generation(ctx.gen)
         o = plan.output
         g = o.act.grad()
         g[..., o.c0:o.c0 + o.c].copy_(dy.permute(0, 2, 3, 1))
@@ -1184,13 +1201,14 @@ class _DetectFn(torch.autograd.Function):
         for v, x in zip(plan.inputs, xs):
             v.act.t.copy_(x.permute(0, 2, 3, 1))
         plan.forward()
-        ctx.plan = plan
+        ctx.plan, ctx.gen = plan, plan.new_generation()
         ctx.needs = [x.requires_grad for x in xs]
         return plan.head.clone()
 
     @staticmethod
     def backward(ctx, dhead):
         plan = ctx.plan
+        plan.check_generation(ctx.gen)
         plan.dhead = dhead.contiguous()
         plan.backward_from_head()
         plan.install_grads()
@@ -1235,6 +1253,7 @@ def run_detect(det, xs):
         for v, x in zip(plan.inputs, xs32):
             v.act.t.copy_(x.permute(0, 2, 3, 1))
         plan.forward()
+        plan.new_generation()
         head = plan.head.clone()
     return head, plan
 
@@ -1264,5 +1283,7 @@ def run_model(model, img: torch.Tensor):
     else:
         plan.img = img32.contiguous()
         plan.forward()
-        head = plan.head
+        plan.new_generation()
+        # a fresh tensor: the plan's buffer is rewritten by the next forward of this shape
+        head = plan.head.clone()
     return head, plan
