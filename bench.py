@@ -7,9 +7,11 @@ forward (HIP plan) + v8 loss (fused kernels) + backward + RCCL gradient all-redu
 
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torchrun)
 
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel (the conv implicit-GEMM
-forward of the heaviest layer) timed live with HIP events on the launch stream;
-`roofline_step` prices the whole step against the same bf16 MFMA peak.  `cpu_baseline`
+Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel family by time (every conv
+forward / data-gradient / weight-gradient launch of a step bracketed with HIP events on its own
+stream); `roofline_probe` is the heaviest single conv launch (HIP events on the launch stream,
+HBM traffic from the committed counter pass); `roofline_step` prices the whole step against the
+same 16-bit MFMA peak.  `cpu_baseline`
 times the CPU oracle restatement (test infrastructure, fp32) on a bounded sample of the
 same workload on this host's cores.
 """
@@ -51,7 +53,7 @@ def traffic_for(key: str):
     return e["bytes_per_launch"] if e else None
 
 
-def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 1, steps: int = 2):
+def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 2, steps: int = 3):
     """Oracle (fp32 CPU restatement of the reference) train step on a bounded sample."""
     import torch
     from oracle import model as om
@@ -83,8 +85,8 @@ def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 1, steps: int =
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="images per GPU")
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--scale", default="s")
@@ -195,13 +197,25 @@ def main():
         step(args.warmup + args.steps + i)
     torch.cuda.synchronize()
     plan.probe = None
+    # kernel families by time: every ConvBN's forward / data-gradient / weight-gradient launch bracketed
+    # with HIP events on its own stream over PROBE_STEPS steps (the step's busiest kernels)
+    plan.family_events = {"fwd": [], "dgrad": [], "wgrad": []}
+    for i in range(PROBE_STEPS):
+        step(args.warmup + args.steps + PROBE_STEPS + i)
+    torch.cuda.synchronize()
+    fams = {}
+    for kind, evs in plan.family_events.items():
+        ms = sum(a.elapsed_time(b) for a, b, _ in evs) / PROBE_STEPS
+        fl = sum(op.flops() for _, _, op in evs) / PROBE_STEPS
+        fams[kind] = (ms, fl, len(evs) // PROBE_STEPS)
+    plan.family_events = None
     # host time to enqueue one step (Python + ctypes launches) vs its wall time: a step whose
     # enqueue time approaches its wall time leaves the GPU waiting on the host
     host = []
     for i in range(3):
         torch.cuda.synchronize()
         h0 = time.perf_counter()
-        step(args.warmup + args.steps + PROBE_STEPS + i)
+        step(args.warmup + args.steps + 2 * PROBE_STEPS + i)
         host.append(time.perf_counter() - h0)
     torch.cuda.synchronize()
     host_ms = 1e3 * sorted(host)[1]
@@ -235,6 +249,20 @@ def main():
         roof = {"bound": "mfma", "achieved": round(dom_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4)}
     step_tf = value / world * per_img / 1e12
+    # the dominant kernel family by time (per step: summed launch durations, algorithmic FLOPs)
+    fam_kind = max(fams, key=lambda k: fams[k][0])
+    f_ms, f_fl, f_n = fams[fam_kind]
+    f_tf = f_fl / (f_ms * 1e-3) / 1e12 if f_ms > 0 else 0.0
+    names = {"fwd": "conv forward (implicit GEMM / halo / pipelined kernels)",
+             "dgrad": "conv data gradient (implicit GEMM / halo / pipelined kernels)",
+             "wgrad": "conv weight gradient (wgrad3 / wgrad1 + split-K reduce)"}
+    roof_family = {"bound": "mfma", "achieved": round(f_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                   "frac": round(f_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic_for(f"family {fam_kind} bs{args.batch}"),
+                   "kernel": f"{names[fam_kind]}: {f_n} launches per step, {f_fl / 1e9:.0f} GFLOP algorithmic in "
+                             f"{f_ms:.3f} ms summed launch time (HIP events on each launch's stream, {PROBE_STEPS} steps)",
+                   "families_ms_per_step": {k: round(v[0], 3) for k, v in fams.items()},
+                   "families_frac": {k: round(v[1] / (v[0] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4) if v[0] > 0 else 0.0
+                                     for k, v in fams.items()}}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -246,13 +274,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16",
+        "dtype": "fp16 fwd / bf16 bwd (fp32 accumulate, fp32 loss + optimizer)",
         "data": "synthetic (640x640 uniform images, 1-20 log-uniform boxes/img, seeded per rank)",
         "config": {"workload": f"YOLOv11-{args.scale} {args.imgsz}x{args.imgsz} train step "
                                f"(fwd+loss+bwd+allreduce+clip+AdamW)",
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch, "imgsz": args.imgsz,
                    "parallelism": f"dp{world}"},
-        "roofline": {**roof, "traffic": traffic_for(probe_key),
+        "roofline": roof_family,
+        "roofline_probe": {**roof, "traffic": traffic_for(probe_key),
                      "kernel": f"conv_gemm_kernel fwd {dom.m.__class__.__name__} {dom.ci}->{dom.co} "
                                f"k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W}, {dom.flops() / 1e9:.1f} GFLOP and "
                                f"{alg_bytes / 1e6:.0f} MB algorithmic per launch, {kern_ms:.3f} ms avg over "

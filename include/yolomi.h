@@ -12,8 +12,9 @@
  *  - All pointers are DEVICE pointers unless stated; buffers are allocated by
  *    the caller (PyTorch caching allocator); the library never allocates or
  *    frees caller memory and keeps no TENSOR state between calls.  The only
- *    process-wide state is configuration and diagnostics: the halo-kernel
- *    selection policy (ym_conv_set_halo / YM_CONV_HALO, read once) and the
+ *    process-wide state is configuration and diagnostics: the conv kernel
+ *    selection policies (ym_conv_set_halo / ym_conv_set_pipe, YM_CONV_HALO / YM_CONV_PIPE read
+ *    once) and the
  *    NMS segment counters (ym_debug_nms_stamps, written when YM_NMS_STAMPS is
  *    set); neither changes a result.
  *  - `stream` is a hipStream_t (0 = legacy default stream); every call is
@@ -144,13 +145,17 @@ int ym_conv_stat_blocks(int64_t m, int cout);
 /* Rows of the BN statistics partials ym_conv_fwd writes for this conv (the halo-staged 3x3
  * kernel and the implicit GEMM use different grids); size stat_sum / stat_sq with it. */
 int ym_conv_fwd_stat_rows(const ym_conv_desc* d);
-/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 1 = the
- * halo-staged 3x3 stride-1 kernel, 0 = the implicit GEMM. */
+/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 2 = the persistent
+ * pipelined implicit GEMM, 1 = the halo-staged 3x3 stride-1 kernel, 0 = the 2-stage implicit GEMM. */
 int ym_conv_algo(const ym_conv_desc* d, int dgrad);
 /* Selection policy of the halo-staged kernel for later calls: -1 YM_CONV_HALO / default, 0 never,
  * 1 wherever it applies, 2 where it measured faster (default: maps <= 24 wide).  Returns the
  * previous setting.  Process-wide; not for use while other threads launch convolutions. */
 int ym_conv_set_halo(int mode);
+/* Selection policy of the persistent pipelined implicit GEMM (conv_pipe.hip) for later calls: -1
+ * YM_CONV_PIPE / default, 0 never, 1 layers of >= 1024 256-pixel tiles (default), 2 >= 256 tiles.
+ * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+int ym_conv_set_pipe(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
  * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,

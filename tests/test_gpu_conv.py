@@ -167,3 +167,84 @@ def test_dgrad_accumulate_stride2():
     torch.cuda.synchronize()
     err = float((dx.float().cpu() - ref).abs().max() / ref.abs().max())
     assert err < 1e-2
+
+
+# persistent pipelined implicit GEMM (conv_pipe.hip), forced on with ym_conv_set_pipe(2) (layers of
+# >= 256 tiles): 256 x 128 tiles (>= 128 output channels) and 256 x 64 tiles, 3x3 and 1x1, stride 2
+# forward and the 4-class stride-2 data gradient, partial pixel / channel tiles, strided channel views
+# (a conv reading / writing a slice of a concat buffer), fp16 + BN statistics / bf16 outputs, and
+# gradient accumulation
+PIPE = [
+    # n, h, w, cin, cout, k, stride, pad, in_extra, out_extra (extra channels of the surrounding view)
+    (16, 64, 64, 128, 128, 3, 1, 1, 0, 0),
+    (18, 61, 63, 128, 192, 3, 1, 1, 64, 8),
+    (16, 64, 64, 64, 128, 3, 1, 1, 0, 64),
+    (16, 128, 128, 64, 128, 3, 2, 1, 0, 0),
+    (16, 64, 64, 256, 128, 1, 1, 0, 128, 0),
+    (12, 80, 80, 64, 64, 3, 1, 1, 0, 0),
+]
+
+
+@pytest.mark.parametrize("shape", PIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in PIPE])
+def test_pipe_kernel_vs_torch(shape):
+    """fp16 forward (+ BN statistic partials), bf16 data gradient (overwrite, then accumulate)."""
+    from yolomi._lib import call, lib, ConvDesc
+    n, h, w, cin, cout, k, s, p, xe, ye = shape
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, oh, ow, cout, k, s, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * (cin + xe), cin + xe, oh * ow * (cout + ye), cout + ye
+    d.out_f32, d.accumulate = 2, 0
+    g = torch.Generator().manual_seed(hash(shape) & 0xFFFF)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, generator=g).half()
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    dz = torch.randn(n, oh, ow, cout, generator=g).bfloat16()
+    w16, wbf = wt.half(), wt.bfloat16()
+    prev = lib().ym_conv_set_pipe(2)
+    try:
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 2
+        assert lib().ym_conv_algo(ctypes.byref(d), 1) == 2
+        xbuf = torch.zeros(n, h, w, cin + xe, dtype=torch.float16, device=dev)
+        xbuf[..., :cin] = x.to(dev)
+        ybuf = torch.full((n, oh, ow, cout + ye), 7.0, dtype=torch.float16, device=dev)
+        rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+        ss = torch.full((rows, cout), float("nan"), device=dev)
+        sq = torch.full((rows, cout), float("nan"), device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        w_fwd = w16.permute(0, 2, 3, 1).contiguous().to(dev)
+        call("ym_conv_fwd", ctypes.byref(d), xbuf.data_ptr(), w_fwd.data_ptr(), ybuf.data_ptr(), None,
+             ss.data_ptr(), sq.data_ptr(), st)
+        # dgrad: dz in the output view, dx into the input view (overwrite, then accumulate a second copy)
+        dzbuf = torch.zeros(n, oh, ow, cout + ye, dtype=torch.bfloat16, device=dev)
+        dzbuf[..., :cout] = dz.to(dev)
+        dxbuf = torch.full((n, h, w, cin + xe), float("nan"), dtype=torch.bfloat16, device=dev)
+        dxbuf[..., cin:] = 3.0
+        w_t = wbf.permute(1, 2, 3, 0).contiguous().to(dev)
+        dd = ConvDesc.from_buffer_copy(d)
+        call("ym_conv_dgrad", ctypes.byref(dd), dzbuf.data_ptr(), w_t.data_ptr(), dxbuf.data_ptr(), st)
+        dx1 = dxbuf.clone()
+        dd.accumulate = 1
+        call("ym_conv_dgrad", ctypes.byref(dd), dzbuf.data_ptr(), w_t.data_ptr(), dxbuf.data_ptr(), st)
+        torch.cuda.synchronize()
+    finally:
+        lib().ym_conv_set_pipe(prev)
+    y_ref = F.conv2d(x.float().permute(0, 3, 1, 2), w16.float(), stride=s, padding=p).permute(0, 2, 3, 1)
+    dx_ref = torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz.float().permute(0, 3, 1, 2),
+                                        stride=s, padding=p).permute(0, 2, 3, 1)
+
+    def rel(a, b):
+        return float((a.float().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+    yc = ybuf.cpu()
+    assert rel(yc[..., :cout], y_ref) < 2e-3                       # one fp16 rounding
+    assert (yc[..., cout:] == 7.0).all()                           # the rest of the view untouched
+    ref_sum, ref_sq = y_ref.reshape(-1, cout).sum(0), (y_ref.reshape(-1, cout) ** 2).sum(0)
+    # per-channel sums can cancel to ~0: bound by the sum of magnitudes
+    assert float((ss.sum(0).cpu() - ref_sum).abs().max()) < 1e-4 * float(y_ref.abs().reshape(-1, cout).sum(0).max())
+    assert rel(sq.sum(0), ref_sq) < 1e-3
+    d1 = dx1.float().cpu()
+    assert torch.isfinite(d1).all()
+    assert rel(d1[..., :cin], dx_ref) < 1e-2
+    assert (d1[..., cin:] == 3.0).all()
+    assert rel(dxbuf[..., :cin], 2 * dx_ref) < 1e-2

@@ -29,6 +29,7 @@
 
 #include "common.h"
 #include "conv_halo.h"
+#include "conv_pipe.h"
 #include "reduce.h"
 #include "tile.h"
 
@@ -753,23 +754,13 @@ using namespace ym;
 
 struct Tile {
     int bm, bn;
-    int deep = 0;    // 256x128 on 4 waves of 64 channels x 128 pixels (YM_CONV_TILE=2564)
 };
 
-// Large problems: 256 x 128 tiles on 8 waves (a quarter fewer operand bytes per FLOP than 128x128,
-// the L2 -> LDS stream being what bounds this kernel; 256 x 256 does not fit 256 VGPRs per lane).  Otherwise 128-pixel tiles with the widest
-// channel tile that still gives >= 1.5 workgroups per CU (small late layers: 20x20 maps).
-// Measured (tools/layer_bench.py, s@640 bs64): 256 x 128 tiles are 9 % slower in sum than
-// 128 x 128 at this kernel's pipeline depth, so they are opt-in: YM_CONV_TILE=256.
+// 128-pixel tiles with the widest channel tile that still gives >= 1.5 workgroups per CU (small late
+// layers: 20x20 maps).  The large layers' 256 x 128 tiles live in conv_pipe.hip (persistent,
+// 3-stage LDS-DMA ring): at this kernel's pipeline depth they measured 9 % slower in sum than
+// 128 x 128 (tools/layer_bench.py, s@640 bs64), so the former opt-in here is gone.
 static Tile pick_tile(int64_t Mc, int classes, int nout) {
-    static const int use256 = [] {
-        const char* e = getenv("YM_CONV_TILE");
-        return e ? atoi(e) : 0;
-    }();
-    // YM_CONV_TILE=256: 8 waves of 64x64; YM_CONV_TILE=2564: 4 waves of 64 channels x 128 pixels
-    // (32-deep stages, 3-stage ring, 72 KB: two workgroups per CU)
-    if (nout >= 128 && use256 && ((Mc + 255) / 256) * classes * ((nout + 127) / 128) >= 512)
-        return {256, 128, use256 == 2564};
     const int64_t blocks_per_ntile = ((Mc + 127) / 128) * classes;
     int bn = nout >= 128 ? 128 : (nout >= 64 ? 64 : 32);
     while (bn > 32 && blocks_per_ntile * ((nout + bn - 1) / bn) < 384) bn >>= 1;
@@ -778,8 +769,6 @@ static Tile pick_tile(int64_t Mc, int classes, int nout) {
 
 template <int KB, int NS, int MODE>
 static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
-    if (t.bm == 256 && t.deep) return launch_gemm<256, 128, 2, 2, 32, 3, MODE>(a, max_blocks, st);
-    if (t.bm == 256) return launch_gemm<256, 128, 2, 4, KB, NS, MODE>(a, max_blocks, st);
     if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
     if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
     // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
@@ -829,14 +818,26 @@ extern "C" int ym_conv_set_halo(int mode) {
     return prev;
 }
 
+extern "C" int ym_conv_set_pipe(int mode) {
+    // selection policy of the pipelined implicit GEMM: -1 env/default, 0 never, 1 layers of >= 1024
+    // tiles (default), 2 >= 256 tiles; returns the previous setting
+    const int prev = g_pipe_force;
+    g_pipe_force = mode < -1 || mode > 2 ? -1 : mode;
+    return prev;
+}
+
 extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
-    // 1: halo-staged 3x3 kernel (conv_halo.hip), 0: implicit GEMM
+    // 2: persistent pipelined implicit GEMM (conv_pipe.hip), 1: halo-staged 3x3 kernel
+    // (conv_halo.hip), 0: 2-stage implicit GEMM
+    if (d && pipe_plan(d, dgrad ? 1 : 0).ok) return 2;
     return d && halo_plan(d, dgrad ? 1 : 0).ok ? 1 : 0;
 }
 
 extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     // rows of the BN statistics partials ym_conv_fwd writes for this conv (halo or implicit-GEMM grid)
     if (!d) return 0;
+    const PipePlan pp = pipe_plan(d, 0);
+    if (pp.ok) return pp.rows;
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) return hp.gx;
     return ym_conv_stat_blocks(int64_t(d->n) * d->oh * d->ow, d->cout);
@@ -865,6 +866,12 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
+    const PipePlan pp = pipe_plan(d, 0);
+    if (pp.ok) {
+        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_fwd (pipe)");
+        return YM_OK;
+    }
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) {
         halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
@@ -900,6 +907,12 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->y_bs, int64_t(d->h / d->stride) * (d->w / d->stride)),
                  "ym_conv_dgrad: gradient image stride too large");
+    const PipePlan pp = pipe_plan(d, 1);
+    if (pp.ok) {
+        pipe_launch(pp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_dgrad (pipe)");
+        return YM_OK;
+    }
     const HaloPlan hp = halo_plan(d, 1);
     if (hp.ok) {
         halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));

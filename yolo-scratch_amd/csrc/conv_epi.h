@@ -1,0 +1,83 @@
+// Conv epilogue shared by the pipelined implicit GEMM (conv_pipe.hip) and the halo-staged 3x3
+// kernel (conv_halo.hip): MFMA accumulators -> BatchNorm statistics -> 16-bit NHWC stores.
+//
+// A 16x16 MFMA accumulator gives each lane 4 consecutive channels of ONE pixel, so storing it
+// straight out costs one 8-B store per (subtile, lane), 16 pixels x 32 B per instruction: scattered
+// partial-line writes whose issue and drain held a 256 x 128 tile's epilogue at ~40 % of the tile's
+// time (measured, tools/pipe_abl.sh ablation 5).  Here each 16-pixel slice of the wave's
+// accumulators is transposed through a small per-wave LDS area (swizzled 16-B chunks: conflict-free
+// writes and reads) and stored as 16-B pieces of each pixel's contiguous channel run (8 lanes = 128 B),
+// with raw buffer stores whose out-of-tile pixels fall out of range (a fixed instruction count, no
+// branches).
+#pragma once
+#include "common.h"
+#include "tile.h"
+
+namespace ym {
+
+// acc[i][j][r]: channel wch0 + i*16 + fc*4 + r, wave-local pixel q = j*16 + fr (fc = lane>>4, fr = lane&15).
+// WCH = 16 * TM channels of this wave; ep: this wave's LDS area (16 * WCH * 2 bytes).
+// pix_off(q) -> byte offset of wave-local pixel q's channel wch0 in the output (OOB when the pixel
+// is outside the map / tile).  half: fp16 (1) or bf16 (0) output; accumulate: add into the bf16 output.
+template <int TM, int TN, class PixOff>
+__device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
+                                               bool stats, char* ep, int lane, int wch0, int nout,
+                                               __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
+                                               PixOff pix_off) {
+    constexpr int WCH = 16 * TM;
+    constexpr int CPR = WCH * 2 / 16;          // 16-B chunks per pixel row of this wave
+    constexpr int RPS = 64 / CPR;              // pixel rows per store instruction
+    static_assert(CPR >= 1 && CPR <= 8 && 16 % RPS == 0, "epilogue transpose geometry");
+    const int fc = lane >> 4, fr = lane & 15;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const bool pvalid = pix_off(j * 16 + fr) != OOB;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int cb = wch0 + i * 16 + fc * 4;
+            if (stats && pvalid) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (cb + r < nout) {
+                        const float v = acc[i][j][r];
+                        ssum[i][r] += v;
+                        ssq[i][r] += v * v;
+                    }
+            }
+            uint2 o;
+            if (half) {
+                o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
+                o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
+            } else {
+                o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
+                o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
+            }
+            const int byte = (i * 16 + fc * 4) * 2;                    // within the pixel row
+            const int chunk = (byte >> 4) ^ (fr & (CPR - 1));          // swizzled 16-B chunk
+            *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
+        }
+#pragma unroll
+        for (int h = 0; h < 16 / RPS; ++h) {
+            const int p = h * RPS + lane / CPR, c = lane % CPR;
+            uint4 v = *reinterpret_cast<const uint4*>(ep + p * (WCH * 2) + ((c ^ (p & (CPR - 1))) * 16));
+            uint32_t off = pix_off(j * 16 + p);
+            if (off != OOB) {
+                if (wch0 + c * 8 < nout) off += uint32_t(c) * 16u;
+                else off = OOB;
+            }
+            if (accumulate) {                                          // gradient fan-in (bf16)
+                const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
+                uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
+                                  bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
+                v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                   yres, off, 0, 0);
+        }
+    }
+}
+
+}  // namespace ym

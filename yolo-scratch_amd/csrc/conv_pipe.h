@@ -1,0 +1,24 @@
+// Persistent, software-pipelined implicit-GEMM convolution (conv_pipe.hip): applicability plan +
+// launch, used by ym_conv_fwd / ym_conv_dgrad in conv.hip ahead of the halo kernel and the
+// 2-stage implicit GEMM.
+#pragma once
+#include "common.h"
+
+namespace ym {
+
+struct PipePlan {
+    int ok;          // the pipelined kernel handles this conv
+    int cfg;         // tile configuration (conv_pipe.hip: kCfg)
+    int grid;        // workgroups (persistent; a multiple of 8 * channel tiles)
+    int rows;        // rows of the BN statistics partials (= grid / channel tiles)
+};
+
+// -1: YM_CONV_PIPE / default policy; 0 never; 1 layers of >= 1024 tiles; 2 >= 256 tiles (ym_conv_set_pipe)
+extern int g_pipe_force;
+
+// dgrad = 0: forward conv described by d; 1: its data gradient
+PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);
+int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st);
+
+}  // namespace ym

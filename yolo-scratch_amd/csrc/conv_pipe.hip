@@ -1,0 +1,600 @@
+// Persistent software-pipelined implicit-GEMM convolution for gfx950 (fp16 forward, bf16 data
+// gradient, fp32 accumulate) — the large 3x3 / 1x1 layers of the YOLOv11 graph.
+//
+// Replaces nn.Conv2d forward / input-gradient inside Conv (/root/reference/yolo_scratch_cuda/
+// models/yolo11_modules.py:21-33, Detect :221-234) where the GEMM is big enough to fill the chip.
+//
+// Why a second implicit GEMM (conv.hip keeps the 2-stage one for small / odd shapes): its
+// 128 x 128 tiles, one K stage in flight and one barrier + read burst per K step leave the MFMA
+// pipes 77 % idle (profiles/r01/pmc_op6): every K step opens with the LDS latency of its fragment
+// reads, and 64 B/cycle of staging per CU at peak is more than the TA delivers.  Here:
+//  * 256 pixels x 128 channels per tile, 8 waves of 64 x 64, K steps of 64 (two 32-deep halves):
+//    a third fewer staged bytes per FLOP than 128 x 128;
+//  * a 3-stage LDS ring filled by LDS-DMA (buffer_load ... lds) with TWO stages in flight, counted
+//    vmcnt waits and raw s_barrier (no vmcnt(0) drain in the loop);
+//  * the barrier sits in the MIDDLE of a K step: a step reads its second-half fragments, runs the
+//    first half's 16 MFMAs, waits for the next stage, barriers, issues the DMA into the buffer it
+//    has just finished with, reads the next stage's first-half fragments and runs the second half's
+//    16 MFMAs — every LDS read has 16 MFMAs to hide behind, the pipe never waits on a fresh read;
+//  * the K offset rides in the buffer instruction's SGPR soffset (channel counts are multiples of
+//    64): one DMA costs no VALU inside a tap;
+//  * persistent workgroups (one per CU) stream their tiles back to back: the next tile's first
+//    stages are in flight during the current tile's epilogue; tiles are grouped per XCD, the
+//    channel tiles of one pixel tile on the same XCD (input rows reused from its L2);
+//  * BatchNorm statistics accumulate in registers across a workgroup's tiles and are written as
+//    one partial row per workgroup (no atomics, fixed order: bit-reproducible).
+// The stride-2 data gradient runs as 4 output-parity classes inside the same tile stream, each
+// with only the taps that land (as conv.hip).
+#include <algorithm>
+#include <cstdlib>
+
+#include "common.h"
+#include "conv_pipe.h"
+#include "tile.h"
+
+namespace ym {
+
+// selection policy: -1 YM_CONV_PIPE / default (1); 0 never; 1 layers of >= 1024 tiles; 2 >= 256 tiles
+int g_pipe_force = -1;
+
+namespace {
+
+constexpr int PF = 0;   // forward: fp16 x fp16
+constexpr int PD = 1;   // data gradient: bf16 x bf16
+
+struct PipeArgs {
+    const bf16_t* x; int64_t x_bs, x_ld;     // gathered tensor view (elements)
+    const bf16_t* w;                          // [Nout][KH][KW][Kin]
+    void* y; int64_t y_bs, y_ld;              // output view
+    const float* bias;                        // [Nout] or null
+    float* st_sum; float* st_sq;              // [rows][Nout] or null
+    int GH, GW, Kin;
+    int OH, OW, Nout;
+    int KH, KW, stride, pad, N;
+    int out_f32, accumulate;
+    int os;                                   // 2: stride-2 data gradient (4 parity classes)
+    int ntiles;                               // channel tiles
+    int mt_pre[5];                            // first m-tile of each class (prefix), mt_pre[ncls] = total
+    int ncls;
+};
+
+struct Cls {
+    int py, px, OWc, kh0, kw0, nkw, ntap;
+    uint32_t OHW;
+    int64_t Mc;
+};
+
+__device__ __forceinline__ Cls cls_of(const PipeArgs& a, int c) {
+    Cls k;
+    const int os = a.os;
+    k.py = os == 2 ? (c >> 1) : 0;
+    k.px = os == 2 ? (c & 1) : 0;
+    const int OHc = (a.OH - k.py + os - 1) / os;
+    k.OWc = (a.OW - k.px + os - 1) / os;
+    k.kh0 = os == 2 ? ((k.py + a.pad) & 1) : 0;
+    k.kw0 = os == 2 ? ((k.px + a.pad) & 1) : 0;
+    k.nkw = (a.KW - k.kw0 + os - 1) / os;
+    k.ntap = ((a.KH - k.kh0 + os - 1) / os) * k.nkw;
+    k.OHW = uint32_t(OHc) * uint32_t(k.OWc);
+    k.Mc = int64_t(a.N) * k.OHW;
+    return k;
+}
+
+__device__ __forceinline__ int cls_find(const PipeArgs& a, int mt) {
+    int c = 0;
+    while (c + 1 < a.ncls && mt >= a.mt_pre[c + 1]) ++c;
+    return c;
+}
+
+__device__ __forceinline__ int fsw128(int r) { return (r >> 1) & 7; }
+
+// one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc + voff + soff land at lds + 16 l
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
+// every ds_read issued so far has returned, then the workgroup barrier (no vmcnt drain); the
+// sched_barriers keep the compiler from moving MFMAs / LDS reads across it
+__device__ __forceinline__ void step_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// issue side of the stage stream: which tile / tap / 64-channel chunk the next LDS-DMA stage
+// stages, and the per-lane gather offsets of the current tile and tap.  All control state is
+// wave-uniform (scalar registers); per stage the DMAs cost one M0 write each, per tap one
+// bounds select per gather row, per tile one pixel decomposition.
+template <int BM, int BN, int NW, int MODE>
+struct Issuer {
+    static constexpr int AI = BN / 8 / NW, BI = BM / 8 / NW, RB = 128;
+    const PipeArgs& a;
+    int wave, lrow, lslot, kc;
+    uint32_t xld_b;
+    int mt_lo, qstride, ntile;
+    // stream position
+    int i = 0, ti = 0, tj = 0, kci = 0;
+    // current tile
+    int nrows = 0, nkw = 1, kh0 = 0, kw0 = 0;
+    const bf16_t* x_tile = nullptr;
+    int x_bytes = 0;
+    int bh[BI], bw[BI];
+    uint32_t bc[BI], b_off[BI];
+    uint32_t a_tap = 0;
+
+    __device__ Issuer(const PipeArgs& a_, int wave_, int lane, int mt_lo_, int qstride_, int ntile_)
+        : a(a_), wave(wave_), lrow(lane >> 3), lslot(lane & 7), kc(a_.Kin >> 6), xld_b(uint32_t(a_.x_ld) * 2u),
+          mt_lo(mt_lo_), qstride(qstride_), ntile(ntile_) {}
+
+    __device__ __forceinline__ void tile_setup() {
+        const int mt = mt_lo + i * qstride;
+        const int c = cls_find(a, mt);
+        const Cls k = cls_of(a, c);
+        nkw = k.nkw;
+        nrows = k.ntap / k.nkw;
+        kh0 = k.kh0;
+        kw0 = k.kw0;
+        const int64_t m0 = int64_t(mt - a.mt_pre[c]) * BM;
+        const uint32_t nfirst = uint32_t(m0 / k.OHW);
+        x_tile = a.x + int64_t(nfirst) * a.x_bs;
+        const int64_t xb = (int64_t(a.N) - nfirst) * a.x_bs * 2;
+        x_bytes = int(xb < 0x7fffffff ? xb : 0x7fffffff);
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const int r = (wave * BI + j) * 8 + lrow;
+            const int64_t m = m0 + r;
+            if (m < k.Mc) {
+                const uint32_t um = uint32_t(m);
+                const uint32_t n = um / k.OHW, pix = um - n * k.OHW;
+                const uint32_t ii = pix / uint32_t(k.OWc);
+                const int oh = int(ii) * a.os + k.py, ow = int(pix - ii * uint32_t(k.OWc)) * a.os + k.px;
+                if (MODE == PF) {
+                    bh[j] = oh * a.stride - a.pad;
+                    bw[j] = ow * a.stride - a.pad;
+                } else {                        // the class's first tap lands on whole pixels
+                    bh[j] = (oh + a.pad - k.kh0) >> (a.stride - 1);
+                    bw[j] = (ow + a.pad - k.kw0) >> (a.stride - 1);
+                }
+                bc[j] = (n - nfirst) * uint32_t(a.x_bs) * 2u + uint32_t(bh[j] * a.GW + bw[j]) * xld_b +
+                        uint32_t(lslot ^ fsw128(r)) * 16u;
+            } else {
+                bh[j] = -(1 << 20);             // no tap is in range
+                bw[j] = 0;
+                bc[j] = 0;
+            }
+        }
+    }
+
+    __device__ __forceinline__ void tap_setup() {
+        const int dir = MODE == PF ? 1 : -1;
+        const int ost = MODE == PF ? 1 : a.stride;
+        const uint32_t delta = uint32_t(dir * (ti * a.GW + tj)) * xld_b;
+#pragma unroll
+        for (int j = 0; j < BI; ++j) {
+            const int gh = bh[j] + dir * ti, gw = bw[j] + dir * tj;
+            const bool ok = uint32_t(gh) < uint32_t(a.GH) && uint32_t(gw) < uint32_t(a.GW);
+            b_off[j] = ok ? bc[j] + delta : OOB;
+        }
+        a_tap = uint32_t(((kh0 + ti * ost) * a.KW + (kw0 + tj * ost)) * a.Kin) * 2u;
+    }
+
+    // one stage into `st`, then advance the stream position
+    template <int ABL>
+    __device__ __forceinline__ void issue(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off) {
+        if (kci == 0) tap_setup();
+        const uint32_t kb = uint32_t(kci) * 128u;
+        if constexpr (ABL < 2) {
+            // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
+            const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
+            const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
+            const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
+            const __amdgpu_buffer_rsrc_t xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
+                                                          __builtin_amdgcn_readfirstlane(x_bytes));
+#pragma unroll
+            for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, a_off[j], a_tap + kb);
+#pragma unroll
+            for (int j = 0; j < BI; ++j) dma16(xres, st + BN * RB + (wave * BI + j) * 1024, b_off[j], kb);
+        }
+        if (++kci == kc) {
+            kci = 0;
+            if (++tj == nkw) {
+                tj = 0;
+                if (++ti == nrows) {
+                    ti = 0;
+                    if (++i < ntile) tile_setup();
+                }
+            }
+        }
+    }
+};
+
+// ABL (timing ablations only, YM_PIPE_ABL): 1 = no MFMAs (fragments kept live), 2 = no DMA issue
+template <int BM, int BN, int WM, int WN, int MODE, int ABL = 0>
+__global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
+    constexpr int NS = 3;                     // LDS ring: stage g computing, g+1 and g+2 in flight
+    constexpr int RB = 128;                   // 64 K x 2 B per LDS row
+    constexpr int NW = WM * WN;
+    constexpr int AI = BN / 8 / NW;           // weight DMA instructions per wave per stage
+    constexpr int BI = BM / 8 / NW;           // activation DMA instructions per wave per stage
+    constexpr int DPS = AI + BI;              // DMAs per wave per stage (the vmcnt unit)
+    constexpr int TM = BN / WM / 16;          // 16-channel subtiles per wave
+    constexpr int TN = BM / WN / 16;          // 16-pixel subtiles per wave
+    constexpr int STAGE = (BM + BN) * RB;
+    static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile too small for 8-row DMA pieces");
+    // epilogue transpose area: 16 pixels x (BN / WM) channels x 2 B per wave, after the ring
+    constexpr int WCH = BN / WM;                          // channels per wave
+    constexpr int EPW = 16 * WCH * 2;                     // bytes per wave
+    static_assert(NS * STAGE + NW * EPW <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + NW * EPW];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave / WN, wc = wave % WN;
+    const int fc = lane >> 4, fr = lane & 15;
+    const int kc = a.Kin >> 6;                // 64-deep K chunks per tap
+
+    // ---- this workgroup's tiles: channel tile fixed per workgroup, m-tiles of its XCD's range
+    const int G8 = int(gridDim.x) >> 3;
+    const int xcd = int(blockIdx.x) & 7, q = int(blockIdx.x) >> 3;
+    const int nt = q % a.ntiles, qq = q / a.ntiles, qstride = G8 / a.ntiles;
+    const int mt_total = a.mt_pre[a.ncls];
+    const int per = (mt_total + 7) >> 3;
+    const int mt_lo = xcd * per + qq, mt_hi = min(xcd * per + per, mt_total);
+    const int ntile = mt_lo < mt_hi ? (mt_hi - mt_lo + qstride - 1) / qstride : 0;
+    const int n0 = nt * BN;
+    int total = 0;                            // K steps of this workgroup's whole stream
+    if (a.ncls == 1) total = ntile * cls_of(a, 0).ntap * kc;
+    else
+        for (int t = 0; t < ntile; ++t) total += cls_of(a, cls_find(a, mt_lo + t * qstride)).ntap * kc;
+
+    // weight DMA rows (fixed): row r of the A image = output channel n0 + r
+    const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
+    const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
+    uint32_t a_off[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int r = (wave * AI + j) * 8 + (lane >> 3);
+        const int ch = n0 + r;
+        a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t((lane & 7) ^ fsw128(r)) * 16u : OOB;
+    }
+
+    // per-lane fragment read offsets inside a stage (subtile i / j adds 2048 * i: fsw128 is 16-periodic)
+    uint32_t offA[2], offB[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int ra = wr * (BN / WM) + fr, rb = wc * (BM / WN) + fr;
+        offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
+        offB[kk] = uint32_t(BN * RB + rb * RB + (((kk * 4 + fc) ^ fsw128(rb)) << 4));
+    }
+    bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
+    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) __device__ {
+        if constexpr (ABL >= 4) {
+            if (buf >= 0) return;
+        }
+        const char* As = smem + buf * STAGE + offA[kk];
+        const char* Bs = smem + buf * STAGE + offB[kk];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * RB);
+    };
+    f32x4 acc[TM][TN];
+    auto mma = [&](const bf16x8* fa, const bf16x8* fb) __device__ {
+        if constexpr (ABL == 1) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (MODE == PF)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
+                                                                        __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0,
+                                                                        0, 0);
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+    };
+
+    float ssum[TM][4], ssq[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
+
+    Issuer<BM, BN, NW, MODE> is(a, wave, lane, mt_lo, qstride, ntile);
+    if (ntile > 0) is.tile_setup();
+
+    // prologue: stages 0..2 in flight; stage 0 landed everywhere; its first-half fragments read
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+        if (s < total) is.template issue<ABL>(smem + s * STAGE, wres, a_off);
+    if (total >= 3) vm_wait<2 * DPS>();
+    else if (total == 2) vm_wait<DPS>();
+    else vm_wait<0>();
+    step_barrier();
+    if (total > 0) read_frags(f0a, f0b, 0, 0);
+
+    // compute side: one K step per iteration; tiles end inside the stream
+    int ct = 0, ck = 0, cnk = 0, buf = 0;
+    int64_t m0 = 0;
+    Cls cc{};
+    for (int g = 0; g < total; ++g) {
+        if (ck == 0) {
+            const int mt = mt_lo + ct * qstride;
+            const int c = cls_find(a, mt);
+            cc = cls_of(a, c);
+            m0 = int64_t(mt - a.mt_pre[c]) * BM;
+            cnk = cc.ntap * kc;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        read_frags(f1a, f1b, buf, 1);
+        mma(f0a, f0b);
+        // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight
+        if (g + 1 < total) {
+            if (g + 2 < total) vm_wait<DPS>();
+            else vm_wait<0>();
+        }
+        if constexpr (ABL != 3) step_barrier();
+        // the slot of stage g is free again (every wave's reads of it returned before the barrier)
+        if (g + 3 < total) is.template issue<ABL>(smem + buf * STAGE, wres, a_off);
+        const int nbuf = buf == NS - 1 ? 0 : buf + 1;
+        if (g + 1 < total) read_frags(f0a, f0b, nbuf, 0);
+        mma(f1a, f1b);
+        buf = nbuf;
+        if (++ck < cnk) continue;
+        ck = 0;
+        ++ct;
+
+        // epilogue: D[channel][pixel] (a lane holds 4 consecutive channels of one pixel per subtile) is
+        // transposed through this wave's LDS area 16 pixels at a time, so every store is a 16-B piece of
+        // a pixel's contiguous channel run (8 lanes = one 128-B segment), issued as buffer stores whose
+        // out-of-tile pixels fall out of range (no branches, a fixed count per tile)
+        if constexpr (ABL == 5) {             // timing only: no epilogue at all
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+            continue;
+        }
+        {
+            char* ep = smem + NS * STAGE + wave * EPW;
+            const int wch0 = n0 + wr * WCH;                   // first channel of this wave
+            const bool half = a.out_f32 == 2;                  // fp16 z (forward) or bf16 (data gradient)
+            const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
+            const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
+            constexpr int CPR = WCH * 2 / 16;                  // 16-B chunks per pixel row of this wave
+            constexpr int RPS = 64 / CPR;                      // pixel rows per store instruction
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                // stats (fp32, before rounding) and the rounded values into LDS: row fr, channel i*16+fc*4
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int cb = wch0 + i * 16 + fc * 4;
+                    if (a.st_sum && m0 + wc * (BM / WN) + j * 16 + fr < cc.Mc) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (cb + r < a.Nout) {
+                                const float v = acc[i][j][r];
+                                ssum[i][r] += v;
+                                ssq[i][r] += v * v;
+                            }
+                    }
+                    uint2 o;
+                    if (half) {
+                        o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
+                        o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
+                    } else {
+                        o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
+                        o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
+                    }
+                    const int byte = (i * 16 + fc * 4) * 2;                       // within the row
+                    const int chunk = (byte >> 4) ^ (fr & (CPR - 1));            // swizzled 16-B chunk
+                    *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);           // lgkmcnt(0): this wave's LDS writes landed
+#pragma unroll
+                for (int h = 0; h < 16 / RPS; ++h) {
+                    const int p = h * RPS + lane / CPR, c = lane % CPR;
+                    const uint4 v = *reinterpret_cast<const uint4*>(ep + p * (WCH * 2) + ((c ^ (p & (CPR - 1))) * 16));
+                    const int64_t m = m0 + wc * (BM / WN) + j * 16 + p;
+                    uint32_t off = OOB;
+                    if (m < cc.Mc && wch0 + c * 8 < a.Nout) {
+                        const uint32_t n = uint32_t(m) / cc.OHW, pix = uint32_t(m) - n * cc.OHW;
+                        const uint32_t ci_ = pix / uint32_t(cc.OWc);
+                        const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW +
+                                             int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
+                        off = uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0 + c * 8) * 2);
+                    }
+                    uint4 w = v;
+                    if (a.accumulate) {                        // gradient fan-in: dx += conv^T(dz) (bf16)
+                        const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
+                        uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
+                                          bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
+                        w = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, w),
+                                                           yres, off, 0, 0);
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);           // reads done before the next j rewrites the area
+            }
+        }
+    }
+
+    if (a.st_sum) {
+        // one partial row per workgroup of this channel tile: row = xcd + 8 * qq
+        vm_wait<0>();
+        __syncthreads();
+        float (*red)[WN][BN] = reinterpret_cast<float (*)[WN][BN]>(smem);   // [sum|sq][pixel wave][channel]
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = ssum[i][r], sq = ssq[i][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    s += __shfl_xor(s, o, 64);
+                    sq += __shfl_xor(sq, o, 64);
+                }
+                if (fr == 0) {
+                    const int cl = wr * (BN / WM) + i * 16 + fc * 4 + r;
+                    red[0][wc][cl] = s;
+                    red[1][wc][cl] = sq;
+                }
+            }
+        __syncthreads();
+        const int row = xcd + 8 * qq;
+        for (int cl = tid; cl < BN; cl += NW * 64) {
+            const int ch = n0 + cl;
+            if (ch < a.Nout) {
+                float ps = 0.f, pq = 0.f;
+#pragma unroll
+                for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
+                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
+            }
+        }
+    }
+}
+
+// tile configurations
+struct Cfg {
+    int bm, bn;
+};
+constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
+
+static int pipe_mode() {
+    static const int env = [] {
+        const char* e = getenv("YM_CONV_PIPE");
+        return e ? atoi(e) : 1;
+    }();
+    return g_pipe_force >= 0 ? g_pipe_force : env;
+}
+
+template <int ABL>
+void launch_abl(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
+    if (mode == PF) {
+        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PF, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PF, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
+    } else {
+        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PD, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PD, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
+    }
+}
+
+void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
+    static const int abl = [] {
+        const char* e = getenv("YM_PIPE_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    if (abl == 1) return launch_abl<1>(mode, cfg, a, grid, st);
+    if (abl == 2) return launch_abl<2>(mode, cfg, a, grid, st);
+    if (abl == 3) return launch_abl<3>(mode, cfg, a, grid, st);
+    if (abl == 4) return launch_abl<4>(mode, cfg, a, grid, st);
+    if (abl == 5) return launch_abl<5>(mode, cfg, a, grid, st);
+    if (mode == PF) {
+        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
+    } else {
+        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PD><<<dim3(grid), dim3(512), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PD><<<dim3(grid), dim3(512), 0, st>>>(a);
+    }
+}
+
+}  // namespace
+
+PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
+    PipePlan p{};
+    const int mode = pipe_mode();
+    if (!d || mode == 0) return p;
+    const int kin = dgrad ? d->cout : d->cin, nout = dgrad ? d->cin : d->cout;
+    if (kin % 64 != 0 || nout % 8 != 0) return p;
+    if (d->k != 3 && d->k != 1) return p;
+    if (d->stride != 1 && d->stride != 2) return p;
+    if (dgrad && d->k == 1 && d->stride == 2) return p;
+    const int64_t in_ld = dgrad ? d->y_ld : d->x_ld, in_bs = dgrad ? d->y_bs : d->x_bs;
+    const int64_t out_ld = dgrad ? d->x_ld : d->y_ld, out_bs = dgrad ? d->x_bs : d->y_bs;
+    if (in_ld % 8 || in_bs % 8 || out_ld % 4 || out_bs % 4) return p;
+    if (!dgrad && d->out_f32 == 1) return p;       // Detect's fp32 bias convs stay on conv.hip
+    const int os = dgrad ? d->stride : 1;
+    // default policy: only where it measured faster than conv.hip / conv_halo.hip (tools/pipe_check.py,
+    // DESIGN.md §conv): >= 128 output channels (the 256 x 128 tile) and no stride-2 data gradient
+    if (mode == 1 && (nout < 128 || os == 2)) return p;
+    const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
+    const int64_t M = int64_t(d->n) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
+    p.cfg = nout >= 128 ? 0 : 1;
+    const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
+    const int ntiles = (nout + bn - 1) / bn;
+    const int64_t tiles = (M / bm) * ntiles;
+    // enough tiles to keep every CU busy for several tiles (tail imbalance), else conv.hip's kernels
+    if (tiles < int64_t(mode >= 2 ? 256 : 1024)) return p;
+    // 32-bit buffer offsets relative to a tile's first image
+    if (in_bs * 2 * (256 / std::max<int64_t>(int64_t(OH / os) * (OW / os), 1) + 2) >= (int64_t(1) << 31)) return p;
+    int grid = 256;
+    const int unit = 8 * ntiles;
+    grid = (grid / unit) * unit;
+    if (grid < unit) return p;
+    p.grid = grid;
+    p.rows = grid / ntiles;
+    p.ok = 1;
+    return p;
+}
+
+int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
+    PipeArgs a{};
+    const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
+    if (!dgrad) {
+        a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
+        a.y = y; a.y_bs = d->y_bs; a.y_ld = d->y_ld;
+        a.GH = d->h; a.GW = d->w; a.Kin = d->cin;
+        a.OH = d->oh; a.OW = d->ow; a.Nout = d->cout;
+        a.os = 1;
+        a.out_f32 = d->out_f32;
+    } else {
+        a.x = x; a.x_bs = d->y_bs; a.x_ld = d->y_ld;
+        a.y = y; a.y_bs = d->x_bs; a.y_ld = d->x_ld;
+        a.GH = d->oh; a.GW = d->ow; a.Kin = d->cout;
+        a.OH = d->h; a.OW = d->w; a.Nout = d->cin;
+        a.os = d->stride;
+        a.out_f32 = 0;
+    }
+    a.w = w;
+    a.bias = bias; a.st_sum = st_sum; a.st_sq = st_sq;
+    a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad; a.N = d->n;
+    a.accumulate = d->accumulate;
+    a.ntiles = (a.Nout + bn - 1) / bn;
+    a.ncls = a.os == 2 ? 4 : 1;
+    int acc = 0;
+    for (int c = 0; c < a.ncls; ++c) {
+        const int py = a.os == 2 ? (c >> 1) : 0, px = a.os == 2 ? (c & 1) : 0;
+        const int64_t ohc = (a.OH - py + a.os - 1) / a.os, owc = (a.OW - px + a.os - 1) / a.os;
+        a.mt_pre[c] = acc;
+        acc += int((int64_t(a.N) * ohc * owc + bm - 1) / bm);
+    }
+    a.mt_pre[a.ncls] = acc;
+    launch_cfg(dgrad ? PD : PF, p.cfg, a, p.grid, st);
+    return YM_OK;
+}
+
+}  // namespace ym

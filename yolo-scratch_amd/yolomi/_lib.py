@@ -51,6 +51,7 @@ SIGNATURES = {
     "ym_conv_fwd_stat_rows": (R, [P]),
     "ym_conv_algo": (R, [P, INT]),
     "ym_conv_set_halo": (R, [INT]),
+    "ym_conv_set_pipe": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),

@@ -216,19 +216,29 @@ class ConvBN:
         w = [_kg(self.y)] + ([_kg(self.x)] if plan.needs_grad(self.x) else []) + ([_kg(self.res)] if self.res else [])
         return [_ka(self.x), _kg(self.y)], w
 
+    def _timed(self, plan, kind, stream, fn):
+        """Run one conv launch; the bench brackets it with HIP events on its own stream when it times
+        this op (plan.probe) or this kernel family (plan.family_events: 'fwd' / 'dgrad' / 'wgrad')."""
+        fam = plan.family_events
+        probe = kind == "fwd" and plan.probe is self
+        if not probe and (fam is None or kind not in fam):
+            fn()
+            return
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        fn()
+        ev1.record(stream)
+        if probe:
+            plan.probe_events.append((ev0, ev1))
+        if fam is not None and kind in fam:
+            fam[kind].append((ev0, ev1, self))
+
     def forward(self, plan, st):
         bn = self.m.bn
         ss, sq = self.ps[0], self.ps[1]
-        probe = plan.probe is self
-        if probe:
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev0.record(plan._cur_stream)
-        call("ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
-             ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st)
-        if probe:
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record(plan._cur_stream)
-            plan.probe_events.append((ev0, ev1))
+        self._timed(plan, "fwd", plan._cur_stream, lambda: call(
+            "ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
+            ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st))
         sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
         if plan.training:
             call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
@@ -264,13 +274,16 @@ class ConvBN:
                  rs, self.act, self.coef.data_ptr(), dz.data_ptr(), st)
         # weight gradient: on the side stream, beside this layer's data gradient and the next BN backward
         ws = plan.wgrad_ws()
-        call("ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
-             plan.gptr(self.m.conv.weight), 0, plan.side(st))
+        sst = plan.side(st)
+        self._timed(plan, "wgrad", plan.side_stream or plan._cur_stream, lambda: call(
+            "ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
+            plan.gptr(self.m.conv.weight), 0, sst))
         # data gradient
         if plan.needs_grad(self.x):
             acc = self.x.grad_for_write(st)
             self.desc.accumulate = acc
-            call("ym_conv_dgrad", ctypes.byref(self.desc), dz.data_ptr(), self.wt.data_ptr(), self.x.gptr(), st)
+            self._timed(plan, "dgrad", plan._cur_stream, lambda: call(
+                "ym_conv_dgrad", ctypes.byref(self.desc), dz.data_ptr(), self.wt.data_ptr(), self.x.gptr(), st))
             self.desc.accumulate = 0
             self.x.mark()
 
@@ -607,6 +620,7 @@ class Plan:
         self.acts, self.ops = [], []
         self.weights = WeightStore(self)
         self.probe, self.probe_events = None, []   # bench: time one op's conv launch
+        self.family_events = None  # bench: {'fwd'|'dgrad'|'wgrad': [(ev0, ev1, op)]} for every ConvBN launch
         self._bn_ws = []           # one BN-reduction workspace per scheduler stream (see bn_ws)
         self._cur = 0              # scheduler stream the current op runs on
         self.input = None          # View for block plans
@@ -831,7 +845,7 @@ class Plan:
     # graph runs its kernels with less overlap than the streams do.
     def _graph_ok(self):
         return (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
-                and os.environ.get("YM_GRAPH", "0") == "1")
+                and self.family_events is None and os.environ.get("YM_GRAPH", "0") == "1")
 
     @property
     def graph_active(self):
