@@ -8,8 +8,8 @@ forward (HIP plan) + v8 loss (fused kernels) + backward + RCCL gradient all-redu
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torchrun)
 
 Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel family by time (every conv
-forward / data-gradient / weight-gradient launch of a step bracketed with HIP events on its own
-stream); `roofline_probe` is the heaviest single conv launch (HIP events on the launch stream,
+forward / data-gradient / weight-gradient launch and every BatchNorm pass of a step bracketed with
+HIP events, in a pass that runs all launches on one stream); `roofline_probe` is the heaviest single conv launch (HIP events on the launch stream,
 HBM traffic from the committed counter pass); `roofline_step` prices the whole step against the
 same 16-bit MFMA peak.  `cpu_baseline`
 times the CPU oracle restatement (test infrastructure, fp32) on a bounded sample of the
@@ -197,17 +197,26 @@ def main():
         step(args.warmup + args.steps + i)
     torch.cuda.synchronize()
     plan.probe = None
-    # kernel families by time: every ConvBN's forward / data-gradient / weight-gradient launch bracketed
-    # with HIP events on its own stream over PROBE_STEPS steps (the step's busiest kernels)
-    plan.family_events = {"fwd": [], "dgrad": [], "wgrad": []}
+    # kernel families by time: every conv forward / data-gradient / weight-gradient launch and every
+    # BatchNorm pass (finalize + apply, reduce + finalize + apply) bracketed with HIP events over
+    # PROBE_STEPS steps, run on ONE stream (YM_STREAMS=1, YM_SIDE_STREAM=0) so that each duration is
+    # the kernel's own, not stretched by kernels of other streams sharing the CUs
+    saved = {k: os.environ.get(k) for k in ("YM_STREAMS", "YM_SIDE_STREAM")}
+    os.environ.update(YM_STREAMS="1", YM_SIDE_STREAM="0")
+    plan.family_events = {"fwd": [], "dgrad": [], "wgrad": [], "bn": []}
     for i in range(PROBE_STEPS):
         step(args.warmup + args.steps + PROBE_STEPS + i)
     torch.cuda.synchronize()
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     fams = {}
     for kind, evs in plan.family_events.items():
         ms = sum(a.elapsed_time(b) for a, b, _ in evs) / PROBE_STEPS
-        fl = sum(op.flops() for _, _, op in evs) / PROBE_STEPS
-        fams[kind] = (ms, fl, len(evs) // PROBE_STEPS)
+        work = sum(w for _, _, w in evs) / PROBE_STEPS
+        fams[kind] = (ms, work, len(evs) // PROBE_STEPS)
     plan.family_events = None
     # host time to enqueue one step (Python + ctypes launches) vs its wall time: a step whose
     # enqueue time approaches its wall time leaves the GPU waiting on the host
@@ -249,20 +258,39 @@ def main():
         roof = {"bound": "mfma", "achieved": round(dom_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(dom_tf / PEAK_BF16_TFLOPS, 4)}
     step_tf = value / world * per_img / 1e12
-    # the dominant kernel family by time (per step: summed launch durations, algorithmic FLOPs)
+    import ctypes
+    from yolomi._lib import lib as _yl
+    probe_kernel = {2: "conv_pipe_kernel", 1: "conv_halo_kernel"}.get(
+        _yl().ym_conv_algo(ctypes.byref(dom.desc), 0), "conv_gemm_kernel")
+    # the dominant kernel family by time (per step: summed launch durations; conv families against the
+    # MFMA peak with their algorithmic FLOPs, BatchNorm against HBM with its algorithmic bytes)
     fam_kind = max(fams, key=lambda k: fams[k][0])
-    f_ms, f_fl, f_n = fams[fam_kind]
-    f_tf = f_fl / (f_ms * 1e-3) / 1e12 if f_ms > 0 else 0.0
-    names = {"fwd": "conv forward (implicit GEMM / halo / pipelined kernels)",
-             "dgrad": "conv data gradient (implicit GEMM / halo / pipelined kernels)",
-             "wgrad": "conv weight gradient (wgrad3 / wgrad1 + split-K reduce)"}
-    roof_family = {"bound": "mfma", "achieved": round(f_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                   "frac": round(f_tf / PEAK_BF16_TFLOPS, 4), "traffic": traffic_for(f"family {fam_kind} bs{args.batch}"),
-                   "kernel": f"{names[fam_kind]}: {f_n} launches per step, {f_fl / 1e9:.0f} GFLOP algorithmic in "
-                             f"{f_ms:.3f} ms summed launch time (HIP events on each launch's stream, {PROBE_STEPS} steps)",
+    f_ms, f_work, f_n = fams[fam_kind]
+    names = {"fwd": "conv forward (pipelined / halo / implicit-GEMM kernels)",
+             "dgrad": "conv data gradient (pipelined / halo / implicit-GEMM kernels)",
+             "wgrad": "conv weight gradient (wgrad3 / wgrad1 + split-K reduce)",
+             "bn": "BatchNorm + SiLU passes (finalize + apply; bwd reduce + finalize + apply)"}
+
+    def fam_rate(kind):
+        ms, work, _ = fams[kind]
+        if ms <= 0:
+            return 0.0, 0.0
+        if kind == "bn":
+            gbs = work / (ms * 1e-3) / 1e9
+            return gbs, gbs / HBM_PEAK_GBS
+        tf = work / (ms * 1e-3) / 1e12
+        return tf, tf / PEAK_BF16_TFLOPS
+    f_rate, f_frac = fam_rate(fam_kind)
+    bn_fam = fam_kind == "bn"
+    roof_family = {"bound": "hbm" if bn_fam else "mfma", "achieved": round(f_rate, 2),
+                   "peak": HBM_PEAK_GBS if bn_fam else PEAK_BF16_TFLOPS, "unit": "GB/s" if bn_fam else "TFLOP/s",
+                   "frac": round(f_frac, 4), "traffic": traffic_for(f"family {fam_kind} bs{args.batch}"),
+                   "kernel": f"{names[fam_kind]}: {f_n} launch groups per step, "
+                             f"{f_work / 1e9:.0f} {'GB' if bn_fam else 'GFLOP'} algorithmic in {f_ms:.3f} ms summed "
+                             f"launch time (HIP events, all launches on one stream, {PROBE_STEPS} steps)",
                    "families_ms_per_step": {k: round(v[0], 3) for k, v in fams.items()},
-                   "families_frac": {k: round(v[1] / (v[0] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4) if v[0] > 0 else 0.0
-                                     for k, v in fams.items()}}
+                   "families_frac": {k: round(fam_rate(k)[1], 4) for k in fams},
+                   "families_bound": {k: ("hbm" if k == "bn" else "mfma") for k in fams}}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -282,7 +310,7 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": roof_family,
         "roofline_probe": {**roof, "traffic": traffic_for(probe_key),
-                     "kernel": f"conv_gemm_kernel fwd {dom.m.__class__.__name__} {dom.ci}->{dom.co} "
+                     "kernel": f"{probe_kernel} fwd {dom.m.__class__.__name__} {dom.ci}->{dom.co} "
                                f"k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W}, {dom.flops() / 1e9:.1f} GFLOP and "
                                f"{alg_bytes / 1e6:.0f} MB algorithmic per launch, {kern_ms:.3f} ms avg over "
                                f"{len(lens)} launches ({dom_tf:.0f} TFLOP/s = {dom_tf / PEAK_BF16_TFLOPS:.3f} of the "

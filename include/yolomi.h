@@ -13,8 +13,8 @@
  *    the caller (PyTorch caching allocator); the library never allocates or
  *    frees caller memory and keeps no TENSOR state between calls.  The only
  *    process-wide state is configuration and diagnostics: the conv kernel
- *    selection policies (ym_conv_set_halo / ym_conv_set_pipe, YM_CONV_HALO / YM_CONV_PIPE read
- *    once) and the
+ *    selection policies (ym_conv_set_halo / ym_conv_set_pipe / ym_conv_set_direct, YM_CONV_HALO /
+ *    YM_CONV_PIPE / YM_CONV_DIRECT read once) and the
  *    NMS segment counters (ym_debug_nms_stamps, written when YM_NMS_STAMPS is
  *    set); neither changes a result.
  *  - `stream` is a hipStream_t (0 = legacy default stream); every call is
@@ -145,8 +145,9 @@ int ym_conv_stat_blocks(int64_t m, int cout);
 /* Rows of the BN statistics partials ym_conv_fwd writes for this conv (the halo-staged 3x3
  * kernel and the implicit GEMM use different grids); size stat_sum / stat_sq with it. */
 int ym_conv_fwd_stat_rows(const ym_conv_desc* d);
-/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 2 = the persistent
- * pipelined implicit GEMM, 1 = the halo-staged 3x3 stride-1 kernel, 0 = the 2-stage implicit GEMM. */
+/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 3 = the direct
+ * register-weight kernel, 2 = the persistent pipelined implicit GEMM, 1 = the halo-staged 3x3
+ * stride-1 kernel, 0 = the 2-stage implicit GEMM. */
 int ym_conv_algo(const ym_conv_desc* d, int dgrad);
 /* Selection policy of the halo-staged kernel for later calls: -1 YM_CONV_HALO / default, 0 never,
  * 1 wherever it applies, 2 where it measured faster (default: maps <= 24 wide).  Returns the
@@ -156,6 +157,10 @@ int ym_conv_set_halo(int mode);
  * YM_CONV_PIPE / default, 0 never, 1 layers of >= 1024 256-pixel tiles (default), 2 >= 256 tiles.
  * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_pipe(int mode);
+/* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
+ * layers) for later calls: -1 YM_CONV_DIRECT / default, 0 never, 1 maps of >= 1 M output pixels
+ * (default), 2 any size.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+int ym_conv_set_direct(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
  * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
@@ -169,18 +174,48 @@ int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt,
 size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d);
 int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, void* workspace,
                   size_t workspace_bytes, float* dw_oihw, int accumulate, void* stream);
+/* Training BatchNorm2d state and outputs for the fused finalize of ym_conv_fwd_bn /
+ * ym_conv_first_fwd_bn / ym_dw3x3_fwd_bn: the kernel that produces the batch statistics also
+ * reduces them (fixed order, fp64; ticket-elected last workgroups, no spinning) and writes what
+ * ym_bn_finalize would — scale, shift, mean, rstd, running stats, num_batches_tracked — so no
+ * finalize launch sits between the conv and ym_bn_apply.  workspace: ym_bn_workspace_size(cout)
+ * bytes, shared with the other BN calls of the same stream (counters left at zero). */
+typedef struct {
+    const float* gamma;
+    const float* beta;
+    float* running_mean;       /* may be NULL (no running stats) */
+    float* running_var;
+    int64_t* num_batches_tracked;   /* may be NULL */
+    float momentum, eps;
+    float* scale;
+    float* shift;
+    float* mean;
+    float* rstd;
+    void* workspace;
+} ym_bn_train;
+/* ym_conv_fwd (out_f32 = 2, statistics required) + ym_bn_finalize in one launch; count = n*oh*ow. */
+int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* z, float* stat_sum,
+                   float* stat_sq, const ym_bn_train* bn, void* stream);
 /* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0). */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
 /* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
  * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). cout <= 128. */
 size_t ym_conv_first_wgrad_workspace_size(int cout);
+/* ym_conv_first_fwd + ym_bn_finalize in one launch (count = n*oh*ow). */
+int ym_conv_first_fwd_bn(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
+                         int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
+                         const ym_bn_train* bn, void* stream);
 int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
                         int cout, int stride, int pad, float* workspace, size_t workspace_bytes, void* stream);
 /* Depthwise 3x3 s1 p1 (Attention.pe, yolo11_modules.py:122); input channel c reads source
  * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
 int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks, void* stream);
+/* ym_dw3x3_fwd + ym_bn_finalize in one launch (count = n*h*wd). */
+int ym_dw3x3_fwd_bn(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
+                    uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks,
+                    const ym_bn_train* bn, void* stream);
 size_t ym_dw3x3_bwd_workspace_size(int c);
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
@@ -214,6 +249,12 @@ int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint1
 int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                        const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
                        float* coef, void* workspace, void* stream);
+/* ym_bn_bwd_reduce + ym_bn_bwd_finalize in one launch (the statistics pass's last workgroups fold
+ * the partials, fixed order): part_* hold ym_bn_bwd_blocks(m, c) rows; count = m. */
+int ym_bn_bwd_reduce_finalize(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
+                              int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
+                              int act, float* part_sum, float* part_dot, const float* gamma, float* dgamma,
+                              float* dbeta, int accumulate, float* coef, void* workspace, void* stream);
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                     const float* coef, uint16_t* dz, void* stream);

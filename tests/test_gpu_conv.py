@@ -248,3 +248,81 @@ def test_pipe_kernel_vs_torch(shape):
     assert rel(d1[..., :cin], dx_ref) < 1e-2
     assert (d1[..., cin:] == 3.0).all()
     assert rel(dxbuf[..., :cin], 2 * dx_ref) < 1e-2
+
+
+# direct register-weight kernel (conv_direct.hip), forced on at any size with ym_conv_set_direct(2):
+# every instantiated (Cin, Cout, k, stride) in both directions, odd map sizes (partial 16-pixel groups,
+# odd stride-2 parity classes), channel-slice views, fp16 + BN statistics forward, bf16 data gradient
+# overwrite and accumulate
+DIRECT = [
+    # n, h, w, cin, cout, k, stride, in_extra, out_extra
+    (2, 17, 19, 32, 64, 3, 2, 0, 0),
+    (3, 33, 21, 32, 32, 3, 1, 32, 16),
+    (2, 15, 13, 64, 64, 1, 1, 0, 64),
+    (2, 11, 23, 96, 128, 1, 1, 32, 0),
+    (1, 19, 9, 64, 64, 1, 1, 0, 0),
+    (2, 21, 16, 32, 64, 3, 2, 32, 0),
+]
+
+
+@pytest.mark.parametrize("shape", DIRECT, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in DIRECT])
+def test_direct_kernel_vs_torch(shape):
+    from yolomi._lib import call, lib, ConvDesc
+    n, h, w, cin, cout, k, s, xe, ye = shape
+    p = k // 2
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, oh, ow, cout, k, s, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * (cin + xe), cin + xe, oh * ow * (cout + ye), cout + ye
+    d.out_f32, d.accumulate = 2, 0
+    g = torch.Generator().manual_seed(hash(shape) & 0xFFFF)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, generator=g).half()
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    dz = torch.randn(n, oh, ow, cout, generator=g).bfloat16()
+    w16, wbf = wt.half(), wt.bfloat16()
+    prev = lib().ym_conv_set_direct(2)
+    try:
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 3
+        assert lib().ym_conv_algo(ctypes.byref(d), 1) == 3
+        xbuf = torch.zeros(n, h, w, cin + xe, dtype=torch.float16, device=dev)
+        xbuf[..., :cin] = x.to(dev)
+        ybuf = torch.full((n, oh, ow, cout + ye), 7.0, dtype=torch.float16, device=dev)
+        rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+        ss = torch.full((rows, cout), float("nan"), device=dev)
+        sq = torch.full((rows, cout), float("nan"), device=dev)
+        st = torch.cuda.current_stream().cuda_stream
+        w_fwd = w16.permute(0, 2, 3, 1).contiguous().to(dev)
+        call("ym_conv_fwd", ctypes.byref(d), xbuf.data_ptr(), w_fwd.data_ptr(), ybuf.data_ptr(), None,
+             ss.data_ptr(), sq.data_ptr(), st)
+        dzbuf = torch.zeros(n, oh, ow, cout + ye, dtype=torch.bfloat16, device=dev)
+        dzbuf[..., :cout] = dz.to(dev)
+        dxbuf = torch.full((n, h, w, cin + xe), float("nan"), dtype=torch.bfloat16, device=dev)
+        dxbuf[..., cin:] = 3.0
+        w_t = wbf.permute(1, 2, 3, 0).contiguous().to(dev)
+        call("ym_conv_dgrad", ctypes.byref(d), dzbuf.data_ptr(), w_t.data_ptr(), dxbuf.data_ptr(), st)
+        dx1 = dxbuf.clone()
+        dd = ConvDesc.from_buffer_copy(d)
+        dd.accumulate = 1
+        call("ym_conv_dgrad", ctypes.byref(dd), dzbuf.data_ptr(), w_t.data_ptr(), dxbuf.data_ptr(), st)
+        torch.cuda.synchronize()
+    finally:
+        lib().ym_conv_set_direct(prev)
+    y_ref = F.conv2d(x.float().permute(0, 3, 1, 2), w16.float(), stride=s, padding=p).permute(0, 2, 3, 1)
+    dx_ref = torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz.float().permute(0, 3, 1, 2),
+                                        stride=s, padding=p).permute(0, 2, 3, 1)
+
+    def rel(a, b):
+        return float((a.float().cpu() - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+    yc = ybuf.cpu()
+    assert rel(yc[..., :cout], y_ref) < 2e-3
+    assert (yc[..., cout:] == 7.0).all()
+    yr = y_ref.reshape(-1, cout)
+    assert float((ss.sum(0).cpu() - yr.sum(0)).abs().max()) < 1e-4 * float(yr.abs().sum(0).max())
+    assert rel(sq.sum(0), (yr ** 2).sum(0)) < 1e-3
+    d1 = dx1.float().cpu()
+    assert torch.isfinite(d1).all()
+    assert rel(d1[..., :cin], dx_ref) < 1e-2
+    assert (d1[..., cin:] == 3.0).all()
+    assert rel(dxbuf[..., :cin], 2 * dx_ref) < 1e-2

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "bnfold.h"
 #include "common.h"
 
 namespace ym {
@@ -321,7 +322,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act,
-                                                            float* __restrict__ ps, float* __restrict__ pg) {
+                                                            float* __restrict__ ps, float* __restrict__ pg,
+                                                            BnFold fold) {
     extern __shared__ float red[];   // [2][rows][C]
     const Lanes L = lanes(C);
     const int c0 = L.g * 8;
@@ -370,9 +372,10 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
             a += red[r * C + c];
             b += red[(L.rows + r) * C + c];
         }
-        ps[int64_t(blockIdx.x) * C + c] = a;
-        pg[int64_t(blockIdx.x) * C + c] = b;
+        st_row(&ps[int64_t(blockIdx.x) * C + c], a, fold.cnt != nullptr);
+        st_row(&pg[int64_t(blockIdx.x) * C + c], b, fold.cnt != nullptr);
     }
+    if (fold.cnt) bn_fold_tail(fold, ps, pg, C, blockIdx.x, red);
 }
 
 // dz[m][c] = k1*(g - k2 - xhat*k3), dz dense [M][C] (may alias z)
@@ -539,8 +542,34 @@ extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, 
     int blocks = ym_bn_bwd_blocks(m, c);
     int rows = 256 / (c / 8);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2) * rows * c * sizeof(float),
-                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot);
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot,
+                       BnFold{});
     YM_LAUNCH_CHECK("ym_bn_bwd_reduce");
+    return YM_OK;
+}
+
+extern "C" int ym_bn_bwd_reduce_finalize(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m,
+                                         int c, int hw, const float* scale, const float* shift, const float* mean,
+                                         const float* rstd, int act, float* part_sum, float* part_dot,
+                                         const float* gamma, float* dgamma, float* dbeta, int accumulate, float* coef,
+                                         void* workspace, void* stream) {
+    CHECK_C(c);
+    CHECK_VIEW(d_bs, d_ld, hw);
+    YM_CHECK_ARG(m > 0 && workspace && gamma && rstd && coef && part_sum && part_dot,
+                 "ym_bn_bwd_reduce_finalize: null argument / no pixels");
+    const int blocks = ym_bn_bwd_blocks(m, c);
+    const int rows = 256 / (c / 8);
+    BnFold f{};
+    f.cnt = static_cast<unsigned*>(workspace);
+    f.p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
+    f.bwd = 1;
+    f.count = double(m);
+    f.gamma = gamma; f.rstd_in = rstd;
+    f.dgamma = dgamma; f.dbeta = dbeta; f.accumulate = accumulate; f.coef = coef;
+    bn_fold_groups(f, blocks, 1);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2) * rows * c * sizeof(float),
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot, f);
+    YM_LAUNCH_CHECK("ym_bn_bwd_reduce_finalize");
     return YM_OK;
 }
 

@@ -28,7 +28,9 @@
 #include <string>
 
 #include "common.h"
+#include "conv_direct.h"
 #include "conv_halo.h"
+#include "bnfold.h"
 #include "conv_pipe.h"
 #include "reduce.h"
 #include "tile.h"
@@ -54,6 +56,7 @@ struct GemmArgs {
     int N;                                   // images
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
     int ntl;                                 // channel tiles interleaved into grid x (0: they are grid y)
+    BnFold fold;                             // fused BN finalize (fold.cnt null: none)
 };
 
 // LDS images are lane-linear (LDS-DMA writes lane l of a wave-instruction at base + 16*l): 128-B
@@ -374,10 +377,11 @@ conv_gemm_kernel(GemmArgs a) {
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                a.st_sum[int64_t(bx) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(bx) * a.Nout + ch] = pq;
+                st_row(&a.st_sum[int64_t(bx) * a.Nout + ch], ps, a.fold.cnt != nullptr);
+                st_row(&a.st_sq[int64_t(bx) * a.Nout + ch], pq, a.fold.cnt != nullptr);
             }
         }
+        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, bx, smem);
     }
 }
 
@@ -416,7 +420,7 @@ __device__ __forceinline__ void ordered_wave_add72(float* red, const float (*acc
 __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                              uint16_t* __restrict__ y, float* __restrict__ st_sum,
                                                              float* __restrict__ st_sq, int N, int H, int W, int OH,
-                                                             int OW, int Cout, int stride, int pad) {
+                                                             int OW, int Cout, int stride, int pad, BnFold fold) {
     __shared__ float red[2][512];
     const int G = Cout >> 3;                 // channel groups (divides 64)
     const int g = threadIdx.x % G;
@@ -467,9 +471,10 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < Cout; c += 256) {
-        st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
-        st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
+        st_row(&st_sum[int64_t(blockIdx.x) * Cout + c], red[0][c], fold.cnt != nullptr);
+        st_row(&st_sq[int64_t(blockIdx.x) * Cout + c], red[1][c], fold.cnt != nullptr);
     }
+    if (fold.cnt) bn_fold_tail(fold, st_sum, st_sq, Cout, blockIdx.x, &red[0][0]);
 }
 
 // part[block][co*9 + t] = sum over the block's pixels p of dz[p][co] * patch(p)[t]  (no dgrad: the
@@ -553,7 +558,7 @@ __device__ __forceinline__ void unpack8(uint4 u, float* f, bool half) {
     }
 }
 
-__global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
+__global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq, BnFold fold) {
     __shared__ float red[2][512];
     const int G = a.C >> 3, g = threadIdx.x % G;
     const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
@@ -600,9 +605,10 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < a.C; c += 256) {
-        st_sum[int64_t(blockIdx.x) * a.C + c] = red[0][c];
-        st_sq[int64_t(blockIdx.x) * a.C + c] = red[1][c];
+        st_row(&st_sum[int64_t(blockIdx.x) * a.C + c], red[0][c], fold.cnt != nullptr);
+        st_row(&st_sq[int64_t(blockIdx.x) * a.C + c], red[1][c], fold.cnt != nullptr);
     }
+    if (fold.cnt) bn_fold_tail(fold, st_sum, st_sq, a.C, blockIdx.x, &red[0][0]);
 }
 
 // dx (mapped channels, overwrite or accumulate into the view) and dW (+=) from dense dz (N,H,W,C)
@@ -726,6 +732,7 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
+    if (a.fold.cnt) bn_fold_groups(a.fold, gx, ntiles);
     // YM_CONV_ABLATE=nomma|nodma: timing-only builds without the MFMAs / without the staging
     static const int abl = [] {
         const char* e = getenv("YM_CONV_ABLATE");
@@ -826,9 +833,18 @@ extern "C" int ym_conv_set_pipe(int mode) {
     return prev;
 }
 
+extern "C" int ym_conv_set_direct(int mode) {
+    // selection policy of the direct register-weight kernel: -1 env/default, 0 never, 1 maps of
+    // >= 1 M output pixels (default), 2 any size; returns the previous setting
+    const int prev = g_direct_force;
+    g_direct_force = mode < -1 || mode > 2 ? -1 : mode;
+    return prev;
+}
+
 extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
-    // 2: persistent pipelined implicit GEMM (conv_pipe.hip), 1: halo-staged 3x3 kernel
-    // (conv_halo.hip), 0: 2-stage implicit GEMM
+    // 3: direct register-weight kernel (conv_direct.hip), 2: persistent pipelined implicit GEMM
+    // (conv_pipe.hip), 1: halo-staged 3x3 kernel (conv_halo.hip), 0: 2-stage implicit GEMM
+    if (d && direct_plan(d, dgrad ? 1 : 0).ok) return 3;
     if (d && pipe_plan(d, dgrad ? 1 : 0).ok) return 2;
     return d && halo_plan(d, dgrad ? 1 : 0).ok ? 1 : 0;
 }
@@ -836,6 +852,8 @@ extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
 extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     // rows of the BN statistics partials ym_conv_fwd writes for this conv (halo or implicit-GEMM grid)
     if (!d) return 0;
+    const DirectPlan dp = direct_plan(d, 0);
+    if (dp.ok) return dp.grid;
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) return pp.rows;
     const HaloPlan hp = halo_plan(d, 0);
@@ -843,8 +861,8 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     return ym_conv_stat_blocks(int64_t(d->n) * d->oh * d->ow, d->cout);
 }
 
-extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
-                           float* stat_sum, float* stat_sq, void* stream) {
+static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
+                         float* stat_sum, float* stat_sq, const BnFold* fold, void* stream) {
     YM_CHECK_ARG(d && x && w && y, "ym_conv_fwd: null argument");
     YM_CHECK_ARG(d->cin % 8 == 0, "ym_conv_fwd: Cin %% 8 != 0 (Cin=%d)", d->cin);
     YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_fwd: kernel size %d unsupported (1..3)", d->k);
@@ -863,24 +881,48 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
     a.out_f32 = d->out_f32; a.accumulate = d->accumulate;
     a.N = d->n;
     a.ostep = 1;
+    if (fold) a.fold = *fold;
     if (a.M == 0) return YM_OK;
+    const DirectPlan dp = fold ? DirectPlan{} : direct_plan(d, 0);
+    if (dp.ok) {
+        direct_launch(dp, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_fwd (direct)");
+        return YM_OK;
+    }
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) {
-        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, fold, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (pipe)");
         return YM_OK;
     }
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) {
-        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, fold, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
     pick_and_launch(a, MODE_FWD, fwd_stat_blocks(), as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
+}
+
+extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
+                           float* stat_sum, float* stat_sq, void* stream) {
+    return conv_fwd_impl(d, x, w, y, bias, stat_sum, stat_sq, nullptr, stream);
+}
+
+extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* z,
+                              float* stat_sum, float* stat_sq, const ym_bn_train* bn, void* stream) {
+    YM_CHECK_ARG(d && bn && bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd,
+                 "ym_conv_fwd_bn: null argument");
+    YM_CHECK_ARG(stat_sum && stat_sq && d->out_f32 == 2, "ym_conv_fwd_bn: needs statistics and fp16 z (out_f32 = 2)");
+    YM_CHECK_ARG(d->cout <= 2048, "ym_conv_fwd_bn: cout > 2048");
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    YM_CHECK_ARG(M > 0, "ym_conv_fwd_bn: no pixels");
+    const BnFold f = bn_fold_fwd(bn, double(M));
+    return conv_fwd_impl(d, x, w, z, nullptr, stat_sum, stat_sq, &f, stream);
 }
 
 extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream) {
@@ -907,15 +949,21 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->y_bs, int64_t(d->h / d->stride) * (d->w / d->stride)),
                  "ym_conv_dgrad: gradient image stride too large");
+    const DirectPlan dp = direct_plan(d, 1);
+    if (dp.ok) {
+        direct_launch(dp, d, 1, dz, wt, dx, nullptr, nullptr, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_dgrad (direct)");
+        return YM_OK;
+    }
     const PipePlan pp = pipe_plan(d, 1);
     if (pp.ok) {
-        pipe_launch(pp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
+        pipe_launch(pp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, nullptr, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_dgrad (pipe)");
         return YM_OK;
     }
     const HaloPlan hp = halo_plan(d, 1);
     if (hp.ok) {
-        halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
+        halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, nullptr, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_dgrad (halo)");
         return YM_OK;
     }
@@ -924,16 +972,39 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     return YM_OK;
 }
 
-extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
-                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
-                                 void* stream) {
+static int conv_first_fwd_impl(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
+                               int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
+                               const ym_bn_train* bn, void* stream) {
     YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd: cout=%d unsupported", cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd: too many pixels");
+    YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_conv_first_fwd: statistics buffers / blocks");
+    BnFold f{};
+    if (bn) {
+        YM_CHECK_ARG(bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd &&
+                     int64_t(n) * oh * ow > 0, "ym_conv_first_fwd_bn: null argument / no pixels");
+        f = bn_fold_fwd(bn, double(int64_t(n) * oh * ow));
+        bn_fold_groups(f, blocks, 1);
+    }
     hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
-                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad);
+                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, f);
     YM_LAUNCH_CHECK("ym_conv_first_fwd");
     return YM_OK;
+}
+
+extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
+                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
+                                 void* stream) {
+    return conv_first_fwd_impl(img, w_oihw, y, stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, blocks, nullptr,
+                               stream);
+}
+
+extern "C" int ym_conv_first_fwd_bn(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum,
+                                    float* stat_sq, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
+                                    int blocks, const ym_bn_train* bn, void* stream) {
+    YM_CHECK_ARG(bn, "ym_conv_first_fwd_bn: null BN state");
+    return conv_first_fwd_impl(img, w_oihw, y, stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, blocks, bn,
+                               stream);
 }
 
 extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
@@ -963,15 +1034,37 @@ static bool dw_shape_ok(int64_t x_bs, int64_t x_ld, int gsz, int gstride, int go
            goff % 8 == 0 && x_bs % 8 == 0 && x_ld % 8 == 0;
 }
 
+static int dw3x3_fwd_impl(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
+                          const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
+                          int blocks, const ym_bn_train* bn, void* stream) {
+    YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
+                 "ym_dw3x3_fwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+    YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_dw3x3_fwd: statistics buffers / blocks");
+    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
+    BnFold f{};
+    if (bn) {
+        YM_CHECK_ARG(bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd &&
+                     int64_t(n) * h * wd > 0, "ym_dw3x3_fwd_bn: null argument / no pixels");
+        f = bn_fold_fwd(bn, double(int64_t(n) * h * wd));
+        bn_fold_groups(f, blocks, 1);
+    }
+    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq, f);
+    YM_LAUNCH_CHECK("ym_dw3x3_fwd");
+    return YM_OK;
+}
+
 extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
                             const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
                             int blocks, void* stream) {
-    YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
-                 "ym_dw3x3_fwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
-    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
-    YM_LAUNCH_CHECK("ym_dw3x3_fwd");
-    return YM_OK;
+    return dw3x3_fwd_impl(x, x_bs, x_ld, gsz, gstride, goff, w, y, stat_sum, stat_sq, n, h, wd, c, blocks, nullptr,
+                          stream);
+}
+
+extern "C" int ym_dw3x3_fwd_bn(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
+                               const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd,
+                               int c, int blocks, const ym_bn_train* bn, void* stream) {
+    YM_CHECK_ARG(bn, "ym_dw3x3_fwd_bn: null BN state");
+    return dw3x3_fwd_impl(x, x_bs, x_ld, gsz, gstride, goff, w, y, stat_sum, stat_sq, n, h, wd, c, blocks, bn, stream);
 }
 
 extern "C" size_t ym_dw3x3_bwd_workspace_size(int c) {

@@ -1,0 +1,22 @@
+// Direct MFMA convolution with register-resident weights (conv_direct.hip): applicability plan +
+// launch, tried by ym_conv_fwd / ym_conv_dgrad in conv.hip before the other conv kernels.
+#pragma once
+#include "common.h"
+
+namespace ym {
+
+struct DirectPlan {
+    int ok;          // the direct kernel handles this conv
+    int variant;     // template instance (conv_direct.hip: kVariants)
+    int grid;        // workgroups per output-parity class (= rows of the BN statistics partials)
+    int classes;     // output-parity classes (4: stride-2 data gradient, else 1)
+};
+
+// -1: YM_CONV_DIRECT / default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size
+extern int g_direct_force;
+
+DirectPlan direct_plan(const ym_conv_desc* d, int dgrad);
+int direct_launch(const DirectPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w,
+                  void* y, float* st_sum, float* st_sq, hipStream_t st);
+
+}  // namespace ym

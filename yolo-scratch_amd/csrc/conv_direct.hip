@@ -1,0 +1,360 @@
+// Direct MFMA convolution for the high-resolution, few-channel layers of the YOLOv11 graph
+// (the 320x320 / 160x160 maps of the stem stage: 32-128 channels), fp16 forward / bf16 data
+// gradient, fp32 accumulate.
+//
+// Replaces nn.Conv2d forward / input-gradient inside Conv (/root/reference/yolo_scratch_cuda/
+// models/yolo11_modules.py:21-33) where the implicit GEMMs (conv.hip, conv_pipe.hip) are
+// latency-bound: with 32-96 input channels a 128-pixel tile has only 5-9 K steps, each one a full
+// LDS-DMA round trip, and the 3x3 taps re-stage the input nine times through LDS (measured
+// 0.22-0.26 ms for a 32->32 3x3 160x160 layer whose HBM roof is 0.03 ms).
+//
+// Here the whole weight tensor of the layer lives in registers (at most 144 VGPRs: Cout/16 x taps x
+// Cin/32 MFMA A-fragments per lane) and every wave streams pixels: each 16-pixel MFMA B-fragment
+// is ONE 16-byte load per lane straight from the NHWC activation (8 consecutive channels of one
+// pixel; the 3x3 neighbours' re-reads hit L1/L2), out-of-image taps read zero through out-of-range
+// buffer offsets.  No LDS on the main path, no barriers; the only reduction is the BatchNorm
+// statistics (xor shuffles, then the waves in order through LDS: one partial row per workgroup).
+// Data gradients: stride 1 as a conv of dz with the transposed weight copy (taps mirrored by the
+// index formula), stride 2 as 4 output-parity classes, each task one class (its pixels every other
+// column, so the valid taps are the same for every lane).
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "common.h"
+#include "conv_direct.h"
+#include "tile.h"
+
+namespace ym {
+
+int g_direct_force = -1;
+
+namespace {
+
+struct DirArgs {
+    const uint16_t* x; int64_t x_bs, x_ld;    // gathered input view (fwd: x fp16, dgrad: dz bf16)
+    const uint16_t* w;                         // [Nout][KS][KS][Kin] (fwd: fp16 w, dgrad: bf16 transposed copy)
+    void* y; int64_t y_bs, y_ld;               // output view
+    float* st_sum; float* st_sq;               // [gridDim.x][Nout] or null
+    int GH, GW, OH, OW, N;                     // gathered map, output map
+    int Kin, Nout, pad;
+    int accumulate;
+    int OHc, OWc;                              // class map (dgrad stride 2: ceil(O/2); else O)
+    int64_t tpc;                               // tasks per class
+    int ncls;
+};
+
+template <int MODE>
+using frag_t = typename std::conditional<MODE == 0, f16x8, bf16x8>::type;
+
+__device__ __forceinline__ f32x4 mma(f16x8 a, f16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// pixel coordinates of the lane's pixel in each 16-pixel group of task `tl` (class (PY, PX) of a
+// stride-2 data gradient: every other row / column)
+template <int TP, int CS>
+struct TaskPix {
+    int n[TP], oh[TP], ow[TP];
+    bool ok[TP];
+    __device__ __forceinline__ void decode(const DirArgs& a, int64_t tl, int fr, int py, int px) {
+        const uint32_t chw = uint32_t(a.OHc) * uint32_t(a.OWc);
+#pragma unroll
+        for (int g = 0; g < TP; ++g) {
+            const int64_t m = tl * (16 * TP) + g * 16 + fr;
+            const uint32_t nn = uint32_t(m / chw), r = uint32_t(m - int64_t(nn) * chw);
+            const uint32_t i = r / uint32_t(a.OWc), j = r - i * uint32_t(a.OWc);
+            n[g] = int(nn);
+            oh[g] = int(i) * CS + py;
+            ow[g] = int(j) * CS + px;
+            ok[g] = int(nn) < a.N && oh[g] < a.OH && ow[g] < a.OW;
+        }
+    }
+};
+
+// NT: 16-channel output tiles (Nout <= 16 NT), KC: 32-channel input chunks (Kin = 32 KC), KS kernel
+// size, S stride, MODE 0 forward (fp16 out + statistics) / 1 data gradient (bf16 out), TP 16-pixel
+// groups per wave task, (PY, PX) the output-parity class of a stride-2 data gradient (else 0, 0).
+// All of a task's input fragments are loaded before its first MFMA (one memory latency per task, not
+// one per tap); the 1x1 forms also load the NEXT task's fragments before this task's MFMAs.
+template <int NT, int KC, int KS, int S, int MODE, int TP, int PY, int PX>
+__device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][4], float (&ssq)[NT][4], int64_t first,
+                                            int64_t step) {
+    using F = frag_t<MODE>;
+    constexpr int TAPS = KS * KS;
+    constexpr bool CLS = S == 2 && MODE == 1;
+    constexpr int CS = CLS ? 2 : 1;
+    const int lane = threadIdx.x & 63, fr = lane & 15, fc = lane >> 4;
+    // taps that reach this class (all taps otherwise)
+    auto live = [&](int t) constexpr -> bool {
+        const int kh = t / KS, kw = t % KS;
+        return !CLS || (((PY + 1 - kh) & 1) == 0 && ((PX + 1 - kw) & 1) == 0);
+    };
+    F wa[TAPS][KC][NT];
+    {
+        const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, int64_t(a.Nout) * TAPS * a.Kin * 2);
+#pragma unroll
+        for (int t = 0; t < TAPS; ++t) {
+            if (!live(t)) continue;
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int co = nt * 16 + fr;
+                    const uint32_t off =
+                        co < a.Nout ? uint32_t(((co * TAPS + t) * a.Kin + kc * 32 + fc * 8) * 2) : OOB;
+                    wa[t][kc][nt] = __builtin_bit_cast(F, buf_load16(wr, off));
+                }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
+    auto load = [&](const TaskPix<TP, CS>& P, F (&b)[TAPS][TP][KC]) {
+#pragma unroll
+        for (int t = 0; t < TAPS; ++t) {
+            if (!live(t)) continue;
+            const int kh = t / KS, kw = t % KS;
+#pragma unroll
+            for (int g = 0; g < TP; ++g) {
+                int ih, iw;
+                if constexpr (MODE == 0) {
+                    ih = P.oh[g] * S - a.pad + kh;
+                    iw = P.ow[g] * S - a.pad + kw;
+                } else {
+                    ih = (P.oh[g] + a.pad - kh) >> (S - 1);     // exact for the taps this class keeps
+                    iw = (P.ow[g] + a.pad - kw) >> (S - 1);
+                }
+                const bool in = P.ok[g] && unsigned(ih) < unsigned(a.GH) && unsigned(iw) < unsigned(a.GW);
+                const uint32_t base =
+                    in ? uint32_t((int64_t(P.n[g]) * a.x_bs + (int64_t(ih) * a.GW + iw) * a.x_ld + fc * 8) * 2) : OOB;
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc)
+                    b[t][g][kc] = __builtin_bit_cast(F, buf_load16(xr, base == OOB ? OOB : base + kc * 64));
+            }
+        }
+    };
+    const int64_t ntask = a.tpc;
+    TaskPix<TP, CS> P;
+    F b[TAPS][TP][KC];
+    int64_t task = first;
+    if (task < ntask) {
+        P.decode(a, task, fr, PY, PX);
+        load(P, b);
+    }
+    for (; task < ntask; task += step) {
+        f32x4 acc[TP][NT];
+#pragma unroll
+        for (int g = 0; g < TP; ++g)
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[g][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        TaskPix<TP, CS> Q = P;
+        if constexpr (KS == 1) {
+            // the next task's fragments in flight during this task's MFMAs and stores
+            F bn[TAPS][TP][KC];
+            const bool more = task + step < ntask;
+            if (more) {
+                P.decode(a, task + step, fr, PY, PX);
+                load(P, bn);
+            }
+#pragma unroll
+            for (int g = 0; g < TP; ++g)
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt) acc[g][nt] = mma(wa[0][kc][nt], b[0][g][kc], acc[g][nt]);
+#pragma unroll
+            for (int g = 0; g < TP; ++g)
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc) b[0][g][kc] = bn[0][g][kc];
+        } else {
+#pragma unroll
+            for (int t = 0; t < TAPS; ++t) {
+                if (!live(t)) continue;
+#pragma unroll
+                for (int g = 0; g < TP; ++g)
+#pragma unroll
+                    for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                        for (int nt = 0; nt < NT; ++nt) acc[g][nt] = mma(wa[t][kc][nt], b[t][g][kc], acc[g][nt]);
+            }
+            if (task + step < ntask) {
+                P.decode(a, task + step, fr, PY, PX);
+                load(P, b);
+            }
+        }
+        // epilogue: lane holds channels nt*16 + fc*4 + r of pixel fr of group g
+#pragma unroll
+        for (int g = 0; g < TP; ++g) {
+            if (!Q.ok[g]) continue;
+            const int64_t ob = int64_t(Q.n[g]) * a.y_bs + (int64_t(Q.oh[g]) * a.OW + Q.ow[g]) * a.y_ld;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) {
+                const int cb = nt * 16 + fc * 4;
+                if (cb >= a.Nout) continue;                 // Nout % 8 == 0: 4-channel groups are whole
+                const f32x4 v = acc[g][nt];
+                uint2 o;
+                if constexpr (MODE == 0) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        ssum[nt][r] += v[r];
+                        ssq[nt][r] += v[r] * v[r];
+                    }
+                    o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
+                    o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
+                } else {
+                    float w4[4] = {v[0], v[1], v[2], v[3]};
+                    if (a.accumulate) {
+                        const uint2 old = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(a.y) + ob + cb);
+                        w4[0] += bf2f(bf16_t(old.x & 0xffff)); w4[1] += bf2f(bf16_t(old.x >> 16));
+                        w4[2] += bf2f(bf16_t(old.y & 0xffff)); w4[3] += bf2f(bf16_t(old.y >> 16));
+                    }
+                    o.x = pk2bf(w4[0], w4[1]);
+                    o.y = pk2bf(w4[2], w4[3]);
+                }
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(a.y) + ob + cb) = o;
+            }
+        }
+    }
+}
+
+// grid (blocks, classes): blockIdx.y is the output-parity class of a stride-2 data gradient
+template <int NT, int KC, int KS, int S, int MODE, int TP>
+__global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
+    __shared__ float red[2][4][16 * NT];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int fr = lane & 15, fc = lane >> 4;
+    float ssum[NT][4], ssq[NT][4];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ssum[nt][r] = ssq[nt][r] = 0.f;
+    const int64_t first = int64_t(blockIdx.x) * 4 + wave, step = int64_t(gridDim.x) * 4;
+    if constexpr (S == 2 && MODE == 1) {
+        switch (blockIdx.y) {
+            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step); break;
+            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step); break;
+            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step); break;
+            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step); break;
+        }
+    } else {
+        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step);
+    }
+    if constexpr (MODE == 0) {
+        if (!a.st_sum) return;
+        // 16 pixel lanes per channel group, then the 4 waves in order
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = ssum[nt][r], q = ssq[nt][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    s += __shfl_xor(s, o, 64);
+                    q += __shfl_xor(q, o, 64);
+                }
+                if (fr == 0) {
+                    red[0][wave][nt * 16 + fc * 4 + r] = s;
+                    red[1][wave][nt * 16 + fc * 4 + r] = q;
+                }
+            }
+        __syncthreads();
+        for (int c = threadIdx.x; c < a.Nout; c += 256) {
+            a.st_sum[int64_t(blockIdx.x) * a.Nout + c] = (red[0][0][c] + red[0][1][c]) + (red[0][2][c] + red[0][3][c]);
+            a.st_sq[int64_t(blockIdx.x) * a.Nout + c] = (red[1][0][c] + red[1][1][c]) + (red[1][2][c] + red[1][3][c]);
+        }
+    }
+}
+
+using KernFn = void (*)(DirArgs);
+
+struct Variant {
+    int nt, kc, ks, s, mode, tp;
+    KernFn fn;
+};
+
+#define YM_DIR(NT, KC, KS, S, MODE, TP) {NT, KC, KS, S, MODE, TP, conv_direct_kernel<NT, KC, KS, S, MODE, TP>}
+// the YOLOv11 stem-stage layers (s@640: stem 1->32 s2 has its own kernel; model.1 32->64 3x3 s2,
+// C3k2 64->64 1x1 / 32->32 3x3 / 96->128 1x1) in both directions (an 80x80 128->128 1x1 variant
+// measured slower than the implicit GEMM: 0.083 vs 0.076 ms)
+const Variant kVariants[] = {
+    YM_DIR(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
+    YM_DIR(2, 2, 3, 2, 1, 2),   // dgrad of it: dz 64 -> dx 32, 4 parity classes
+    YM_DIR(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
+    YM_DIR(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
+    YM_DIR(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
+    YM_DIR(4, 2, 1, 1, 1, 4),
+    YM_DIR(8, 3, 1, 1, 0, 2),   // fwd 96 -> 128 1x1
+    YM_DIR(6, 4, 1, 1, 1, 2),   // dgrad: dz 128 -> dx 96
+};
+#undef YM_DIR
+
+int direct_mode() {
+    if (g_direct_force >= 0) return g_direct_force;
+    static const int v = [] {
+        const char* e = getenv("YM_CONV_DIRECT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+
+}  // namespace
+
+DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
+    DirectPlan p{};
+    const int mode = direct_mode();
+    if (!d || mode == 0) return p;
+    if (d->k != 1 && d->k != 3) return p;
+    if (d->pad != d->k / 2 || (d->stride != 1 && d->stride != 2)) return p;
+    if (dgrad && d->k == 1 && d->stride != 1) return p;
+    const int kin = dgrad ? d->cout : d->cin, nout = dgrad ? d->cin : d->cout;
+    if (kin % 32 || nout % 8) return p;
+    if (!dgrad && d->out_f32 != 2) return p;          // z (fp16) of a Conv block only
+    const int64_t in_ld = dgrad ? d->y_ld : d->x_ld, in_bs = dgrad ? d->y_bs : d->x_bs;
+    const int64_t out_ld = dgrad ? d->x_ld : d->y_ld, out_bs = dgrad ? d->x_bs : d->y_bs;
+    if (in_ld % 8 || in_bs % 8 || out_ld % 4 || out_bs % 4) return p;
+    if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31)) return p;
+    // high-resolution maps only (where the implicit GEMMs are latency-bound): >= 1 M output pixels
+    const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
+    const int64_t M = int64_t(d->n) * OH * OW;
+    if (mode == 1 && M < (int64_t(1) << 20)) return p;
+    for (int i = 0; i < int(sizeof(kVariants) / sizeof(kVariants[0])); ++i) {
+        const Variant& v = kVariants[i];
+        if (v.mode != dgrad || v.ks != d->k || v.s != d->stride || v.kc * 32 != kin) continue;
+        if (v.nt * 16 < nout || (v.nt - 1) * 16 >= nout) continue;
+        p.ok = 1;
+        p.variant = i;
+        const int os = dgrad ? d->stride : 1;
+        const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
+        const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
+        p.classes = os * os;
+        p.grid = int(std::max<int64_t>(1, std::min<int64_t>(1024 / p.classes, (tpc + 3) / 4)));
+        return p;
+    }
+    return p;
+}
+
+int direct_launch(const DirectPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w,
+                  void* y, float* st_sum, float* st_sq, hipStream_t st) {
+    const Variant& v = kVariants[p.variant];
+    DirArgs a{};
+    a.x = x; a.w = w; a.y = y;
+    if (!dgrad) {
+        a.x_bs = d->x_bs; a.x_ld = d->x_ld; a.y_bs = d->y_bs; a.y_ld = d->y_ld;
+        a.GH = d->h; a.GW = d->w; a.OH = d->oh; a.OW = d->ow; a.Kin = d->cin; a.Nout = d->cout;
+        a.st_sum = st_sum; a.st_sq = st_sq;
+    } else {
+        a.x_bs = d->y_bs; a.x_ld = d->y_ld; a.y_bs = d->x_bs; a.y_ld = d->x_ld;
+        a.GH = d->oh; a.GW = d->ow; a.OH = d->h; a.OW = d->w; a.Kin = d->cout; a.Nout = d->cin;
+    }
+    a.N = d->n; a.pad = d->pad; a.accumulate = d->accumulate;
+    const int os = dgrad ? d->stride : 1;
+    a.OHc = (a.OH + os - 1) / os; a.OWc = (a.OW + os - 1) / os;
+    a.ncls = os * os;
+    a.tpc = (int64_t(a.N) * a.OHc * a.OWc + 16 * v.tp - 1) / (16 * v.tp);
+    hipLaunchKernelGGL(v.fn, dim3(p.grid, a.ncls), dim3(256), 0, st, a);
+    return 0;
+}
+
+}  // namespace ym

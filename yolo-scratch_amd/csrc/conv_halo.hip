@@ -21,6 +21,7 @@
 // and flipped tap offsets.
 #include <algorithm>
 
+#include "bnfold.h"
 #include "common.h"
 #include "conv_halo.h"
 #include "tile.h"
@@ -43,6 +44,7 @@ struct HaloArgs {
     int RT, CT;                               // tiles per image: rows, cols
     int ntiles;
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
+    BnFold fold;                              // fused BN finalize (fold.cnt null: none)
 };
 
 // 64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1).
@@ -340,10 +342,11 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WPX; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = pq;
+                st_row(&a.st_sum[int64_t(blockIdx.x) * a.Nout + ch], ps, a.fold.cnt != nullptr);
+                st_row(&a.st_sq[int64_t(blockIdx.x) * a.Nout + ch], pq, a.fold.cnt != nullptr);
             }
         }
+        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, blockIdx.x, smem);
     }
 }
 
@@ -418,7 +421,7 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
+                const float* bias, float* st_sum, float* st_sq, const BnFold* fold, hipStream_t st) {
     HaloArgs a{};
     a.x = x;
     a.w = w;
@@ -438,6 +441,10 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     a.accumulate = d->accumulate;
     a.TH = p.TH; a.TW = p.TW; a.HWd = p.TW + 2; a.HP = (p.TH + 2) * (p.TW + 2);
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
+    if (fold && st_sum) {
+        a.fold = *fold;
+        bn_fold_groups(a.fold, p.gx, p.nco);
+    }
     const dim3 grid(p.gx, p.nco);
     static const int abl = [] {
         const char* e = getenv("YM_HALO_ABL");

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "bnfold.h"
 #include "common.h"
 #include "conv_pipe.h"
 #include "tile.h"
@@ -56,6 +57,7 @@ struct PipeArgs {
     int ntiles;                               // channel tiles
     int mt_pre[5];                            // first m-tile of each class (prefix), mt_pre[ncls] = total
     int ncls;
+    BnFold fold;                              // fused BN finalize (fold.cnt null: none)
 };
 
 struct Cls {
@@ -470,10 +472,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
-                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
+                st_row(&a.st_sum[int64_t(row) * a.Nout + ch], ps, a.fold.cnt != nullptr);
+                st_row(&a.st_sq[int64_t(row) * a.Nout + ch], pq, a.fold.cnt != nullptr);
             }
         }
+        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, row, smem);
     }
 }
 
@@ -561,7 +564,7 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
+                const float* bias, float* st_sum, float* st_sq, const BnFold* fold, hipStream_t st) {
     PipeArgs a{};
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
     if (!dgrad) {
@@ -584,6 +587,10 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad; a.N = d->n;
     a.accumulate = d->accumulate;
     a.ntiles = (a.Nout + bn - 1) / bn;
+    if (fold && st_sum) {
+        a.fold = *fold;
+        bn_fold_groups(a.fold, p.rows, a.ntiles);
+    }
     a.ncls = a.os == 2 ? 4 : 1;
     int acc = 0;
     for (int c = 0; c < a.ncls; ++c) {

@@ -27,6 +27,13 @@ class ConvDesc(ctypes.Structure):
                 ("y_ld", I64), ("out_f32", I32), ("accumulate", I32)]
 
 
+class BnTrain(ctypes.Structure):
+    """ym_bn_train (include/yolomi.h): BatchNorm state + outputs of the fused statistics finalize."""
+    _fields_ = [("gamma", P), ("beta", P), ("running_mean", P), ("running_var", P), ("num_batches_tracked", P),
+                ("momentum", F32), ("eps", F32), ("scale", P), ("shift", P), ("mean", P), ("rstd", P),
+                ("workspace", P)]
+
+
 class AdamWEntry(ctypes.Structure):
     """ym_adamw_entry (include/yolomi.h)."""
     _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("offset", I64), ("n", I64)]
@@ -52,14 +59,18 @@ SIGNATURES = {
     "ym_conv_algo": (R, [P, INT]),
     "ym_conv_set_halo": (R, [INT]),
     "ym_conv_set_pipe": (R, [INT]),
+    "ym_conv_set_direct": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
+    "ym_conv_fwd_bn": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_fwd_bn": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P, P]),
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
+    "ym_dw3x3_fwd_bn": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P, P]),
     "ym_dw3x3_bwd_workspace_size": (SZ, [INT]),
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
@@ -70,6 +81,7 @@ SIGNATURES = {
     "ym_bn_bwd_blocks": (R, [I64, INT]),
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P, P]),
+    "ym_bn_bwd_reduce_finalize": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply_res": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, I64, I64, INT, P]),
     "ym_maxpool5_f32_fwd": (R, [P, P, P, P, I64, I64, INT, INT, INT, INT, P]),

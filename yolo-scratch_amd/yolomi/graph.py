@@ -23,7 +23,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
+from ._lib import BnTrain, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
 
 BF16 = torch.bfloat16
 F16 = torch.float16
@@ -162,6 +162,16 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def bn_fold_on():
+    """YM_BN_FOLD=1: training BatchNorm statistics finalized inside the kernel that produces them
+    (ym_conv_fwd_bn, ym_bn_bwd_reduce_finalize, ...) instead of a separate ym_bn_finalize /
+    ym_bn_bwd_finalize launch.  Off by default: measured 2678 vs 2798 img/s (s@640 bs64) — every
+    workgroup's ticket (write-through stores, vmcnt(0), barrier, agent atomic) plus the elected
+    workgroups' two-level fold cost the conv forward family +1.5 ms/step, more than the 154 finalize
+    launches it removes."""
+    return os.environ.get("YM_BN_FOLD", "0") == "1"
+
+
 # buffer-range keys for the stream scheduler: ('a' activation | 'g' gradient, Act id, c0, c1)
 def _ka(v):
     return ("a", id(v.act), v.c0, v.c0 + v.c)
@@ -216,9 +226,10 @@ class ConvBN:
         w = [_kg(self.y)] + ([_kg(self.x)] if plan.needs_grad(self.x) else []) + ([_kg(self.res)] if self.res else [])
         return [_ka(self.x), _kg(self.y)], w
 
-    def _timed(self, plan, kind, stream, fn):
-        """Run one conv launch; the bench brackets it with HIP events on its own stream when it times
-        this op (plan.probe) or this kernel family (plan.family_events: 'fwd' / 'dgrad' / 'wgrad')."""
+    def _timed(self, plan, kind, stream, fn, work=None):
+        """Run one launch; the bench brackets it with HIP events on its own stream when it times this
+        op (plan.probe) or this kernel family (plan.family_events: conv 'fwd' / 'dgrad' / 'wgrad' with
+        their algorithmic FLOPs, 'bn' with its algorithmic HBM bytes in `work`)."""
         fam = plan.family_events
         probe = kind == "fwd" and plan.probe is self
         if not probe and (fam is None or kind not in fam):
@@ -231,47 +242,97 @@ class ConvBN:
         if probe:
             plan.probe_events.append((ev0, ev1))
         if fam is not None and kind in fam:
-            fam[kind].append((ev0, ev1, self))
+            fam[kind].append((ev0, ev1, self.flops() if work is None else work))
+
+    def _bn_train(self, plan):
+        """ym_bn_train for the fused finalize (pointers only; the workspace is the current stream's)."""
+        bn = self.m.bn
+        t = BnTrain()
+        t.gamma, t.beta = _p(bn.weight), _p(bn.bias)
+        t.running_mean, t.running_var = _p(bn.running_mean), _p(bn.running_var)
+        t.num_batches_tracked = _p(bn.num_batches_tracked)
+        t.momentum, t.eps = float(bn.momentum), float(bn.eps)
+        t.scale, t.shift, t.mean, t.rstd = (self.bnv[i].data_ptr() for i in range(4))
+        t.workspace = plan.bn_ws.data_ptr()
+        return t
+
+    def _bn_fwd(self, plan, st, ss, sq, finalized=False):
+        """BatchNorm finalize + apply (+ SiLU, + residual) of the forward: 'bn' family, algorithmic bytes
+        = the partial rows read + z read + y written (+ residual read)."""
+        bn = self.m.bn
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        r = self.res
+        e = self.M * self.co * 2
+        work = 8 * self.G * self.co * (1 if plan.training and not finalized else 0) + 2 * e + (e if r else 0)
+
+        def run():
+            if finalized:
+                pass
+            elif plan.training:
+                call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
+                     _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+                     float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
+            else:
+                call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
+                     _p(bn.running_var), float(bn.eps), sc, sh, st)
+            call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, self.act,
+                 r.ptr() if r else None, r.bs if r else 0, r.ld if r else 0, self.y.ptr(), self.y.bs, self.y.ld,
+                 _p(getattr(self, "out32", None)), st)
+        self._timed(plan, "bn", plan._cur_stream, run, work)
 
     def forward(self, plan, st):
-        bn = self.m.bn
         ss, sq = self.ps[0], self.ps[1]
+        if plan.training and bn_fold_on():
+            bt = self._bn_train(plan)
+            self._timed(plan, "fwd", plan._cur_stream, lambda: call(
+                "ym_conv_fwd_bn", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(),
+                ss.data_ptr(), sq.data_ptr(), ctypes.byref(bt), st))
+            self._bn_fwd(plan, st, ss, sq, finalized=True)
+            return
         self._timed(plan, "fwd", plan._cur_stream, lambda: call(
             "ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
             ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st))
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        if plan.training:
-            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
-                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-        else:
-            call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
-                 float(bn.eps), sc, sh, st)
-        r = self.res
-        call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, self.act,
-             r.ptr() if r else None, r.bs if r else 0, r.ld if r else 0, self.y.ptr(), self.y.bs, self.y.ld,
-             _p(getattr(self, "out32", None)), st)
+        self._bn_fwd(plan, st, ss, sq)
 
-    def backward(self, plan, st):
+    def _bn_bwd(self, plan, st, dy):
+        """BatchNorm (+ SiLU) backward: statistics pass over dy and z, finalize (dgamma, dbeta, apply
+        coefficients), then dz = f(dy, z) written over z (+ the shortcut's gradient from the same dy
+        read).  'bn' family: algorithmic bytes = dy + z read twice, dz written, partial rows, the
+        shortcut gradient written (and read when it accumulates)."""
         bn = self.m.bn
-        dy = self.y.grad_for_read(st)
         sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
         Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
-        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
-             self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-        dz = self.z  # reuse the z buffer? no: z is needed by nobody after this op -> in-place dz
-        if self.res is not None:
-            # the shortcut's gradient (dres (+)= dy) comes out of the same pass over dy
-            acc = self.res.grad_for_write(st)
-            call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
-                 mu, rs, self.act, self.coef.data_ptr(), dz.data_ptr(), self.res.gptr(), self.res.bs, self.res.ld,
-                 acc, st)
-            self.res.mark()
-        else:
-            call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu,
-                 rs, self.act, self.coef.data_ptr(), dz.data_ptr(), st)
+        r = self.res
+        racc = r.grad_for_write(st) if r is not None else 0
+        e = self.M * self.co * 2
+        fold = bn_fold_on()
+        work = 5 * e + 16 * Gb * self.co + ((2 + racc) * e if r is not None else 0)
+
+        def run():
+            if fold:
+                call("ym_bn_bwd_reduce_finalize", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co,
+                     self.HW, sc, sh, mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), _p(bn.weight),
+                     plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
+            else:
+                call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                     mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+                call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+                     _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
+                     plan.bn_ws.data_ptr(), st)
+            if r is not None:
+                call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc,
+                     sh, mu, rs, self.act, self.coef.data_ptr(), self.z.data_ptr(), r.gptr(), r.bs, r.ld, racc, st)
+            else:
+                call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                     mu, rs, self.act, self.coef.data_ptr(), self.z.data_ptr(), st)
+        self._timed(plan, "bn", plan._cur_stream, run, work)
+        if r is not None:
+            r.mark()
+
+    def backward(self, plan, st):
+        dy = self.y.grad_for_read(st)
+        self._bn_bwd(plan, st, dy)      # dz over z (z is needed by nobody after this op)
+        dz = self.z
         # weight gradient: on the side stream, beside this layer's data gradient and the next BN backward
         ws = plan.wgrad_ws()
         sst = plan.side(st)
@@ -311,33 +372,22 @@ class StemConvBN(ConvBN):
         self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
 
     def forward(self, plan, st):
-        bn = self.m.bn
         ss, sq = self.ps[0], self.ps[1]
         B = plan.B
+        if plan.training and bn_fold_on():
+            bt = self._bn_train(plan)
+            call("ym_conv_first_fwd_bn", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(),
+                 ss.data_ptr(), sq.data_ptr(), B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G,
+                 ctypes.byref(bt), st)
+            self._bn_fwd(plan, st, ss, sq, finalized=True)
+            return
         call("ym_conv_first_fwd", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(), ss.data_ptr(),
              sq.data_ptr(), B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        if plan.training:
-            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
-                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-        else:
-            call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
-                 float(bn.eps), sc, sh, st)
-        call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, 1, None, 0, 0, self.y.ptr(),
-             self.y.bs, self.y.ld, None, st)
+        self._bn_fwd(plan, st, ss, sq)
 
     def backward(self, plan, st):
-        bn = self.m.bn
         dy = self.y.grad_for_read(st)
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
-        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
-             1, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-        call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, mu, rs,
-             1, self.coef.data_ptr(), self.z.data_ptr(), st)
+        self._bn_bwd(plan, st, dy)
         ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
         call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight), plan.B,
              self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
@@ -364,36 +414,22 @@ class DWConvBN(ConvBN):
         self.coef = torch.empty(3, C, dtype=F32, device=plan.dev)
 
     def forward(self, plan, st):
-        bn = self.m.bn
         ss, sq = self.ps[0], self.ps[1]
         gsz, gstr, goff = self.map
+        if plan.training and bn_fold_on():
+            bt = self._bn_train(plan)
+            call("ym_dw3x3_fwd_bn", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
+                 self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G,
+                 ctypes.byref(bt), st)
+            self._bn_fwd(plan, st, ss, sq, finalized=True)
+            return
         call("ym_dw3x3_fwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
              self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G, st)
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        if plan.training:
-            call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.C, float(self.M), _p(bn.weight),
-                 _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                 float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-        else:
-            call("ym_bn_eval_coeff", self.C, _p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var),
-                 float(bn.eps), sc, sh, st)
-        r = self.res
-        call("ym_bn_apply", self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, 0, r.ptr(), r.bs, r.ld, self.y.ptr(),
-             self.y.bs, self.y.ld, None, st)
+        self._bn_fwd(plan, st, ss, sq)
 
     def backward(self, plan, st):
-        bn = self.m.bn
         dy = self.y.grad_for_read(st)
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        Gb = lib().ym_bn_bwd_blocks(self.M, self.C)
-        call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu, rs,
-             0, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-        call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.C, float(self.M),
-             _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-        acc = self.res.grad_for_write(st)
-        call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.C, self.HW, sc, sh, mu,
-             rs, 0, self.coef.data_ptr(), self.z.data_ptr(), self.res.gptr(), self.res.bs, self.res.ld, acc, st)
-        self.res.mark()
+        self._bn_bwd(plan, st, dy)
         # dx into the v channels of dqkv (accumulate if the attention core wrote them already)
         hd, hs, goff = self.map
         heads = self.C // hd
