@@ -196,7 +196,7 @@ typedef struct {
 /* ym_conv_fwd (out_f32 = 2, statistics required) + ym_bn_finalize in one launch; count = n*oh*ow. */
 int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* z, float* stat_sum,
                    float* stat_sq, const ym_bn_train* bn, void* stream);
-/* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0). */
+/* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0); y = NULL: statistics only. */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
 /* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
@@ -208,6 +208,24 @@ int ym_conv_first_fwd_bn(const float* img, const float* w_oihw, uint16_t* y, flo
                          const ym_bn_train* bn, void* stream);
 int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
                         int cout, int stride, int pad, float* workspace, size_t workspace_bytes, void* stream);
+/* The stem Conv block with its pre-BatchNorm z recomputed from the image instead of stored (z is
+ * the step's largest tensor; 9 MACs per element): ym_stem_stats gives the forward statistics
+ * ([blocks][cout] partials for ym_bn_finalize), ym_stem_apply writes act = SiLU(z*scale + shift) (fp16) into the y view; the
+ * backward's ym_stem_bwd_reduce gives the [blocks][cout] partials of sum(g), sum(g*xhat) for
+ * ym_bn_bwd_finalize, and ym_stem_bwd_wgrad forms dz and adds the weight gradient into dw_oihw
+ * without storing dz.  bnv: [4][cout] scale, shift, mean, rstd; coef: ym_bn_bwd_finalize's. */
+int ym_stem_stats(const float* img, const float* w_oihw, float* stat_sum, float* stat_sq, int blocks, int n, int h,
+                  int w, int oh, int ow, int cout, int stride, int pad, void* stream);
+int ym_stem_apply(const float* img, const float* w_oihw, const float* scale, const float* shift, uint16_t* y,
+                  int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
+                  void* stream);
+int ym_stem_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
+                       const float* bnv, float* part_sum, float* part_dot, int blocks, int n, int h, int w, int oh,
+                       int ow, int cout, int stride, int pad, void* stream);
+size_t ym_stem_bwd_wgrad_workspace_size(int cout);
+int ym_stem_bwd_wgrad(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
+                      const float* bnv, const float* coef, float* dw_oihw, float* workspace, size_t workspace_bytes,
+                      int n, int h, int w, int oh, int ow, int cout, int stride, int pad, void* stream);
 /* Depthwise 3x3 s1 p1 (Attention.pe, yolo11_modules.py:122); input channel c reads source
  * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
 int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,

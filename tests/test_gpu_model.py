@@ -326,3 +326,31 @@ def test_loss_with_host_max_gt_matches_synced_count():
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     for a, c in zip(outs[0][2], outs[1][2]):
         assert torch.equal(a, c)
+
+
+def test_stem_recompute_matches_stored(golden, monkeypatch):
+    """The stem Conv block (1 -> 32, 3x3 s2) with z recomputed from the image (ym_stem_stats / _apply /
+    _bwd_reduce / _bwd_wgrad) against the stored-z path on the same input and output gradient: the
+    same fp16 / bf16 roundings at the same points, the statistics summed in a different fixed order
+    (so a few fp16 outputs differ by one ulp): y within 1e-3, parameter gradients and running
+    statistics within 1e-4 (relative L2)."""
+    import models as M
+    d = golden("blocks.npz")
+    sd = {k[len("conv0") + 3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("conv0/p:")}
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("YM_STEM_RECOMPUTE", flag)      # read when the block's plan is built
+        mod = M.Conv(1, 32, 3, 2)
+        mod.load_state_dict(sd)
+        mod.bn.eps, mod.bn.momentum = 1e-3, 0.03
+        mod = mod.cuda().train()
+        y = mod(torch.from_numpy(d["conv0/x"]).cuda())
+        y.backward(torch.from_numpy(d["conv0/dy"]).cuda())
+        out.append((y.detach().float().cpu(), {k: p.grad.detach().cpu() for k, p in mod.named_parameters()},
+                    {k: v.detach().cpu() for k, v in mod.state_dict().items() if "running" in k}))
+    (y0, g0, s0), (y1, g1, s1) = out
+    assert rel(y1, y0) < 1e-3, rel(y1, y0)
+    for k in g0:
+        assert rel(g1[k], g0[k]) < 1e-4, (k, rel(g1[k], g0[k]))
+    for k in s0:
+        assert rel(s1[k], s0[k]) < 1e-5, k

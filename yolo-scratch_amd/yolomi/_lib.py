@@ -66,6 +66,11 @@ SIGNATURES = {
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_stem_stats": (R, [P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_stem_apply": (R, [P, P, P, P, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_stem_bwd_reduce": (R, [P, I64, I64, P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_stem_bwd_wgrad_workspace_size": (SZ, [INT]),
+    "ym_stem_bwd_wgrad": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_conv_first_fwd_bn": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P, P]),
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),

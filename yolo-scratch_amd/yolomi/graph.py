@@ -349,6 +349,15 @@ class ConvBN:
             self.x.mark()
 
 
+def stem_recompute_on():
+    """YM_STEM_RECOMPUTE=1: the stem's pre-BatchNorm z recomputed from the image (ym_stem_stats /
+    _apply / _bwd_reduce / _bwd_wgrad) instead of stored — 2.5 GB less HBM traffic and 420 MB less
+    memory per s@640 bs64 step, but its VALU passes (9-tap conv + SiLU derivative + weight-gradient
+    outer product per element) run 0.16-0.41 ms each, so the step measured the same (2938 vs 2931
+    img/s): off by default until those passes move to MFMA."""
+    return os.environ.get("YM_STEM_RECOMPUTE", "0") == "1"
+
+
 class StemConvBN(ConvBN):
     """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
 
@@ -365,14 +374,43 @@ class StemConvBN(ConvBN):
         oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
         assert (oh, ow) == (y.H, y.W)
         self.M, self.HW, self.oh, self.ow = B * oh * ow, oh * ow, oh, ow
-        self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
+        self.recompute = stem_recompute_on()
+        # z only when it is stored (the recompute path never materialises it)
+        self.z = None if self.recompute else torch.empty(self.M, co, dtype=BF16, device=plan.dev)
         self.G = 1024
-        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
+        self.Gb = 1024
+        self.ps = torch.empty(2, max(self.G, self.Gb, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
         self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)
         self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
 
+    def _geo(self, plan):
+        return (plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1)
+
     def forward(self, plan, st):
         ss, sq = self.ps[0], self.ps[1]
+        if not self.recompute:
+            self._forward_stored(plan, st, ss, sq)
+            return
+        bn = self.m.bn
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        if plan.training:
+            call("ym_stem_stats", plan.img.data_ptr(), _p(self.m.conv.weight), ss.data_ptr(), sq.data_ptr(), self.G,
+                 *self._geo(plan), st)
+        e = self.M * self.co * 2
+
+        def run():
+            if plan.training:
+                call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
+                     _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+                     float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
+            else:
+                call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
+                     _p(bn.running_var), float(bn.eps), sc, sh, st)
+            call("ym_stem_apply", plan.img.data_ptr(), _p(self.m.conv.weight), sc, sh, self.y.ptr(), self.y.bs,
+                 self.y.ld, *self._geo(plan), st)
+        self._timed(plan, "bn", plan._cur_stream, run, e + 4 * plan.B * self.H * self.W)
+
+    def _forward_stored(self, plan, st, ss, sq):
         B = plan.B
         if plan.training and bn_fold_on():
             bt = self._bn_train(plan)
@@ -387,10 +425,27 @@ class StemConvBN(ConvBN):
 
     def backward(self, plan, st):
         dy = self.y.grad_for_read(st)
-        self._bn_bwd(plan, st, dy)
-        ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
-        call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight), plan.B,
-             self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
+        if not self.recompute:
+            self._bn_bwd(plan, st, dy)
+            ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
+            call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight),
+                 plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
+            return
+        bn = self.m.bn
+        rs = self.bnv[3].data_ptr()
+        ps, pd = self.ps[0], self.ps[1]
+        ws = plan.private_ws(self, lib().ym_stem_bwd_wgrad_workspace_size(self.co))
+        e = self.M * self.co * 2
+
+        def run():
+            call("ym_stem_bwd_reduce", dy, self.y.bs, self.y.ld, plan.img.data_ptr(), _p(self.m.conv.weight),
+                 self.bnv.data_ptr(), ps.data_ptr(), pd.data_ptr(), self.Gb, *self._geo(plan), st)
+            call("ym_bn_bwd_finalize", ps.data_ptr(), pd.data_ptr(), self.Gb, self.co, float(self.M), _p(bn.weight), rs,
+                 plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
+            call("ym_stem_bwd_wgrad", dy, self.y.bs, self.y.ld, plan.img.data_ptr(), _p(self.m.conv.weight),
+                 self.bnv.data_ptr(), self.coef.data_ptr(), plan.gptr(self.m.conv.weight), ws.data_ptr(),
+                 ws.numel() * 4, *self._geo(plan), st)
+        self._timed(plan, "bn", plan._cur_stream, run, 2 * e + 8 * plan.B * self.H * self.W)
 
 
 class DWConvBN(ConvBN):
