@@ -150,12 +150,14 @@ int ym_conv_fwd_stat_rows(const ym_conv_desc* d);
  * stride-1 kernel, 0 = the 2-stage implicit GEMM. */
 int ym_conv_algo(const ym_conv_desc* d, int dgrad);
 /* Selection policy of the halo-staged kernel for later calls: -1 YM_CONV_HALO / default, 0 never,
- * 1 wherever it applies, 2 where it measured faster (default: maps <= 24 wide).  Returns the
- * previous setting.  Process-wide; not for use while other threads launch convolutions. */
+ * 1 wherever it applies, 2 maps <= 24 wide, 3 (default) maps <= 48 wide or <= 64 output channels.
+ * Returns the previous setting.  Process-wide; not for use while other threads launch convolutions. */
 int ym_conv_set_halo(int mode);
 /* Selection policy of the persistent pipelined implicit GEMM (conv_pipe.hip) for later calls: -1
- * YM_CONV_PIPE / default, 0 never, 1 layers of >= 1024 256-pixel tiles (default), 2 >= 256 tiles.
- * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+ * YM_CONV_PIPE / default, 0 never, 1 layers of >= 1024 256-pixel tiles with >= 128 output channels,
+ * 2 every eligible layer of >= 256 tiles, 3 (default) every 1x1 and the 3x3 with >= 128 output
+ * channels (forward: or inputs) at >= 256 tiles, never a stride-2 data gradient.  Returns the
+ * previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_pipe(int mode);
 /* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
  * layers) for later calls: -1 YM_CONV_DIRECT / default, 0 never, 1 maps of >= 1 M output pixels

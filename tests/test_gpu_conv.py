@@ -61,7 +61,7 @@ def _desc(n, h, w, cin, cout, k, s, p):
 def halo_mode(request):
     """Run each shape under the default kernel selection and with the halo kernel wherever it applies."""
     from yolomi._lib import lib
-    prev = lib().ym_conv_set_halo(2 if request.param == "auto" else 1)
+    prev = lib().ym_conv_set_halo(-1 if request.param == "auto" else 1)
     yield request.param
     lib().ym_conv_set_halo(prev)
 
@@ -128,13 +128,21 @@ HALO = [(2, 32, 32, 64, 128, 3, 1, 1), (5, 20, 20, 96, 64, 3, 1, 1), (1, 40, 40,
 
 def test_halo_kernel_selected(halo_mode):
     """The 3x3 stride-1 shapes above with >= 64 output channels run the halo kernel (fwd) when forced;
-    by default only maps <= 24 wide do."""
+    by default maps <= 48 wide or with <= 64 output channels do (rule 3), rule 2 only maps <= 24 wide."""
     from yolomi._lib import lib
     if halo_mode == "auto":
         d, _, _ = _desc(5, 20, 20, 96, 64, 3, 1, 1)
         assert lib().ym_conv_algo(ctypes.byref(d), 0) == 1
         d, _, _ = _desc(1, 40, 40, 128, 136, 3, 1, 1)
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 1
+        d, _, _ = _desc(1, 56, 56, 128, 136, 3, 1, 1)
         assert lib().ym_conv_algo(ctypes.byref(d), 0) == 0
+        prev = lib().ym_conv_set_halo(2)
+        try:
+            d, _, _ = _desc(1, 40, 40, 128, 136, 3, 1, 1)
+            assert lib().ym_conv_algo(ctypes.byref(d), 0) == 0
+        finally:
+            lib().ym_conv_set_halo(prev)
         return
     for shape in HALO:
         d, _, _ = _desc(*shape)

@@ -800,7 +800,7 @@ extern "C" int ym_conv_set_pipe(int mode) {
     // selection policy of the pipelined implicit GEMM: -1 env/default, 0 never, 1 layers of >= 1024
     // tiles (default), 2 >= 256 tiles; returns the previous setting
     const int prev = g_pipe_force;
-    g_pipe_force = mode < -1 || mode > 2 ? -1 : mode;
+    g_pipe_force = mode < -1 || mode > 3 ? -1 : mode;
     return prev;
 }
 

@@ -15,7 +15,8 @@ struct HaloPlan {
     int gx;              // grid x (= rows of the BN statistics partials)
 };
 
-// -1: YM_CONV_HALO / default policy; 0 never; 1 wherever it applies; 2 default policy (ym_conv_set_halo)
+// -1: YM_CONV_HALO / default policy (3); 0 never; 1 wherever it applies; 2 maps <= 24 wide; 3 maps <= 48
+// wide or <= 64 output channels (ym_conv_set_halo)
 extern int g_halo_force;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient

@@ -376,13 +376,13 @@ int g_halo_force = -1;
 
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
     HaloPlan p{};
-    // YM_CONV_HALO=0: never, =1: wherever it applies, unset (2): maps <= 24 wide (the 20x20 layers).
-    // With the conflict-free swizzle the halo kernel also wins most 40x40 layers and the <= 64-channel
-    // 80x80 ones in isolation (tools/layer_bench.py: -2..-25 %), but selecting it there measured
-    // 0.5 % slower on the whole step (=3: that wider rule, for A/B runs)
+    // YM_CONV_HALO=0: never, =1: wherever it applies, =2: maps <= 24 wide (the 20x20 layers), unset (3):
+    // maps <= 48 wide or <= 64 output channels — with the pipelined kernel taking the >= 128-channel
+    // layers first, this rule measured 2953 vs 2940 img/s over rule 2 (s@640 bs64); in round 1, before
+    // the pipelined kernel, it was 0.5 % slower
     static const int mode = [] {
         const char* e = getenv("YM_CONV_HALO");
-        return !e ? 2 : (e[0] == '0' ? 0 : e[0] == '3' ? 3 : 1);
+        return !e ? 3 : (e[0] == '0' ? 0 : e[0] == '2' ? 2 : e[0] == '3' ? 3 : 1);
     }();
     const int force = g_halo_force >= 0 ? g_halo_force : mode;
     if (force == 0) return p;

@@ -15,7 +15,8 @@ struct PipePlan {
     int rows;        // rows of the BN statistics partials (= grid / channel tiles)
 };
 
-// -1: YM_CONV_PIPE / default policy; 0 never; 1 layers of >= 1024 tiles; 2 >= 256 tiles (ym_conv_set_pipe)
+// -1: YM_CONV_PIPE / default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
+// tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
 extern int g_pipe_force;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient

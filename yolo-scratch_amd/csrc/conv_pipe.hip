@@ -35,7 +35,9 @@
 
 namespace ym {
 
-// selection policy: -1 YM_CONV_PIPE / default (1); 0 never; 1 layers of >= 1024 tiles; 2 >= 256 tiles
+// selection policy: -1 YM_CONV_PIPE / default (3); 0 never; 1 layers of >= 1024 tiles with >= 128
+// output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
+// wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
 int g_pipe_force = -1;
 
 namespace {
@@ -489,7 +491,7 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
 static int pipe_mode() {
     static const int env = [] {
         const char* e = getenv("YM_CONV_PIPE");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 3;
     }();
     return g_pipe_force >= 0 ? g_pipe_force : env;
 }
@@ -540,9 +542,12 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     if (in_ld % 8 || in_bs % 8 || out_ld % 4 || out_bs % 4) return p;
     if (!dgrad && d->out_f32 == 1) return p;       // Detect's fp32 bias convs stay on conv.hip
     const int os = dgrad ? d->stride : 1;
-    // default policy: only where it measured faster than conv.hip / conv_halo.hip (tools/pipe_check.py,
-    // DESIGN.md §conv): >= 128 output channels (the 256 x 128 tile) and no stride-2 data gradient
+    // rule 1: only where it measured faster in isolation (tools/pipe_check.py): >= 128 output channels
+    // (the 256 x 128 tile) and no stride-2 data gradient
     if (mode == 1 && (nout < 128 || os == 2)) return p;
+    // 3: the wider rule (A/B runs): every 1x1, and 3x3 with >= 128 output channels or (forward) >= 128
+    // input channels, at >= 256 tiles; never the stride-2 data gradient
+    if (mode == 3 && (os == 2 || (d->k == 3 && nout < 128 && (dgrad || kin < 128)))) return p;
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
     const int64_t M = int64_t(d->n) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
     p.cfg = nout >= 128 ? 0 : 1;
