@@ -36,7 +36,29 @@ struct WgArgs {
     int64_t units;                            // K units: 64-pixel stages (1x1), 8x8 tiles (3x3), 32-pixel steps
     int64_t chunk;                            // units per split
     int ci_tiles;                             // generic kernel: channel tiles per tap column
+    int co_t, ci_t, splits;                   // wgrad3 / wgrad1: tile grid (1-D launch, see wg_tile)
+    int xcd_map;                              // splits % 8 == 0: one split's tiles all on one XCD
 };
+
+// (co tile, ci tile, split) of this workgroup of a 1-D launch of co_t * ci_t * splits blocks.  With
+// xcd_map the blocks of one split — the (co, ci) tiles that read the SAME pixel range of dz and x —
+// are the consecutive blocks of one XCD (block b runs on XCD b % 8), so that range comes from HBM
+// once and from the XCD's L2 for the other tiles; in plain order the co tiles of one split landed on
+// 8 different XCDs and the weight gradients fetched 2.2x their algorithmic bytes (profiles/r02).
+__device__ __forceinline__ void wg_tile(const WgArgs& a, int& co, int& ci, int& split) {
+    const int b = blockIdx.x, nt = a.co_t * a.ci_t;
+    int t;
+    if (a.xcd_map) {
+        const int xcd = b & 7, q = b >> 3;
+        t = q % nt;
+        split = (q / nt) * 8 + xcd;
+    } else {
+        t = b % nt;
+        split = b / nt;
+    }
+    co = t % a.co_t;
+    ci = t / a.co_t;
+}
 
 // transposed 16x(32 k) fragment: two ds_read_b64_tr_b16, k rows {4g..4g+3} from p_lo and
 // {16+4g..} from p_hi (g = lane>>4); the same k permutation on both operands cancels
@@ -70,7 +92,9 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave / (NWV / 2), wc = wave % (NWV / 2);
-    const int co0 = blockIdx.x * TC, ci0 = blockIdx.y * TC;
+    int cot, cit, split;
+    wg_tile(a, cot, cit, split);
+    const int co0 = cot * TC, ci0 = cit * TC;
     const int sc = tid & 7, srow = tid >> 3;  // staging: chunk sc of rows srow + RPP*it
     const bool co_ok = co0 + sc * 8 < a.Cout, ci_ok = ci0 + sc * 8 < a.Cin;
     int x_hy[XI], x_hx[XI];
@@ -81,7 +105,7 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
         x_hx[it] = r - x_hy[it] * HD;
     }
     const int ntw = (a.OW + 7) >> 3, nth = (a.OH + 7) >> 3;
-    const int64_t t_begin = int64_t(blockIdx.z) * a.chunk;
+    const int64_t t_begin = int64_t(split) * a.chunk;
     const int64_t t_end = std::min<int64_t>(a.units, t_begin + a.chunk);
 
     // fragment-read geometry: lane's k rows (pixels of the 8x8 tile) for the two 32-pixel halves
@@ -178,7 +202,7 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
     }
 
     // partials: D[co][ci], lane holds co rows (lane>>4)*4 + r, ci column lane&15
-    float* base = a.part + int64_t(blockIdx.z) * a.Cout * 9 * a.Cin;
+    float* base = a.part + int64_t(split) * a.Cout * 9 * a.Cin;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -208,9 +232,11 @@ __global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
     __shared__ __attribute__((aligned(16))) char Bs[2][KP * RS];   // x rows x T ci (bf16)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave >> 1, wc = wave & 1;
-    const int co0 = blockIdx.x * T, ci0 = blockIdx.y * T;
+    int cot, cit, split;
+    wg_tile(a, cot, cit, split);
+    const int co0 = cot * T, ci0 = cit * T;
     const int sc = tid % CPR, srow = tid / CPR;
-    const int64_t p_begin = (int64_t(blockIdx.z) * a.chunk) * KP;
+    const int64_t p_begin = (int64_t(split) * a.chunk) * KP;
     const int64_t p_end = std::min<int64_t>(a.M, p_begin + a.chunk * KP);
     uint32_t dz_off[ITEMS], x_off[ITEMS];
 #pragma unroll
@@ -281,7 +307,7 @@ __global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
         __syncthreads();
         buf ^= 1;
     }
-    float* base = a.part + int64_t(blockIdx.z) * a.Cout * a.Cin;
+    float* base = a.part + int64_t(split) * a.Cout * a.Cin;
 #pragma unroll
     for (int i = 0; i < TS; ++i)
 #pragma unroll
@@ -475,6 +501,7 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     }();
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(target / cols, p.units / min_units));
     splits = std::min<int64_t>(splits, p.kind == 0 ? 65535 : 256);
+    if (p.kind != 0 && splits >= 8) splits &= ~int64_t(7);      // whole XCD groups (wg_tile)
     p.chunk = (p.units + splits - 1) / splits;
     p.splits = std::max<int64_t>(1, (p.units + p.chunk - 1) / p.chunk);
     return p;
@@ -517,6 +544,8 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
     a.M = M; a.units = p.units; a.chunk = p.chunk;
     int64_t splits = p.splits;
+    a.co_t = p.co_t; a.ci_t = p.ci_t; a.splits = int(splits);
+    a.xcd_map = splits % 8 == 0;
     if (M == 0) {
         // no pixels: the gradient is zero
         splits = 0;
@@ -526,7 +555,7 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
             const char* e = getenv("YM_WGRAD_WAVES");
             return e && atoi(e) == 4;
         }();
-        const dim3 grid(p.co_t, p.ci_t, unsigned(splits));
+        const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         if (d->stride == 1) {
             if (w4) hipLaunchKernelGGL((wgrad3_kernel<1, 4>), grid, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((wgrad3_kernel<1, 8>), grid, dim3(512), 0, st, a);
@@ -535,10 +564,11 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
             else hipLaunchKernelGGL((wgrad3_kernel<2, 8>), grid, dim3(512), 0, st, a);
         }
     } else if (p.kind == 1) {
+        const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         if (p.T == 128)
-            hipLaunchKernelGGL(wgrad1_kernel<128>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(wgrad1_kernel<128>, grid, dim3(256), 0, st, a);
         else
-            hipLaunchKernelGGL(wgrad1_kernel<64>, dim3(p.co_t, p.ci_t, unsigned(splits)), dim3(256), 0, st, a);
+            hipLaunchKernelGGL(wgrad1_kernel<64>, grid, dim3(256), 0, st, a);
     } else {
         if (hipMemsetAsync(workspace, 0, size_t(E) * sizeof(float), st) != hipSuccess) {
             set_error("ym_conv_wgrad: memset failed");
