@@ -82,7 +82,7 @@ struct TaskPix {
 // one per tap); the 1x1 forms also load the NEXT task's fragments before this task's MFMAs.
 template <int NT, int KC, int KS, int S, int MODE, int TP, int PY, int PX>
 __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][4], float (&ssq)[NT][4], int64_t first,
-                                            int64_t step) {
+                                            int64_t step, int64_t ntask) {
     using F = frag_t<MODE>;
     constexpr int TAPS = KS * KS;
     constexpr bool CLS = S == 2 && MODE == 1;
@@ -135,7 +135,6 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
             }
         }
     };
-    const int64_t ntask = a.tpc;
     TaskPix<TP, CS> P;
     F b[TAPS][TP][KC];
     int64_t task = first;
@@ -230,16 +229,21 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) ssum[nt][r] = ssq[nt][r] = 0.f;
-    const int64_t first = int64_t(blockIdx.x) * 4 + wave, step = int64_t(gridDim.x) * 4;
+    // XCD-contiguous task ranges (gridDim.x is a multiple of 8; block b runs on XCD b % 8): the 3x3
+    // neighbour rows of a task, and for a stride-2 data gradient the other three parity classes of
+    // the same pixels, are read by the same XCD at about the same time — from its L2, not from HBM
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
+    const int64_t lo = a.tpc * xcd / 8, hi = a.tpc * (xcd + 1) / 8;
+    const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
     if constexpr (S == 2 && MODE == 1) {
         switch (blockIdx.y) {
-            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step); break;
-            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step); break;
-            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step); break;
-            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step); break;
+            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi); break;
+            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step, hi); break;
+            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step, hi); break;
+            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step, hi); break;
         }
     } else {
-        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step);
+        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi);
     }
     if constexpr (MODE == 0) {
         if (!a.st_sum) return;
@@ -329,7 +333,7 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
         const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
         const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
         p.classes = os * os;
-        p.grid = int(std::max<int64_t>(1, std::min<int64_t>(1024 / p.classes, (tpc + 3) / 4)));
+        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(1024 / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
         return p;
     }
     return p;
