@@ -28,3 +28,15 @@ def test_python_signatures_cover_header():
     import yolomi._lib as yl
     assert set(declared()) == set(yl.SIGNATURES), set(declared()) ^ set(yl.SIGNATURES)
     assert yl.lib().ym_version() >= 1
+
+
+def test_integration_table_matches_header():
+    """INTEGRATION.md's entry-point table names every declared entry point and nothing else."""
+    doc = (ROOT / "INTEGRATION.md").read_text()
+    table = doc[doc.index("| entry point(s) | reference call site |"):]
+    table = table[:table.index("\n\n")]
+    listed = set()
+    for row in table.splitlines()[2:]:
+        listed.update(re.findall(r"`(ym_\w+)`", row.split("|")[1]))
+    names = set(declared())
+    assert listed == names, {"undeclared": sorted(listed - names), "unlisted": sorted(names - listed)}
