@@ -70,23 +70,25 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
 }
 
 // ------------------------------------------------------------------ 3x3
-// NWV = 4: waves own (co half, ci half), all 9 taps (144 accumulators, one wave per SIMD);
-// NWV = 8: waves own (co half, ci quarter), all 9 taps (72 accumulators, two waves per SIMD
-// sharing the same staged dz / halo)
-template <int S, int NWV>
+// TCO x TCI (64 or 32) channel tiles.  NWV = 4: waves own (co half, ci half), all 9 taps;
+// NWV = 8: waves own (co half, ci quarter) of a 64-ci tile, two waves per SIMD sharing the same
+// staged dz / halo.  32-channel tiles serve the 32-channel layers of the stem stage, which a 64x64
+// tile ran three-quarters empty (zero-filled channels through every MFMA).
+template <int S, int NWV, int TCO, int TCI>
 __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
     constexpr int NT = NWV * 64;
-    constexpr int TI = 2;                     // 16-co subtiles per wave
-    constexpr int TJ = NWV == 8 ? 1 : 2;      // 16-ci subtiles per wave
-    constexpr int WCI = TJ * 16;              // ci per wave
-    constexpr int RPP = NT / 8;               // staged rows per pass
-    constexpr int DI = 64 / RPP;              // dz chunks per thread
-    constexpr int TC = 64;                    // co and ci tile
-    constexpr int RSD = TC * 2 + 32;          // dz rows: consecutive-row tr reads conflict free
-    constexpr int RSX = S == 1 ? 160 : 144;   // halo rows: reads step S rows (S=2 needs 36-dword rows)
+    constexpr int TI = TCO / 32;              // 16-co subtiles per wave (waves split co in halves)
+    constexpr int WCI = TCI / (NWV / 2);      // ci per wave
+    constexpr int TJ = WCI / 16;              // 16-ci subtiles per wave
+    static_assert(TI >= 1 && TJ >= 1, "wgrad3 tile geometry");
+    constexpr int CPD = TCO / 8, CPX = TCI / 8;       // 16-B chunks per dz / halo row
+    constexpr int RPD = NT / CPD, RPX = NT / CPX;     // rows staged per pass
+    constexpr int DI = (64 + RPD - 1) / RPD;  // dz chunks per thread (threads past row 63 idle)
+    constexpr int RSD = TCO * 2 + 32;         // dz rows: consecutive-row tr reads conflict free
+    constexpr int RSX = TCI * 2 + (S == 1 ? 32 : 16);   // halo rows: reads step S rows
     constexpr int HD = 7 * S + 3;             // halo side
     constexpr int HR = HD * HD;
-    constexpr int XI = (HR * 8 + NT - 1) / NT;  // 16-B halo chunks per thread
+    constexpr int XI = (HR + RPX - 1) / RPX;  // 16-B halo chunks per thread
     __shared__ __attribute__((aligned(16))) char Dz[64 * RSD];
     __shared__ __attribute__((aligned(16))) char Xh[HR * RSX];
 
@@ -94,13 +96,14 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
     const int wr = wave / (NWV / 2), wc = wave % (NWV / 2);
     int cot, cit, split;
     wg_tile(a, cot, cit, split);
-    const int co0 = cot * TC, ci0 = cit * TC;
-    const int sc = tid & 7, srow = tid >> 3;  // staging: chunk sc of rows srow + RPP*it
-    const bool co_ok = co0 + sc * 8 < a.Cout, ci_ok = ci0 + sc * 8 < a.Cin;
+    const int co0 = cot * TCO, ci0 = cit * TCI;
+    const int dsc = tid % CPD, dsrow = tid / CPD;     // staging: chunk of rows row + RP*it
+    const int xsc = tid % CPX, xsrow = tid / CPX;
+    const bool co_ok = co0 + dsc * 8 < a.Cout, ci_ok = ci0 + xsc * 8 < a.Cin;
     int x_hy[XI], x_hx[XI];
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
-        const int r = srow + RPP * it;
+        const int r = xsrow + RPX * it;
         x_hy[it] = r / HD;
         x_hx[it] = r - x_hy[it] * HD;
     }
@@ -136,27 +139,27 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
         const __amdgpu_buffer_rsrc_t rxs = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
 #pragma unroll
         for (int it = 0; it < DI; ++it) {
-            const int p = srow + RPP * it;
+            const int p = dsrow + RPD * it;
             const int oh = oh0 + (p >> 3), ow = ow0 + (p & 7);
-            const bool ok = co_ok && oh < a.OH && ow < a.OW;
-            rdz[it] = buf_load16(rd, ok ? uint32_t(((oh * a.OW + ow) * int(a.dz_ld) + co0 + sc * 8) * 2) : OOB);
+            const bool ok = co_ok && p < 64 && oh < a.OH && ow < a.OW;
+            rdz[it] = buf_load16(rd, ok ? uint32_t(((oh * a.OW + ow) * int(a.dz_ld) + co0 + dsc * 8) * 2) : OOB);
         }
         const int ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
 #pragma unroll
         for (int it = 0; it < XI; ++it) {
             const int ih = ih0 + x_hy[it], iw = iw0 + x_hx[it];
-            const bool ok = ci_ok && srow + RPP * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
-            rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + sc * 8) * 2) : OOB);
+            const bool ok = ci_ok && xsrow + RPX * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
+            rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + xsc * 8) * 2) : OOB);
         }
     };
     auto store = [&]() {
 #pragma unroll
         for (int it = 0; it < DI; ++it)
-            *reinterpret_cast<uint4*>(Dz + (srow + RPP * it) * RSD + sc * 16) = rdz[it];
+            if (dsrow + RPD * it < 64) *reinterpret_cast<uint4*>(Dz + (dsrow + RPD * it) * RSD + dsc * 16) = rdz[it];
 #pragma unroll
         for (int it = 0; it < XI; ++it)
-            if (srow + RPP * it < HR)
-                *reinterpret_cast<uint4*>(Xh + (srow + RPP * it) * RSX + sc * 16) = h8_to_bf8(rx[it]);
+            if (xsrow + RPX * it < HR)
+                *reinterpret_cast<uint4*>(Xh + (xsrow + RPX * it) * RSX + xsc * 16) = h8_to_bf8(rx[it]);
     };
 
     if (t_begin < t_end) {
@@ -172,7 +175,7 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
             bf16x8 af[TI];
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
-                const int col = (wr * 32 + i * 16 + 4 * pp) * 2;
+                const int col = (wr * (TCO / 2) + i * 16 + 4 * pp) * 2;
                 af[i] = tr_frag(Dz + (kk * 32 + 4 * g + q) * RSD + col, Dz + (kk * 32 + 16 + 4 * g + q) * RSD + col);
             }
 #pragma unroll
@@ -213,7 +216,7 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
                 if (ci >= a.Cin) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int co = co0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+                    const int co = co0 + wr * (TCO / 2) + i * 16 + (lane >> 4) * 4 + r;
                     if (co < a.Cout) base[(int64_t(co) * 9 + t) * a.Cin + ci] = acc[t][i][j][r];
                 }
             }
@@ -458,7 +461,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 // ------------------------------------------------------------------ launch plan
 struct WgPlan {
     int kind;          // 3: wgrad3, 1: wgrad1, 0: generic
-    int T;
+    int T;             // wgrad1 / generic tile; wgrad3: co tile (ci tile in T2)
+    int T2;
     int co_t, ci_t;
     int64_t units, chunk, splits;
 };
@@ -469,15 +473,18 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     const bool whole = d->x_bs == int64_t(d->h) * d->w * d->x_ld && d->y_bs == int64_t(d->oh) * d->ow * d->y_ld;
     if (d->k == 3 && d->pad == 1 && (d->stride == 1 || d->stride == 2)) {
         p.kind = 3;
-        p.T = 64;
+        p.T = d->cout <= 32 ? 32 : 64;
+        p.T2 = d->cin <= 32 ? 32 : 64;
         p.units = int64_t(d->n) * ((d->oh + 7) / 8) * ((d->ow + 7) / 8);
     } else if (d->k == 1 && d->stride == 1 && d->pad == 0 && whole) {
         p.kind = 1;
-        // 128-wide tiles once both channel counts reach t128 (YM_WGRAD1_T128, default 128): fewer
-        // tiles re-read dz and x fewer times, at the cost of padding a channel count below 128
+        // 128-wide tiles once both channel counts reach t128 (YM_WGRAD1_T128, default 96): fewer
+        // tiles re-read dz and x fewer times, at the cost of padding a channel count below 128 —
+        // the 96 -> 128 1x1 at 160x160 measured 0.357 ms on 64-wide tiles (x and dz read twice
+        // each from HBM), 0.142 ms on one padded 128-wide tile
         static const int t128 = [] {
             const char* e = getenv("YM_WGRAD1_T128");
-            return e ? atoi(e) : 128;
+            return e ? atoi(e) : 96;
         }();
         p.T = (d->cout >= t128 && d->cin >= t128) ? 128 : 64;
         p.units = (M + 63) / 64;
@@ -487,7 +494,7 @@ WgPlan wg_plan(const ym_conv_desc* d) {
         p.units = (M + 31) / 32;
     }
     p.co_t = (d->cout + p.T - 1) / p.T;
-    p.ci_t = (d->cin + p.T - 1) / p.T;
+    p.ci_t = (d->cin + (p.kind == 3 ? p.T2 : p.T) - 1) / (p.kind == 3 ? p.T2 : p.T);
     const int64_t cols = int64_t(p.co_t) * p.ci_t * (p.kind == 0 ? d->k * d->k : 1);
     // enough K units per workgroup to amortise writing its fp32 partial tile (64x64x9 floats for
     // 3x3: 147 KB, about the input an 8x8-pixel unit moves 12 times)
@@ -556,13 +563,23 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
             return e && atoi(e) == 4;
         }();
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
-        if (d->stride == 1) {
-            if (w4) hipLaunchKernelGGL((wgrad3_kernel<1, 4>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((wgrad3_kernel<1, 8>), grid, dim3(512), 0, st, a);
-        } else {
-            if (w4) hipLaunchKernelGGL((wgrad3_kernel<2, 4>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((wgrad3_kernel<2, 8>), grid, dim3(512), 0, st, a);
+        const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
+#define YM_WG3(S_)                                                                                        \
+        switch (tc) {                                                                                     \
+            case 0:                                                                                       \
+                if (w4) hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 64, 64>), grid, dim3(256), 0, st, a);     \
+                else hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 64, 64>), grid, dim3(512), 0, st, a);        \
+                break;                                                                                    \
+            case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 32, 64>), grid, dim3(512), 0, st, a); break;  \
+            case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 64, 32>), grid, dim3(256), 0, st, a); break;  \
+            default: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 32, 32>), grid, dim3(256), 0, st, a); break; \
         }
+        if (d->stride == 1) {
+            YM_WG3(1)
+        } else {
+            YM_WG3(2)
+        }
+#undef YM_WG3
     } else if (p.kind == 1) {
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         if (p.T == 128)
