@@ -154,9 +154,10 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ p2, int R, int
 // level-1 block publishes its fp64 row, takes a ticket on its channel group's counter, and the
 // block drawing the last ticket folds the R rows and runs the finalize (forward: scale / shift /
 // mean / rstd / running stats; backward: dgamma / dbeta / apply coefficients) and re-arms the
-// counter.  Hand-off per MI355X_MICROARCH.md (workgroup dispatch & inter-workgroup visibility):
-// stores -> every wave vmcnt(0) -> barrier -> lane 0 agent release fence -> vmcnt(0) -> relaxed
-// agent fetch_add; the last arriver: agent acquire fence -> vmcnt(0) -> barrier -> plain loads.
+// counter.  Hand-off per MI355X_MICROARCH.md (inter-workgroup visibility, "valid forms"): the fp64
+// rows stored write-through (sc1) -> every wave vmcnt(0) -> barrier -> lane 0 relaxed agent
+// fetch_add; the last arriver: barrier -> sc1 loads.  (The earlier agent release + acquire fences
+// cost ≈1.7 us each on this launch-latency-bound kernel, 154 launches per step.)
 // Deterministic: the fold reads the rows in a fixed order whatever order the blocks finished in.
 template <bool BWD>
 __global__ void __launch_bounds__(256) bn_finalize_fused_kernel(
@@ -182,20 +183,14 @@ __global__ void __launch_bounds__(256) bn_finalize_fused_kernel(
     sh[1][rg][cl] = q;
     __syncthreads();
     if (rg == 0 && c < C) {
-        p2[(int64_t(blockIdx.y) * 2 + 0) * C + c] = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-        p2[(int64_t(blockIdx.y) * 2 + 1) * C + c] = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+        st_wt(&p2[(int64_t(blockIdx.y) * 2 + 0) * C + c], sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl]);
+        st_wt(&p2[(int64_t(blockIdx.y) * 2 + 1) * C + c], sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl]);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned t = __hip_atomic_fetch_add(&counters[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         last_sh = t == unsigned(R - 1);
-        if (last_sh) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
     }
     __syncthreads();
     if (!last_sh) return;
@@ -204,8 +199,8 @@ __global__ void __launch_bounds__(256) bn_finalize_fused_kernel(
     q = 0.0;
     if (c < C)
         for (int r = rg; r < R; r += 4) {
-            s += p2[(int64_t(r) * 2 + 0) * C + c];
-            q += p2[(int64_t(r) * 2 + 1) * C + c];
+            s += ld_wt(&p2[(int64_t(r) * 2 + 0) * C + c]);
+            q += ld_wt(&p2[(int64_t(r) * 2 + 1) * C + c]);
         }
     sh[0][rg][cl] = s;
     sh[1][rg][cl] = q;
