@@ -10,8 +10,8 @@
 // which workgroups finish first: bit-reproducible.  Visibility hand-off per MI355X_MICROARCH.md
 // (inter-workgroup visibility, "valid forms"): the partial rows are stored write-through (relaxed
 // agent-scope atomic stores = `sc1` vector stores) -> every wave vmcnt(0) -> barrier -> one lane's
-// relaxed agent fetch_add; the last arriver: agent acquire -> barrier -> `sc1` loads (relaxed agent
-// atomic loads).  No release fence: an agent release writes back the XCD's whole dirty L2 (the
+// relaxed agent fetch_add; the last arriver: barrier -> `sc1` loads (relaxed agent atomic loads),
+// no fence on either side.  No release fence: an agent release writes back the XCD's whole dirty L2 (the
 // conv's freshly written z), which measured +35 us per conv launch when every workgroup paid it.
 // Vector memory operations only; nothing spins.
 #pragma once
@@ -109,9 +109,7 @@ __device__ __forceinline__ bool bn_ticket(unsigned* counter, unsigned expected, 
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t + 1 == expected;
-        if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        *flag = last;
+        *flag = t + 1 == expected;
     }
     __syncthreads();
     const bool r = *flag != 0;

@@ -172,6 +172,12 @@ def bn_fold_on():
     return os.environ.get("YM_BN_FOLD", "0") == "1"
 
 
+def bn_bwd_fold_on():
+    """YM_BN_BWD_FOLD=1: the backward statistics pass finalizes dgamma / dbeta / the apply coefficients
+    itself (ym_bn_bwd_reduce_finalize) instead of a separate ym_bn_bwd_finalize launch."""
+    return os.environ.get("YM_BN_BWD_FOLD", "0") == "1"
+
+
 # buffer-range keys for the stream scheduler: ('a' activation | 'g' gradient, Act id, c0, c1)
 def _ka(v):
     return ("a", id(v.act), v.c0, v.c0 + v.c)
@@ -305,7 +311,7 @@ class ConvBN:
         r = self.res
         racc = r.grad_for_write(st) if r is not None else 0
         e = self.M * self.co * 2
-        fold = bn_fold_on()
+        fold = bn_bwd_fold_on()
         work = 5 * e + 16 * Gb * self.co + ((2 + racc) * e if r is not None else 0)
 
         def run():
