@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "conv_direct.h"
+#include "conv_epi.h"
 #include "tile.h"
 
 namespace ym {
@@ -82,7 +83,7 @@ struct TaskPix {
 // one per tap); the 1x1 forms also load the NEXT task's fragments before this task's MFMAs.
 template <int NT, int KC, int KS, int S, int MODE, int TP, int PY, int PX>
 __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][4], float (&ssq)[NT][4], int64_t first,
-                                            int64_t step, int64_t ntask) {
+                                            int64_t step, int64_t ntask, char* ep) {
     using F = frag_t<MODE>;
     constexpr int TAPS = KS * KS;
     constexpr bool CLS = S == 2 && MODE == 1;
@@ -111,6 +112,7 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
         }
     }
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
+    const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
     auto load = [&](const TaskPix<TP, CS>& P, F (&b)[TAPS][TP][KC]) {
 #pragma unroll
         for (int t = 0; t < TAPS; ++t) {
@@ -183,6 +185,30 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
                 load(P, b);
             }
         }
+        if constexpr (MODE == 1 && (NT == 2 || NT == 4)) {
+            // data gradients (forward measured slower this way: its statistics need every pixel's
+            // decode again): transposed through this wave's LDS area and stored as 16-B pieces of each pixel's
+            // channel run (conv_epi.h): 8-B fragment stores strided by the pixel pitch were the
+            // epilogue's cost (the stores of a 16-pixel group cover 16 partial lines each)
+            f32x4 accT[NT][TP];
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+                for (int g = 0; g < TP; ++g) accT[nt][g] = acc[g][nt];
+            const int64_t tq = task;
+            auto pix_off = [&](int q) -> uint32_t {
+                const uint32_t chw = uint32_t(a.OHc) * uint32_t(a.OWc);
+                const int64_t m = tq * (16 * TP) + q;
+                const uint32_t nn = uint32_t(m / chw), r = uint32_t(m - int64_t(nn) * chw);
+                const uint32_t i = r / uint32_t(a.OWc), j = r - i * uint32_t(a.OWc);
+                const int oh = int(i) * CS + PY, ow = int(j) * CS + PX;
+                if (int(nn) >= a.N || oh >= a.OH || ow >= a.OW) return OOB;
+                return uint32_t((int64_t(nn) * a.y_bs + (int64_t(oh) * a.OW + ow) * a.y_ld) * 2);
+            };
+            epilogue_store<NT, TP>(accT, ssum, ssq, MODE == 0, ep, lane, 0, a.Nout, yres, MODE == 0,
+                                   MODE == 1 && a.accumulate, pix_off);
+            continue;
+        }
         // epilogue: lane holds channels nt*16 + fc*4 + r of pixel fr of group g
 #pragma unroll
         for (int g = 0; g < TP; ++g) {
@@ -222,6 +248,7 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
 template <int NT, int KC, int KS, int S, int MODE, int TP>
 __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     __shared__ float red[2][4][16 * NT];
+    __shared__ __attribute__((aligned(16))) char epl[4][16 * 16 * NT * 2];   // per-wave epilogue transpose
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int fr = lane & 15, fc = lane >> 4;
     float ssum[NT][4], ssq[NT][4];
@@ -237,13 +264,13 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
     if constexpr (S == 2 && MODE == 1) {
         switch (blockIdx.y) {
-            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi); break;
-            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step, hi); break;
-            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step, hi); break;
-            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step, hi); break;
+            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]); break;
+            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step, hi, epl[wave]); break;
+            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step, hi, epl[wave]); break;
+            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step, hi, epl[wave]); break;
         }
     } else {
-        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi);
+        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]);
     }
     if constexpr (MODE == 0) {
         if (!a.st_sum) return;
@@ -318,7 +345,7 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
     const int64_t in_ld = dgrad ? d->y_ld : d->x_ld, in_bs = dgrad ? d->y_bs : d->x_bs;
     const int64_t out_ld = dgrad ? d->x_ld : d->y_ld, out_bs = dgrad ? d->x_bs : d->y_bs;
     if (in_ld % 8 || in_bs % 8 || out_ld % 4 || out_bs % 4) return p;
-    if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31)) return p;
+    if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31) || int64_t(d->n) * out_bs * 2 >= (int64_t(1) << 31)) return p;
     // high-resolution maps only (where the implicit GEMMs are latency-bound): >= 1 M output pixels
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
     const int64_t M = int64_t(d->n) * OH * OW;
