@@ -29,6 +29,7 @@
 
 #include "common.h"
 #include "conv_direct.h"
+#include "conv_epi.h"
 #include "conv_halo.h"
 #include "bnfold.h"
 #include "conv_pipe.h"
@@ -56,6 +57,7 @@ struct GemmArgs {
     int N;                                   // images
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
     int ntl;                                 // channel tiles interleaved into grid x (0: they are grid y)
+    int ep_lds;                              // data gradient: LDS-transposed 16-B epilogue (conv_epi.h)
     BnFold fold;                             // fused BN finalize (fold.cnt null: none)
 };
 
@@ -288,6 +290,27 @@ conv_gemm_kernel(GemmArgs a) {
             for (int kk = 0; kk < KS; ++kk) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
         }
 
+        if constexpr (MODE == MODE_DGRAD && BN / WM >= 32) {
+            if (a.ep_lds) {
+                // bf16 data gradient (+ fan-in accumulate): transposed through LDS and stored as
+                // 16-B pieces of each pixel's channel run; the staging ring is free once every wave
+                // has read the last stage (the next tile's prologue waits at its own barrier)
+                raw_barrier();
+                const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
+                const int wch0 = n0 + wr * (BN / WM);
+                auto pix_off = [&](int q) -> uint32_t {
+                    const int64_t m = m0 + wc * (BM / WN) + q;
+                    if (m >= Mc) return OOB;
+                    const uint32_t n = uint32_t(m) / OHW, pix = uint32_t(m) - n * OHW;
+                    const uint32_t ci_ = pix / uint32_t(OWc);
+                    const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(pix - ci_ * uint32_t(OWc)) * os + px;
+                    return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
+                };
+                epilogue_store<TM, TN>(acc, ssum, ssq, false, smem + wave * (16 * (BN / WM) * 2), lane, wch0, a.Nout,
+                                       yres, false, a.accumulate != 0, pix_off);
+                continue;
+            }
+        }
         // epilogue: D[channel][pixel]; lane holds 4 consecutive channels of one pixel
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -916,6 +939,12 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_dgrad: kernel size %d unsupported (1..3)", d->k);
     YM_CHECK_ARG(d->stride == 1 || d->stride == 2, "ym_conv_dgrad: stride %d unsupported (1, 2)", d->stride);
     a.ostep = d->stride;
+    static const int ep_env = [] {                 // YM_CONV_EPI=0: fragment stores (A/B runs)
+        const char* e = getenv("YM_CONV_EPI");
+        return e ? atoi(e) : 1;
+    }();
+    a.ep_lds = ep_env && int64_t(d->n) * d->x_bs * 2 < (int64_t(1) << 31) && d->x_ld % 8 == 0 && d->x_bs % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(dx) % 16 == 0;     // 16-B stores of whole 8-channel runs
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
     YM_CHECK_ARG(offsets_fit(d->y_bs, int64_t(d->h / d->stride) * (d->w / d->stride)),
