@@ -290,7 +290,7 @@ conv_gemm_kernel(GemmArgs a) {
             for (int kk = 0; kk < KS; ++kk) __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
         }
 
-        if constexpr (MODE == MODE_DGRAD && BN / WM >= 32) {
+        if constexpr (BN / WM >= 32) {
             if (a.ep_lds) {
                 // bf16 data gradient (+ fan-in accumulate): transposed through LDS and stored as
                 // 16-B pieces of each pixel's channel run; the staging ring is free once every wave
@@ -306,8 +306,9 @@ conv_gemm_kernel(GemmArgs a) {
                     const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(pix - ci_ * uint32_t(OWc)) * os + px;
                     return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
                 };
-                epilogue_store<TM, TN>(acc, ssum, ssq, false, smem + wave * (16 * (BN / WM) * 2), lane, wch0, a.Nout,
-                                       yres, false, a.accumulate != 0, pix_off);
+                epilogue_store<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr,
+                                       smem + wave * (16 * (BN / WM) * 2), lane, wch0, a.Nout, yres, MODE == MODE_FWD,
+                                       MODE == MODE_DGRAD && a.accumulate != 0, pix_off);
                 continue;
             }
         }
@@ -876,6 +877,14 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     a.N = d->n;
     a.ostep = 1;
     if (fold) a.fold = *fold;
+    {
+        static const int ep_env = [] {             // YM_CONV_EPI: 0 fragment stores, 1 data gradient, 2 also forward
+            const char* e = getenv("YM_CONV_EPI");
+            return e ? atoi(e) : 1;
+        }();
+        a.ep_lds = ep_env >= 2 && d->out_f32 == 2 && !bias && !fold && d->y_ld % 8 == 0 && d->y_bs % 8 == 0 &&
+                   int64_t(d->n) * d->y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
+    }
     if (a.M == 0) return YM_OK;
     const DirectPlan dp = fold ? DirectPlan{} : direct_plan(d, 0);
     if (dp.ok) {

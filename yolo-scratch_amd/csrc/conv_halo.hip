@@ -23,6 +23,7 @@
 
 #include "bnfold.h"
 #include "common.h"
+#include "conv_epi.h"
 #include "conv_halo.h"
 #include "tile.h"
 
@@ -44,6 +45,7 @@ struct HaloArgs {
     int RT, CT;                               // tiles per image: rows, cols
     int ntiles;
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
+    int ep_lds;                               // 16-bit output via the LDS-transposed epilogue (conv_epi.h)
     BnFold fold;                              // fused BN finalize (fold.cnt null: none)
 };
 
@@ -254,6 +256,24 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
             if (++kh == 3) { kh = 0; ++cc; }
         }
 
+        if (a.ep_lds) {
+            // transposed through LDS (the halo buffers are free once every wave has read the last
+            // step: barrier; the next tile's prologue waits at its own barrier) and stored as 16-B
+            // pieces of each pixel's channel run
+            raw_barrier();
+            const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
+            const int wch0 = n0 + wc * (TCW * 16);
+            auto pix_off = [&](int q) -> uint32_t {
+                const int p = wp * TPW * 16 + q;
+                const int ph = p / a.TW, pw = p - ph * a.TW;
+                const int oh = oh0 + ph, ow = ow0 + pw;
+                if (p >= ntp || oh >= a.OH || ow >= a.OW) return OOB;
+                return uint32_t((int64_t(n) * a.y_bs + int64_t(oh * a.OW + ow) * a.y_ld + wch0) * 2);
+            };
+            epilogue_store<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, smem + wave * (16 * TCW * 16 * 2), lane, wch0,
+                                     a.Nout, yres, a.out_mode == 2, a.accumulate != 0 && a.out_mode == 0, pix_off);
+            continue;
+        }
         // epilogue: lane holds channels cb..cb+3 of pixel p
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
@@ -440,6 +460,12 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     }
     a.accumulate = d->accumulate;
     a.TH = p.TH; a.TW = p.TW; a.HWd = p.TW + 2; a.HP = (p.TH + 2) * (p.TW + 2);
+    static const int ep_env = [] {   // YM_HALO_EPI: 0 fragment stores, 1 data gradient only, 2 both (default:
+        const char* e = getenv("YM_HALO_EPI");   // 64-ch 80x80 fwd 0.076 -> 0.070 ms, dgrad 0.066 -> 0.058)
+        return e ? atoi(e) : 2;
+    }();
+    a.ep_lds = (dgrad ? ep_env >= 1 : ep_env >= 2) && !bias && a.out_mode != 1 && a.y_ld % 8 == 0 && a.y_bs % 8 == 0 &&
+               int64_t(d->n) * a.y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
     if (fold && st_sum) {
         a.fold = *fold;
