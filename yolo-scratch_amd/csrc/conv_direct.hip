@@ -185,25 +185,26 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
                 load(P, b);
             }
         }
-        if constexpr (MODE == 1 && (NT == 2 || NT == 4)) {
-            // data gradients (forward measured slower this way: its statistics need every pixel's
-            // decode again): transposed through this wave's LDS area and stored as 16-B pieces of each pixel's
-            // channel run (conv_epi.h): 8-B fragment stores strided by the pixel pitch were the
-            // epilogue's cost (the stores of a 16-pixel group cover 16 partial lines each)
+        if constexpr (NT == 2 || NT == 4) {
+            // transposed through this wave's LDS area and stored as 16-B pieces of each pixel's channel
+            // run (conv_epi.h): 8-B fragment stores strided by the pixel pitch were the epilogue's cost.
+            // Pixel q's output offset comes from the lane that owns it (lane q % 16 decoded pixel q of
+            // its group for the loads) by a lane shuffle, not by decoding q again.
             f32x4 accT[NT][TP];
+            uint32_t own[TP];
 #pragma unroll
-            for (int nt = 0; nt < NT; ++nt)
+            for (int g = 0; g < TP; ++g) {
 #pragma unroll
-                for (int g = 0; g < TP; ++g) accT[nt][g] = acc[g][nt];
-            const int64_t tq = task;
+                for (int nt = 0; nt < NT; ++nt) accT[nt][g] = acc[g][nt];
+                own[g] = Q.ok[g] ? uint32_t((int64_t(Q.n[g]) * a.y_bs + (int64_t(Q.oh[g]) * a.OW + Q.ow[g]) * a.y_ld) * 2)
+                                 : OOB;
+            }
             auto pix_off = [&](int q) -> uint32_t {
-                const uint32_t chw = uint32_t(a.OHc) * uint32_t(a.OWc);
-                const int64_t m = tq * (16 * TP) + q;
-                const uint32_t nn = uint32_t(m / chw), r = uint32_t(m - int64_t(nn) * chw);
-                const uint32_t i = r / uint32_t(a.OWc), j = r - i * uint32_t(a.OWc);
-                const int oh = int(i) * CS + PY, ow = int(j) * CS + PX;
-                if (int(nn) >= a.N || oh >= a.OH || ow >= a.OW) return OOB;
-                return uint32_t((int64_t(nn) * a.y_bs + (int64_t(oh) * a.OW + ow) * a.y_ld) * 2);
+                uint32_t v = 0;
+#pragma unroll
+                for (int g = 0; g < TP; ++g)
+                    if ((q >> 4) == g) v = own[g];
+                return uint32_t(__shfl(int(v), q & 15, 64));
             };
             epilogue_store<NT, TP>(accT, ssum, ssq, MODE == 0, ep, lane, 0, a.Nout, yres, MODE == 0,
                                    MODE == 1 && a.accumulate, pix_off);
