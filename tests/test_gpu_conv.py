@@ -196,6 +196,38 @@ PIPE = [
 @pytest.mark.parametrize("shape", PIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in PIPE])
 def test_pipe_kernel_vs_torch(shape):
     """fp16 forward (+ BN statistic partials), bf16 data gradient (overwrite, then accumulate)."""
+    from yolomi._lib import lib
+    _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
+
+
+# halo-staged 3x3 kernel forced on (ym_conv_set_halo(1)) through the same training-path outputs the
+# network uses: fp16 z + BN statistics, bf16 data gradient overwrite and accumulate (concat fan-in),
+# channel-slice views, 16-wide and whole-row tiles, single-tile images (bs1 16x16: the s@128 network)
+HALO_VIEWS = [
+    (1, 16, 16, 64, 64, 3, 1, 1, 0, 0),
+    (1, 32, 32, 128, 128, 3, 1, 1, 64, 0),
+    (2, 20, 20, 128, 128, 3, 1, 1, 0, 128),
+    (3, 40, 40, 64, 64, 3, 1, 1, 32, 32),
+    (2, 16, 16, 256, 128, 3, 1, 1, 0, 0),
+    (4, 80, 80, 64, 64, 3, 1, 1, 0, 0),
+]
+
+
+@pytest.mark.parametrize("shape", HALO_VIEWS,
+                         ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}x{s[8]}y{s[9]}" for s in HALO_VIEWS])
+def test_halo_kernel_views_vs_torch(shape):
+    from yolomi._lib import lib
+    pp, pd = lib().ym_conv_set_pipe(0), lib().ym_conv_set_direct(0)
+    try:
+        _views_fwd_dgrad_check(shape, lib().ym_conv_set_halo, 1, 1)
+    finally:
+        lib().ym_conv_set_pipe(pp)
+        lib().ym_conv_set_direct(pd)
+
+
+def _views_fwd_dgrad_check(shape, setter, mode, algo):
+    """Forward (fp16 z + BN statistic partials) and data gradient (bf16, overwrite then accumulate)
+    of one conv through channel-slice views, with kernel `algo` forced on by setter(mode)."""
     from yolomi._lib import call, lib, ConvDesc
     n, h, w, cin, cout, k, s, p, xe, ye = shape
     oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
@@ -209,10 +241,10 @@ def test_pipe_kernel_vs_torch(shape):
     wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
     dz = torch.randn(n, oh, ow, cout, generator=g).bfloat16()
     w16, wbf = wt.half(), wt.bfloat16()
-    prev = lib().ym_conv_set_pipe(2)
+    prev = setter(mode)
     try:
-        assert lib().ym_conv_algo(ctypes.byref(d), 0) == 2
-        assert lib().ym_conv_algo(ctypes.byref(d), 1) == 2
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) == algo
+        assert lib().ym_conv_algo(ctypes.byref(d), 1) == algo
         xbuf = torch.zeros(n, h, w, cin + xe, dtype=torch.float16, device=dev)
         xbuf[..., :cin] = x.to(dev)
         ybuf = torch.full((n, oh, ow, cout + ye), 7.0, dtype=torch.float16, device=dev)
@@ -236,7 +268,7 @@ def test_pipe_kernel_vs_torch(shape):
         call("ym_conv_dgrad", ctypes.byref(dd), dzbuf.data_ptr(), w_t.data_ptr(), dxbuf.data_ptr(), st)
         torch.cuda.synchronize()
     finally:
-        lib().ym_conv_set_pipe(prev)
+        setter(prev)
     y_ref = F.conv2d(x.float().permute(0, 3, 1, 2), w16.float(), stride=s, padding=p).permute(0, 2, 3, 1)
     dx_ref = torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz.float().permute(0, 3, 1, 2),
                                         stride=s, padding=p).permute(0, 2, 3, 1)

@@ -4,7 +4,8 @@ gen_curve — same key-seeded weights, synth_batch(4, 320, seed=100+step), AdamW
 clip_grad_norm_ 10).
 
 Bound per step: relative loss error <= max(2x that of the CPU oracle run under the HIP
-storage-rounding model (oracle/precision.py) at that step, 1.5x its worst step, 2e-2), and the
+storage-rounding model (oracle/precision.py; the worst of EMU_SAMPLES jittered draws of it) at that
+step, 1.5x its worst step, 2e-2), and the
 mean over the 20 steps <= 2e-2.  The assigner's discrete choices and SPPF's max-pool routing make
 the curve chaotic in the rounding: 16-bit storage alone moves single steps of the oracle by up to
 ~6 %, and any change of summation order (a different reduction split, a different kernel for one
@@ -33,6 +34,9 @@ def _run(model, loss_fn, steps, dev):
     return np.asarray(out)
 
 
+EMU_SAMPLES = 3
+
+
 def test_loss_curve_20_steps_vs_reference(golden):
     from oracle import model as om
     from oracle import loss as ol
@@ -53,26 +57,31 @@ def test_loss_curve_20_steps_vs_reference(golden):
 
     # the same loop on the CPU oracle under the HIP storage-rounding model
     from datasets.synthetic import synth_batch
-    layers, save, P2 = om.build(cfg)
-    params = [v.requires_grad_(True) for k, v in P2.items()
-              if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")]
-    opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
     torch.set_num_threads(8)
-    emu = []
-    for step in range(steps):
-        b = synth_batch(4, 320, seed=100 + step)
-        opt.zero_grad(set_to_none=True)
-        with hip_storage_rounding():
-            heads = om.forward(P2, layers, save, b["img"], training=True)
-        loss = ol.v8_loss(heads, b)[0]
-        loss.backward()
-        torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
-        opt.step()
-        emu.append(float(loss))
-    emu = np.asarray(emu)
 
+    def emulated(jitter):
+        layers, save, P2 = om.build(cfg)
+        params = [v.requires_grad_(True) for k, v in P2.items()
+                  if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")]
+        opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
+        emu = []
+        for step in range(steps):
+            b = synth_batch(4, 320, seed=100 + step)
+            opt.zero_grad(set_to_none=True)
+            with hip_storage_rounding(jitter=jitter):
+                heads = om.forward(P2, layers, save, b["img"], training=True)
+            loss = ol.v8_loss(heads, b)[0]
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
+            opt.step()
+            emu.append(float(loss))
+        return np.asarray(emu)
+
+    # the rounding model's spread over EMU_SAMPLES draws (oracle/precision.py: the curve is a chaotic
+    # function of last-bit differences after a few steps), worst per step
+    emus = [emulated(j) for j in range(EMU_SAMPLES)]
     err = np.abs(gpu - ref) / ref
-    err_emu = np.abs(emu - ref) / ref
+    err_emu = np.max([np.abs(e - ref) / ref for e in emus], axis=0)
     print("gpu rel err", np.round(err, 4).tolist())
     print("emu rel err", np.round(err_emu, 4).tolist())
     bound = np.maximum(np.maximum(2 * err_emu, 1.5 * err_emu.max()), 2e-2)

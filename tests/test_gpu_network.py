@@ -23,30 +23,33 @@ from test_gpu_model import _batch, _seeded_model, rel
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_grads(scale, img, seed, rounding=False):
+def _oracle_grads(scale, img, seed, rounding=False, jitter=0):
     """Parameter gradients of the CPU oracle's network for `seed`: a loss function of the head maps,
-    or fixed head-map gradients; optionally under the HIP storage-rounding model."""
+    or fixed head-map gradients; optionally under the HIP storage-rounding model (sample `jitter`)."""
     import contextlib
     from oracle import model as om
     from oracle.precision import hip_storage_rounding
     layers, save, P = om.build(om.load_cfg(scale))
     leaf = {k: v.requires_grad_(True) for k, v in P.items()
             if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")}
-    with hip_storage_rounding() if rounding else contextlib.nullcontext():
+    with hip_storage_rounding(jitter=jitter) if rounding else contextlib.nullcontext():
         out = om.forward(P, layers, save, torch.as_tensor(img), training=True)
         seed(out).backward() if callable(seed) else torch.autograd.backward(out, seed)
     return {k: v.grad for k, v in leaf.items()}
 
 
 def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_items, ref_grad_norm, ref_full, img,
-                  batch_cpu):
+                  batch_cpu, emu_samples=5):
     """Head maps, loss / items and EVERY parameter gradient of one training step against the
     reference (fixture or oracle run).  Gradients are checked twice:
 
     (1) element-wise against the fp32 oracle's network backward of d loss / d heads evaluated at
         the GPU's own head maps — the loss is a discrete function of the heads (assignment, and
         IoU^4-weighted target scores amplify head rounding), so this isolates the network backward:
-        relative L2 <= max(3e-2, 2 x the storage-rounding model's error on the same head gradients);
+        relative L2 <= max(3e-2, 2 x the storage-rounding model's error on the same head gradients,
+        worst of `emu_samples` samples of that model: oracle/precision.py, the network is chaotic in
+        last-bit differences, e.g. a 1-ulp change in one layer's fp32 BN statistics moves the s@128
+        stem-weight gradient error from 0.10 to 0.16 with every kernel output still correct);
     (2) in norm against the reference's gradients: <= max(0.1, 2 x the rounding model's error,
         2 x the change the GPU's head values alone cause in the fp32 oracle's gradient)."""
     from oracle import loss as ol
@@ -63,7 +66,8 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
     ol.v8_loss(hg, batch_cpu)[0].backward()
     dh = [h.grad for h in hg]
     at_gpu = _oracle_grads(scale, img, dh)
-    at_gpu_emu = _oracle_grads(scale, img, dh, rounding=True)
+    # the rounding model's spread: the unperturbed sample and EMU_SAMPLES - 1 jittered ones
+    at_gpu_emu = [_oracle_grads(scale, img, dh, rounding=True, jitter=j) for j in range(emu_samples)]
     emu = _oracle_grads(scale, img, lambda h: ol.v8_loss(h, batch_cpu)[0], rounding=True)
     gmax = max(ref_grad_norm.values())
     gmax_at = max(float(v.norm()) for v in at_gpu.values())
@@ -76,7 +80,7 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
         r = at_gpu[k].double()
         sc = max(float(r.norm()), 1e-4 * gmax_at)
         err1 = float((g - r).norm()) / sc
-        tol1 = max(3e-2, 2.0 * float((at_gpu_emu[k].double() - r).norm()) / sc)
+        tol1 = max(3e-2, 2.0 * max(float((e[k].double() - r).norm()) for e in at_gpu_emu) / sc)
         worst1.append((err1 / tol1, k, err1, tol1))
         assert err1 <= tol1, ("vs oracle at GPU heads", k, err1, tol1)
         # (2) against the reference's gradient norm
@@ -138,7 +142,7 @@ def test_model_s640_bs2_train_step_vs_oracle():
     full = {k: leaf[k].grad for k in ("model.0.conv.weight", "model.10.m.0.attn.qkv.conv.weight",
                                       "model.23.cv3.0.2.weight")}
     worst = check_network("s", heads, loss, items, m, [h.detach() for h in ref_heads], float(rl), ri.detach(),
-                           ref_norm, full, b["img"], {k: v for k, v in b.items() if k != "img"})
+                           ref_norm, full, b["img"], {k: v for k, v in b.items() if k != "img"}, emu_samples=3)
     print("worst err/tol", worst)
 
 
