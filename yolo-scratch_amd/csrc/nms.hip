@@ -585,6 +585,170 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(int64_t N, int64_t KP, in
     if (tid == 0) out_count[b] = nk;
 }
 
+// Greedy scan, ONE wave per image, visiting only what the kept rows need (nms_scan_kernel reads the
+// whole upper triangle: every earlier row of every column, ~K^2/128 words per image).  A chunk c's
+// removed bits come from two places:
+//  * NEAR rows (the previous group of 4 chunks and the earlier chunks of this group): the words
+//    D(c', c) = column c, rows 64c'..64c'+63 are loaded one group AHEAD (they do not depend on any
+//    decision; coalesced 512-B wave loads) and OR-ed under the kept bits of chunk c';
+//  * FAR rows (two or more groups back): each lane accumulates, for the column blocks it owns
+//    (cb = lane + 64k), the words of every kept row; a group's kept rows are gathered at the start
+//    of the group after next (the loads fly during a whole group of chunk work).
+// The per-chunk work is then one wave OR, the fixpoint of the chunk's 64x64 diagonal block and the
+// keep update: no workgroup barrier, and ~(kept x Wn + 26 x 64 x groups) words read instead of the
+// triangle.  Same decisions as nms_scan_kernel (a box is kept iff no earlier kept box has
+// IoU > thr with it): the removed bits of chunk c are the OR over ALL kept rows j < 64c of
+// mask[j][c], split into near and far.
+constexpr int SCAN_WL = (BM_MAX_WN + 63) / 64;      // column-block words per lane (far bits)
+constexpr int SCAN_RB = 8;                          // kept rows per group gathered asynchronously
+
+__global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP, int Wn, float img_size, Ws w,
+                                                           int32_t* __restrict__ out_count,
+                                                           float* __restrict__ out_boxes,
+                                                           float* __restrict__ out_scores,
+                                                           int64_t* __restrict__ out_labels,
+                                                           int64_t* __restrict__ out_index) {
+    __shared__ int rows_sh[256];
+    const int64_t b = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int K = w.kcount[b];
+    const int64_t base = b * N;
+    if (K == 0) {
+        if (lane == 0) out_count[b] = 0;
+        return;
+    }
+    const int nch = (K + 63) / 64;
+    const int ngr = (nch + 3) / 4;
+    const uint64_t* mcol = w.mask + int64_t(b) * Wn * N;     // column cb: mcol + cb * N, row-indexed
+
+    uint64_t far[SCAN_WL];
+#pragma unroll
+    for (int k = 0; k < SCAN_WL; ++k) far[k] = 0;
+    // D(c', c) for the 4 chunks q of a group: slot s <-> c' = 4g - 4 + s (s <= 4 + q)
+    uint64_t dcur[4][8], dnx[4][8];
+    auto load_group = [&](int g, uint64_t (&d)[4][8]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int c = 4 * g + q, cp = 4 * g - 4 + s;
+                if (s <= 4 + q && c < nch && cp >= 0) d[q][s] = mcol[int64_t(c) * N + 64 * cp + lane];
+                else d[q][s] = 0;
+            }
+    };
+    uint64_t kprev[4] = {0, 0, 0, 0};                 // kept bits of the previous group's chunks
+    uint64_t pend[SCAN_RB][SCAN_WL];                   // far words of the gathered rows, in flight
+    int npend = 0, pend_g = -1;                        // rows in flight, and the group they belong to
+    int nkept = 0;
+    load_group(0, dcur);
+    for (int g = 0; g < ngr; ++g) {
+        if (g + 1 < ngr) load_group(g + 1, dnx);
+        // kept rows of group g-1 -> far words of the columns beyond the next group's near window
+        // (cb >= 4(g+1)); gathered now, OR-ed into far at the end of this group
+        npend = 0;
+        if (g >= 1) {
+            int nr = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint64_t kb = kprev[q];
+                if ((kb >> lane) & 1)
+                    rows_sh[nr + __popcll(kb & ((uint64_t(1) << lane) - 1))] = 64 * (4 * (g - 1) + q) + lane;
+                nr += __popcll(kb);
+            }
+            __builtin_amdgcn_wave_barrier();
+            const int cb_lo = 4 * (g + 1);
+            auto row_words = [&](int j, uint64_t* dst) {
+#pragma unroll
+                for (int k = 0; k < SCAN_WL; ++k) {
+                    const int cb = lane + 64 * k;
+                    dst[k] = (cb >= cb_lo && cb < Wn) ? mcol[int64_t(cb) * N + j] : 0;
+                }
+            };
+            npend = min(nr, SCAN_RB);
+#pragma unroll
+            for (int r = 0; r < SCAN_RB; ++r) {
+                if (r < npend) row_words(rows_sh[r], pend[r]);
+                else
+#pragma unroll
+                    for (int k = 0; k < SCAN_WL; ++k) pend[r][k] = 0;
+            }
+            for (int r = SCAN_RB; r < nr; ++r) {       // more than SCAN_RB kept rows: synchronously
+                uint64_t t[SCAN_WL];
+                row_words(rows_sh[r], t);
+#pragma unroll
+                for (int k = 0; k < SCAN_WL; ++k) far[k] |= t[k];
+            }
+            pend_g = g;
+        }
+        uint64_t kcur[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int c = 4 * g + q;
+            if (c >= nch) break;
+            // near rows: previous group (slots 0..3) and this group's earlier chunks (slots 4..4+q-1)
+            uint64_t near = 0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                if ((kprev[s] >> lane) & 1) near |= dcur[q][s];
+#pragma unroll
+            for (int s = 0; s < q; ++s)
+                if ((kcur[s] >> lane) & 1) near |= dcur[q][4 + s];
+            near = wave_or64(near);
+            // far rows: column c's word lives in lane c & 63, slot c >> 6
+            const int kw = c >> 6;
+            uint64_t fw = far[0];
+#pragma unroll
+            for (int k = 1; k < SCAN_WL; ++k)
+                if (kw == k) fw = far[k];
+            const uint32_t flo = uint32_t(__shfl(int(uint32_t(fw)), c & 63, 64));
+            const uint32_t fhi = uint32_t(__shfl(int(uint32_t(fw >> 32)), c & 63, 64));
+            const uint64_t rem = near | (uint64_t(fhi) << 32) | flo;
+            const int rows = min(64, K - 64 * c);
+            const uint64_t diag = lane < rows ? dcur[q][4 + q] : 0;
+            const uint64_t init = ~rem & (rows == 64 ? ~uint64_t(0) : ((uint64_t(1) << rows) - 1));
+            uint64_t alive = init;
+            for (int it = 0; it <= 64; ++it) {         // unique fixpoint of alive = init & ~OR{diag_s : s alive}
+                const uint64_t nxt = init & ~wave_or64(((alive >> lane) & 1) ? diag : 0);
+                if (nxt == alive) break;
+                alive = nxt;
+            }
+            if ((alive >> lane) & 1) out_index[base + nkept + __popcll(alive & ((uint64_t(1) << lane) - 1))] = 64 * c + lane;
+            nkept += __popcll(alive);
+            kcur[q] = alive;
+        }
+        // rows gathered at the start of this group join the far words (first use: group g+2)
+        if (pend_g == g)
+#pragma unroll
+            for (int r = 0; r < SCAN_RB; ++r)
+#pragma unroll
+                for (int k = 0; k < SCAN_WL; ++k) far[k] |= pend[r][k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) kprev[q] = kcur[q];
+        if (g + 1 < ngr)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) dcur[q][s] = dnx[q][s];
+    }
+    __syncthreads();                                 // this wave's out_index stores are visible to its loads
+    // outputs in kept order (sorted position -> filtered index -> row)
+    for (int k = lane; k < nkept; k += 64) {
+        const int spos = int(out_index[base + k]);
+        const int f = int(uint32_t(w.keys[b * KP + spos]));
+        const int64_t row = base + w.frow[base + f];
+        float4 bx = w.box[row];
+        bx.x = fminf(fmaxf(bx.x / img_size, 0.0f), 1.0f);
+        bx.y = fminf(fmaxf(bx.y / img_size, 0.0f), 1.0f);
+        bx.z = fminf(fmaxf(bx.z / img_size, 0.0f), 1.0f);
+        bx.w = fminf(fmaxf(bx.w / img_size, 0.0f), 1.0f);
+        reinterpret_cast<float4*>(out_boxes)[base + k] = bx;
+        out_scores[base + k] = w.score[row];
+        out_labels[base + k] = w.label[row];
+        out_index[base + k] = f;
+    }
+    if (lane == 0) out_count[b] = nkept;
+}
+
 int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int clamp_norm, Ws w,
                int32_t* out_count, float* out_boxes, float* out_scores, int64_t* out_labels, int64_t* out_index,
                hipStream_t st) {
@@ -603,10 +767,17 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
         hipLaunchKernelGGL(nms_rank_scatter_kernel, dim3(nt, unsigned(B)), dim3(256), 0, st, Nalloc, KP, w);
         hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn), unsigned(Wn), unsigned(B)), dim3(64), 0, st, Nalloc, Wn,
                            iou_thr, w);
-        const size_t scan_lds = 0;
         static const int stamps = getenv("YM_NMS_STAMPS") != nullptr;
-        hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), scan_lds, st, Nalloc, KP, Wn, img_size, w,
-                           out_count, out_boxes, out_scores, out_labels, out_index, stamps);
+        static const int old_scan = [] {         // YM_NMS_SCAN=0: the whole-triangle workgroup scan (A/B)
+            const char* e = getenv("YM_NMS_SCAN");
+            return e && e[0] == '0';
+        }();
+        if (old_scan || stamps)
+            hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), 0, st, Nalloc, KP, Wn, img_size, w,
+                               out_count, out_boxes, out_scores, out_labels, out_index, stamps);
+        else
+            hipLaunchKernelGGL(nms_scan_wave_kernel, dim3(unsigned(B)), dim3(64), 0, st, Nalloc, KP, Wn, img_size, w,
+                               out_count, out_boxes, out_scores, out_labels, out_index);
         YM_LAUNCH_CHECK("nms bitmask path");
         return YM_OK;
     }
