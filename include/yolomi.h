@@ -256,6 +256,14 @@ int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                    float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* workspace,
                    void* stream);
+/* Eval-mode coefficients of many BatchNorm layers in ONE launch (the eval forward's per-layer
+ * ym_bn_eval_coeff calls were 77 launches per YOLOv11-s forward); table in device memory. */
+typedef struct ym_bn_eval_entry {
+    const float* gamma; const float* beta; const float* running_mean; const float* running_var;
+    float* scale; float* shift;
+    int32_t c; float eps;
+} ym_bn_eval_entry;
+int ym_bn_eval_coeff_batch(const ym_bn_eval_entry* table_dev, int n_entries, void* stream);
 int ym_bn_eval_coeff(int c, const float* gamma, const float* beta, const float* running_mean,
                      const float* running_var, float eps, float* scale, float* shift, void* stream);
 /* out_view = act(z*scale+shift) (+ res_view); act: 0 identity, 1 SiLU; hw = pixels per image */

@@ -245,6 +245,17 @@ __global__ void bn_eval_coeff_kernel(int C, const float* gamma, const float* bet
     shift[c] = beta[c] - rm[c] * sc;
 }
 
+// eval: every layer of a table, block y = layer (bn_eval_coeff_kernel's arithmetic)
+__global__ void bn_eval_coeff_batch_kernel(const ym_bn_eval_entry* __restrict__ tab) {
+    const ym_bn_eval_entry e = tab[blockIdx.y];
+    for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < e.c; c += gridDim.x * blockDim.x) {
+        const float rstd = 1.0f / sqrtf(e.running_var[c] + e.eps);
+        const float sc = e.gamma[c] * rstd;
+        e.scale[c] = sc;
+        e.shift[c] = e.beta[c] - e.running_mean[c] * sc;
+    }
+}
+
 // ---------------------------------------------------------------- streaming kernels
 struct Lanes {
     int g, r, rows;
@@ -511,6 +522,15 @@ extern "C" int ym_bn_eval_coeff(int c, const float* gamma, const float* beta, co
     hipLaunchKernelGGL(bn_eval_coeff_kernel, dim3((c + 255) / 256), dim3(256), 0, as_stream(stream), c, gamma, beta,
                        running_mean, running_var, eps, scale, shift);
     YM_LAUNCH_CHECK("ym_bn_eval_coeff");
+    return YM_OK;
+}
+
+extern "C" int ym_bn_eval_coeff_batch(const ym_bn_eval_entry* table_dev, int n_entries, void* stream) {
+    YM_CHECK_ARG(n_entries >= 0 && (table_dev || n_entries == 0), "ym_bn_eval_coeff_batch: null table");
+    if (n_entries == 0) return YM_OK;
+    hipLaunchKernelGGL(bn_eval_coeff_batch_kernel, dim3(8, unsigned(n_entries)), dim3(256), 0, as_stream(stream),
+                       table_dev);
+    YM_LAUNCH_CHECK("ym_bn_eval_coeff_batch");
     return YM_OK;
 }
 

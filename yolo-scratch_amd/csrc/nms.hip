@@ -600,6 +600,11 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(int64_t N, int64_t KP, in
 // IoU > thr with it): the removed bits of chunk c are the OR over ALL kept rows j < 64c of
 // mask[j][c], split into near and far.
 constexpr int SCAN_WL = (BM_MAX_WN + 63) / 64;      // column-block words per lane (far bits)
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32) |
+           uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), l));
+}
 constexpr int SCAN_RB = 8;                          // kept rows per group gathered asynchronously
 
 __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP, int Wn, float img_size, Ws w,
@@ -625,7 +630,7 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
 #pragma unroll
     for (int k = 0; k < SCAN_WL; ++k) far[k] = 0;
     // D(c', c) for the 4 chunks q of a group: slot s <-> c' = 4g - 4 + s (s <= 4 + q)
-    uint64_t dcur[4][8], dnx[4][8];
+    uint64_t dcur[4][8], dnx[4][8], dnx2[4][8];
     auto load_group = [&](int g, uint64_t (&d)[4][8]) {
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -641,8 +646,9 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
     int npend = 0, pend_g = -1;                        // rows in flight, and the group they belong to
     int nkept = 0;
     load_group(0, dcur);
+    if (1 < ngr) load_group(1, dnx);
     for (int g = 0; g < ngr; ++g) {
-        if (g + 1 < ngr) load_group(g + 1, dnx);
+        if (g + 2 < ngr) load_group(g + 2, dnx2);      // two groups ahead: a group's work < one load latency
         // kept rows of group g-1 -> far words of the columns beyond the next group's near window
         // (cb >= 4(g+1)); gathered now, OR-ed into far at the end of this group
         npend = 0;
@@ -685,32 +691,30 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
         for (int q = 0; q < 4; ++q) {
             const int c = 4 * g + q;
             if (c >= nch) break;
-            // near rows: previous group (slots 0..3) and this group's earlier chunks (slots 4..4+q-1)
+            // near rows: previous group (slots 0..3) and this group's earlier chunks (slots 4..4+q-1);
+            // one lane read per KEPT row (a handful per window) instead of a wave-wide OR
             uint64_t near = 0;
 #pragma unroll
-            for (int s = 0; s < 4; ++s)
-                if ((kprev[s] >> lane) & 1) near |= dcur[q][s];
-#pragma unroll
-            for (int s = 0; s < q; ++s)
-                if ((kcur[s] >> lane) & 1) near |= dcur[q][4 + s];
-            near = wave_or64(near);
+            for (int s = 0; s < 4 + q; ++s)
+                for (uint64_t kb = s < 4 ? kprev[s] : kcur[s - 4]; kb; kb &= kb - 1)
+                    near |= readlane64(dcur[q][s], __builtin_ctzll(kb));
             // far rows: column c's word lives in lane c & 63, slot c >> 6
             const int kw = c >> 6;
             uint64_t fw = far[0];
 #pragma unroll
             for (int k = 1; k < SCAN_WL; ++k)
                 if (kw == k) fw = far[k];
-            const uint32_t flo = uint32_t(__shfl(int(uint32_t(fw)), c & 63, 64));
-            const uint32_t fhi = uint32_t(__shfl(int(uint32_t(fw >> 32)), c & 63, 64));
-            const uint64_t rem = near | (uint64_t(fhi) << 32) | flo;
+            const uint64_t rem = near | readlane64(fw, c & 63);
             const int rows = min(64, K - 64 * c);
-            const uint64_t diag = lane < rows ? dcur[q][4 + q] : 0;
-            const uint64_t init = ~rem & (rows == 64 ? ~uint64_t(0) : ((uint64_t(1) << rows) - 1));
-            uint64_t alive = init;
-            for (int it = 0; it <= 64; ++it) {         // unique fixpoint of alive = init & ~OR{diag_s : s alive}
-                const uint64_t nxt = init & ~wave_or64(((alive >> lane) & 1) ? diag : 0);
-                if (nxt == alive) break;
-                alive = nxt;
+            const uint64_t diag = dcur[q][4 + q];
+            // the diagonal block greedily, one iteration per KEPT row (~1-2 per chunk): the lowest
+            // undecided bit s survives, and its row (lane s's word, bits > s only) removes later bits
+            uint64_t und = ~rem & (rows == 64 ? ~uint64_t(0) : ((uint64_t(1) << rows) - 1));
+            uint64_t alive = 0;
+            while (und) {
+                const int sl = __builtin_ctzll(und);
+                alive |= uint64_t(1) << sl;
+                und &= ~readlane64(diag, sl) & ~(uint64_t(1) << sl);
             }
             if ((alive >> lane) & 1) out_index[base + nkept + __popcll(alive & ((uint64_t(1) << lane) - 1))] = 64 * c + lane;
             nkept += __popcll(alive);
@@ -728,7 +732,10 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int s = 0; s < 8; ++s) dcur[q][s] = dnx[q][s];
+                for (int s = 0; s < 8; ++s) {
+                    dcur[q][s] = dnx[q][s];
+                    dnx[q][s] = dnx2[q][s];
+                }
     }
     __syncthreads();                                 // this wave's out_index stores are visible to its loads
     // outputs in kept order (sorted position -> filtered index -> row)

@@ -45,6 +45,12 @@ class WPrepEntry(ctypes.Structure):
                 ("kh", I32), ("kw", I32), ("cout_t", I32)]
 
 
+class BnEvalEntry(ctypes.Structure):
+    """ym_bn_eval_entry (include/yolomi.h)."""
+    _fields_ = [("gamma", P), ("beta", P), ("running_mean", P), ("running_var", P), ("scale", P), ("shift", P),
+                ("c", I32), ("eps", _c.c_float)]
+
+
 R = _c.c_int
 # name -> (restype, argtypes); must match include/yolomi.h
 SIGNATURES = {
@@ -82,6 +88,7 @@ SIGNATURES = {
     "ym_bn_workspace_size": (SZ, [INT]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
     "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
+    "ym_bn_eval_coeff_batch": (R, [P, INT, P]),
     "ym_bn_apply": (R, [P, I64, INT, INT, P, P, INT, P, I64, I64, P, I64, I64, P, P]),
     "ym_bn_bwd_blocks": (R, [I64, INT]),
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),

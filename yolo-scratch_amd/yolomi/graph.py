@@ -23,7 +23,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import BnTrain, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
+from ._lib import BnEvalEntry, BnTrain, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
 
 BF16 = torch.bfloat16
 F16 = torch.float16
@@ -132,6 +132,8 @@ class WeightStore:
     def add(self, w: torch.nn.Parameter, need_t: bool, cout_t: int | None = None):
         co, ci, kh, kw = w.shape
         cout_t = cout_t or co
+        # an eval-mode model plan never runs a backward: no transposed data-gradient copy to prepare
+        need_t = need_t and (self.plan.training or not getattr(self.plan, "is_model", False))
         fwd = torch.empty(co, kh, kw, ci, dtype=F16, device=self.plan.dev)
         t = torch.zeros(ci, kh, kw, cout_t, dtype=BF16, device=self.plan.dev) if need_t else None
         self.items.append((w, fwd, t, cout_t))
@@ -278,7 +280,7 @@ class ConvBN:
                 call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
                      _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
                      float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-            else:
+            elif not plan.eval_coeff_batched:
                 call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
                      _p(bn.running_var), float(bn.eps), sc, sh, st)
             call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, self.act,
@@ -409,7 +411,7 @@ class StemConvBN(ConvBN):
                 call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
                      _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
                      float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-            else:
+            elif not plan.eval_coeff_batched:
                 call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
                      _p(bn.running_var), float(bn.eps), sc, sh, st)
             call("ym_stem_apply", plan.img.data_ptr(), _p(self.m.conv.weight), sc, sh, self.y.ptr(), self.y.bs,
@@ -714,6 +716,7 @@ def op_params(op):
 class Plan:
     def __init__(self, root, B, H, W, dev, training):
         self.root, self.B, self.dev, self.training = root, B, dev, training
+        self.eval_coeff_batched = not training and dev.type == "cuda"   # one launch for every layer
         self.acts, self.ops = [], []
         self.weights = WeightStore(self)
         self.probe, self.probe_events = None, []   # bench: time one op's conv launch
@@ -981,10 +984,31 @@ class Plan:
         g.replay()
 
     # --------------------------------------------------------------- run
+    def _eval_coeffs(self, st):
+        """Eval: every BatchNorm layer's scale / shift from its running statistics in ONE launch
+        (ym_bn_eval_coeff_batch over a pointer table built once per plan; the parameters and buffers
+        are read at launch time, so later weight / statistics updates are picked up)."""
+        key = tuple(op.m.bn.weight.data_ptr() for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m"))
+        if getattr(self, "_eval_key", None) != key:
+            ents = [op for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m")]
+            arr = (BnEvalEntry * len(ents))()
+            for e, op in zip(arr, ents):
+                bn = op.m.bn
+                e.gamma, e.beta = _p(bn.weight), _p(bn.bias)
+                e.running_mean, e.running_var = _p(bn.running_mean), _p(bn.running_var)
+                e.scale, e.shift = op.bnv[0].data_ptr(), op.bnv[1].data_ptr()
+                e.c, e.eps = op.bnv.shape[1], float(bn.eps)
+            self._eval_table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.dev)
+            self._eval_n = len(ents)
+            self._eval_key = key
+        call("ym_bn_eval_coeff_batch", self._eval_table.data_ptr(), self._eval_n, st)
+
     def forward(self):
         def body():
             st = stream_ptr(self.dev)
             self.weights.refresh(st)
+            if self.eval_coeff_batched:
+                self._eval_coeffs(st)
             self._run(self.ops, "fwd")
         self._replay("fwd", body, [("img", self.img)] if self.img is not None else [])
 
