@@ -943,9 +943,25 @@ class Plan:
     # s@640 bs64 step, replay is 1.5-2 ms SLOWER than eager launches (26.3-26.7 vs 24.7 ms/step at
     # 1 and 2 streams): the eager host enqueue already runs ahead of the GPU, and the replayed
     # graph runs its kernels with less overlap than the streams do.
+    # Eval-mode model plans can replay their forward as a HIP graph (YM_EVAL_GRAPH=1; training:
+    # YM_GRAPH=1).  Measured SLOWER, so off by default: s@640 inference bs1 2.66 vs 1.80 ms eager,
+    # bs128 13.7 vs 13.1 ms — the replay of ~175 multi-stream nodes costs more than the eager
+    # ctypes enqueue it removes.  The captured launches read weights, BatchNorm buffers and the
+    # image at fixed addresses: parameters updated in place (optimizer steps, load_state_dict) are
+    # seen by the replay; a parameter or buffer REPLACED by a new tensor changes the address key
+    # checked before every eval replay, which drops the graph (eager run, then a new capture).
     def _graph_ok(self):
-        return (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
-                and self.family_events is None and os.environ.get("YM_GRAPH", "0") == "1")
+        if not (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
+                and self.family_events is None):
+            return False
+        if not self.training:
+            return os.environ.get("YM_EVAL_GRAPH", "0") == "1"
+        return os.environ.get("YM_GRAPH", "0") == "1"
+
+    def _address_key(self):
+        return (tuple(w.data_ptr() for w, *_ in self.weights.items),
+                tuple((op.m.bn.weight.data_ptr(), op.m.bn.running_mean.data_ptr(), op.m.bn.running_var.data_ptr())
+                      for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m")))
 
     @property
     def graph_active(self):
@@ -959,6 +975,12 @@ class Plan:
         if not self._graph_ok():
             body()
             return
+        if not self.training:
+            key = self._address_key()
+            if key != self.__dict__.get("_graph_key"):
+                graphs.clear()
+                runs.clear()
+                self._graph_key = key
         if runs.get(phase, 0) < 1:
             runs[phase] = runs.get(phase, 0) + 1
             body()
