@@ -245,6 +245,127 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
     }
 }
 
+// Stride-2 3x3 data gradient by output-ROW parity PY: a task is 16 x TP column PAIRS (2j, 2j+1) of
+// rows 2i + PY, both column classes computed by the same wave — column 2j takes tap kw = 1 from dz
+// column j, column 2j + 1 taps kw = 0 / 2 from dz columns j + 1 / j — and the epilogue stores the
+// pair's two 16-pixel groups back to back, so each 128-B line of dx (two 32-channel bf16 pixels) is
+// completed by one wave at one time.  (One class per task wrote every other pixel: 64-B halves of
+// lines whose other half came from another grid row of classes much later — 2 TB/s on the s@640
+// model.1 data gradient whose HBM roof is ~6 TB/s.)
+template <int NT, int KC, int TP, int PY>
+__device__ __forceinline__ void direct_body_s2dg(const DirArgs& a, int64_t first, int64_t step, int64_t ntask,
+                                                 char* ep) {
+    using F = bf16x8;
+    const int lane = threadIdx.x & 63, fr = lane & 15, fc = lane >> 4;
+    auto live = [&](int t) constexpr -> bool { return ((PY + 1 - t / 3) & 1) == 0; };
+    auto pxof = [&](int t) constexpr -> int { return (t % 3) == 1 ? 0 : 1; };
+    F wa[9][KC][NT];
+    {
+        const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, int64_t(a.Nout) * 9 * a.Kin * 2);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (!live(t)) continue;
+#pragma unroll
+            for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                for (int nt = 0; nt < NT; ++nt) {
+                    const int co = nt * 16 + fr;
+                    const uint32_t off = co < a.Nout ? uint32_t(((co * 9 + t) * a.Kin + kc * 32 + fc * 8) * 2) : OOB;
+                    wa[t][kc][nt] = __builtin_bit_cast(F, buf_load16(wr, off));
+                }
+        }
+    }
+    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
+    const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
+    // lane's pixel pair in each group: image n, dx row oh, pair j (columns 2j, 2j + 1)
+    struct Pairs {
+        int n[TP], oh[TP], j[TP];
+        bool ok[TP];
+    };
+    auto decode = [&](int64_t tl, Pairs& P) {
+        const uint32_t chw = uint32_t(a.OHc) * uint32_t(a.OWc);
+#pragma unroll
+        for (int g = 0; g < TP; ++g) {
+            const int64_t m = tl * (16 * TP) + g * 16 + fr;
+            const uint32_t nn = uint32_t(m / chw), r = uint32_t(m - int64_t(nn) * chw);
+            const uint32_t i = r / uint32_t(a.OWc), j = r - i * uint32_t(a.OWc);
+            P.n[g] = int(nn);
+            P.oh[g] = int(i) * 2 + PY;
+            P.j[g] = int(j);
+            P.ok[g] = int(nn) < a.N && P.oh[g] < a.OH;
+        }
+    };
+    auto load = [&](const Pairs& P, F (&b)[9][TP][KC]) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (!live(t)) continue;
+            const int kh = t / 3, kw = t % 3;
+#pragma unroll
+            for (int g = 0; g < TP; ++g) {
+                const int ow = 2 * P.j[g] + pxof(t);
+                const int ih = (P.oh[g] + a.pad - kh) >> 1, iw = (ow + a.pad - kw) >> 1;
+                const bool in = P.ok[g] && ow < a.OW && unsigned(ih) < unsigned(a.GH) && unsigned(iw) < unsigned(a.GW);
+                const uint32_t base =
+                    in ? uint32_t((int64_t(P.n[g]) * a.x_bs + (int64_t(ih) * a.GW + iw) * a.x_ld + fc * 8) * 2) : OOB;
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc)
+                    b[t][g][kc] = __builtin_bit_cast(F, buf_load16(xr, base == OOB ? OOB : base + kc * 64));
+            }
+        }
+    };
+    Pairs P;
+    F b[9][TP][KC];
+    int64_t task = first;
+    if (task < ntask) {
+        decode(task, P);
+        load(P, b);
+    }
+    float ssum[NT][4], ssq[NT][4];     // unused (no statistics in a data gradient)
+    for (; task < ntask; task += step) {
+        // acc[2g + px]: the pair's two columns as adjacent 16-pixel groups
+        f32x4 accT[NT][2 * TP];
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int q = 0; q < 2 * TP; ++q) accT[nt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            if (!live(t)) continue;
+#pragma unroll
+            for (int g = 0; g < TP; ++g)
+#pragma unroll
+                for (int kc = 0; kc < KC; ++kc)
+#pragma unroll
+                    for (int nt = 0; nt < NT; ++nt)
+                        accT[nt][2 * g + pxof(t)] = mma(wa[t][kc][nt], b[t][g][kc], accT[nt][2 * g + pxof(t)]);
+        }
+        const Pairs Q = P;
+        if (task + step < ntask) {
+            decode(task + step, P);
+            load(P, b);
+        }
+        uint32_t own[2 * TP];
+#pragma unroll
+        for (int g = 0; g < TP; ++g)
+#pragma unroll
+            for (int px = 0; px < 2; ++px) {
+                const int ow = 2 * Q.j[g] + px;
+                own[2 * g + px] = Q.ok[g] && ow < a.OW
+                                      ? uint32_t((int64_t(Q.n[g]) * a.y_bs + (int64_t(Q.oh[g]) * a.OW + ow) * a.y_ld) * 2)
+                                      : OOB;
+            }
+        auto pix_off = [&](int q) -> uint32_t {
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < 2 * TP; ++k)
+                if ((q >> 4) == k) v = own[k];
+            return uint32_t(__shfl(int(v), q & 15, 64));
+        };
+        epilogue_store<NT, 2 * TP>(accT, ssum, ssq, false, ep, lane, 0, a.Nout, yres, false, a.accumulate != 0,
+                                   pix_off);
+    }
+}
+
 // grid (blocks, classes): blockIdx.y is the output-parity class of a stride-2 data gradient
 template <int NT, int KC, int KS, int S, int MODE, int TP>
 __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
@@ -263,6 +384,13 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
     const int64_t lo = a.tpc * xcd / 8, hi = a.tpc * (xcd + 1) / 8;
     const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
+    if constexpr (S == 2 && MODE == 1 && KS == 3 && (NT == 2 || NT == 4)) {
+        if (a.ncls == 2) {           // row-parity classes, column pairs per task (direct_body_s2dg)
+            if (blockIdx.y == 0) direct_body_s2dg<NT, KC, TP, 0>(a, first, step, hi, epl[wave]);
+            else direct_body_s2dg<NT, KC, TP, 1>(a, first, step, hi, epl[wave]);
+            return;
+        }
+    }
     if constexpr (S == 2 && MODE == 1) {
         switch (blockIdx.y) {
             case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]); break;
@@ -312,7 +440,7 @@ struct Variant {
 // measured slower than the implicit GEMM: 0.083 vs 0.076 ms)
 const Variant kVariants[] = {
     YM_DIR(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
-    YM_DIR(2, 2, 3, 2, 1, 2),   // dgrad of it: dz 64 -> dx 32, 4 parity classes
+    YM_DIR(2, 2, 3, 2, 1, 1),   // dgrad of it: dz 64 -> dx 32, row-parity classes x column pairs
     YM_DIR(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
     YM_DIR(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
     YM_DIR(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
@@ -321,6 +449,16 @@ const Variant kVariants[] = {
     YM_DIR(6, 4, 1, 1, 1, 2),   // dgrad: dz 128 -> dx 96
 };
 #undef YM_DIR
+
+// stride-2 data gradients as 2 row-parity classes over column pairs (default) or 4 parity classes
+// (YM_DIRECT_S2PAIR=0, A/B runs)
+bool s2_pairs() {
+    static const bool v = [] {
+        const char* e = getenv("YM_DIRECT_S2PAIR");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 
 int direct_mode() {
     if (g_direct_force >= 0) return g_direct_force;
@@ -360,8 +498,12 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
         const int os = dgrad ? d->stride : 1;
         const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
         const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
-        p.classes = os * os;
-        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(1024 / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
+        p.classes = os == 2 && s2_pairs() ? 2 : os * os;
+        static const int gcap = [] {     // total workgroups over the classes (YM_DIRECT_GRID: A/B runs)
+            const char* e = getenv("YM_DIRECT_GRID");
+            return e ? std::max(64, atoi(e)) : 1024;
+        }();
+        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(gcap / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
         return p;
     }
     return p;
@@ -382,8 +524,8 @@ int direct_launch(const DirectPlan& p, const ym_conv_desc* d, int dgrad, const u
     }
     a.N = d->n; a.pad = d->pad; a.accumulate = d->accumulate;
     const int os = dgrad ? d->stride : 1;
-    a.OHc = (a.OH + os - 1) / os; a.OWc = (a.OW + os - 1) / os;
-    a.ncls = os * os;
+    a.OHc = (a.OH + os - 1) / os; a.OWc = (a.OW + os - 1) / os;   // (pairs mode: OWc = column pairs)
+    a.ncls = p.classes;
     a.tpc = (int64_t(a.N) * a.OHc * a.OWc + 16 * v.tp - 1) / (16 * v.tp);
     hipLaunchKernelGGL(v.fn, dim3(p.grid, a.ncls), dim3(256), 0, st, a);
     return 0;
