@@ -225,6 +225,13 @@ int ym_stem_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const flo
                        const float* bnv, float* part_sum, float* part_dot, int blocks, int n, int h, int w, int oh,
                        int ow, int cout, int stride, int pad, void* stream);
 size_t ym_stem_bwd_wgrad_workspace_size(int cout);
+/* Stored-z stem backward: dz = BatchNorm-backward apply of dy on the STORED fp16 z (dense
+ * [m][cout]) straight into the weight-gradient partials (dz never written) — replaces
+ * ym_bn_bwd_apply + ym_conv_first_wgrad for the stored path; workspace as ym_stem_bwd_wgrad. */
+int ym_stem_bwd_wgrad_stored(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, const float* img,
+                             const float* bnv, const float* coef, float* dw_oihw, float* workspace,
+                             size_t workspace_bytes, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
+                             void* stream);
 int ym_stem_bwd_wgrad(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
                       const float* bnv, const float* coef, float* dw_oihw, float* workspace, size_t workspace_bytes,
                       int n, int h, int w, int oh, int ow, int cout, int stride, int pad, void* stream);

@@ -338,6 +338,7 @@ def test_stem_recompute_matches_stored(golden, monkeypatch):
     d = golden("blocks.npz")
     sd = {k[len("conv0") + 3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("conv0/p:")}
     out = []
+    monkeypatch.setenv("YM_STEM_FUSED_BWD", "0")           # stored path: separate BN apply + weight gradient
     for flag in ("0", "1"):
         monkeypatch.setenv("YM_STEM_RECOMPUTE", flag)      # read when the block's plan is built
         mod = M.Conv(1, 32, 3, 2)
@@ -354,3 +355,29 @@ def test_stem_recompute_matches_stored(golden, monkeypatch):
         assert rel(g1[k], g0[k]) < 1e-4, (k, rel(g1[k], g0[k]))
     for k in s0:
         assert rel(s1[k], s0[k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 64), (3, 47, 61)])
+def test_stem_fused_bwd_matches_unfused(monkeypatch, shape):
+    """The stored-z stem backward with the BatchNorm apply fused into the weight gradient
+    (ym_stem_bwd_wgrad_stored: dz never written) against ym_bn_bwd_apply + ym_conv_first_wgrad on the
+    same input and output gradient (odd map sizes: partial 8x32 tiles): the same bf16 dz rounding,
+    weight-gradient partials summed in a different fixed order — parameter gradients within 1e-5."""
+    import models as M
+    g = torch.Generator().manual_seed(sum(shape))
+    B, H, W = shape
+    x = torch.rand(B, 1, H, W, generator=g)
+    mod0 = M.Conv(1, 32, 3, 2)
+    sd = mod0.state_dict()
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("YM_STEM_FUSED_BWD", flag)
+        mod = M.Conv(1, 32, 3, 2)
+        mod.load_state_dict(sd)
+        mod = mod.cuda().train()
+        y = mod(x.cuda())
+        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(7)).cuda()
+        y.backward(dy)
+        out.append({k: p.grad.detach().cpu() for k, p in mod.named_parameters()})
+    for k in out[0]:
+        assert rel(out[1][k], out[0][k]) < 1e-5, (k, rel(out[1][k], out[0][k]))

@@ -101,16 +101,18 @@ __device__ __forceinline__ void stem_pix(const float (*wr)[9], const float* win,
 // (G = C / 8 channel groups per pixel).  Software-pipelined over the block's tiles: while tile t is
 // computed from LDS, the image window of tile t+1 and (DY) its dy values are already in flight in
 // registers — one memory latency per tile would otherwise dominate (measured 9 us per 256-pixel tile).
-template <int G, bool DY, class Fn>
+template <int G, bool DY, class Fn, bool ZS = false>
 __device__ __forceinline__ void stem_visit(const float* __restrict__ img, const StemGeo& s, const float (*wr)[9],
                                            float* win, const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld,
-                                           Fn fn) {
+                                           Fn fn, const uint16_t* __restrict__ zst = nullptr) {
+    // ZS: z is read from the stored dense fp16 [M][C] tensor (prefetched like dy) instead of recomputed
     constexpr int PPP = 256 / G, NP = STH * STW / PPP;          // pixels per pass, passes per tile
     constexpr int WI = (SIH * SIW + 255) / 256;                // window elements per thread
     const int pl = threadIdx.x / G, g = threadIdx.x % G;
     const int ntile = stem_tiles(s);
     float wv[WI];
     uint4 dv[DY ? NP : 1];
+    uint4 zv[ZS ? NP : 1];
     auto fetch = [&](int t) {
         const StemTile T = stem_tile(s, t);
         const int ih0 = T.oh0 * s.stride - s.pad, iw0 = T.ow0 * s.stride - s.pad;
@@ -129,6 +131,9 @@ __device__ __forceinline__ void stem_visit(const float* __restrict__ img, const 
                 const int p = q * PPP + pl, r = p / STW, c = p - r * STW;
                 const int oh = min(T.oh0 + r, s.OH - 1), ow = min(T.ow0 + c, s.OW - 1);   // clamped: always in bounds
                 dv[q] = *reinterpret_cast<const uint4*>(dy + int64_t(T.n) * d_bs + int64_t(oh * s.OW + ow) * d_ld + g * 8);
+                if constexpr (ZS)
+                    zv[q] = *reinterpret_cast<const uint4*>(zst + (int64_t(T.n) * s.OH * s.OW + int64_t(oh * s.OW + ow)) * s.C +
+                                                            g * 8);
             }
         }
     };
@@ -142,10 +147,14 @@ __device__ __forceinline__ void stem_visit(const float* __restrict__ img, const 
             const int i = threadIdx.x + k * 256;
             if (i < SIH * SIW) win[i] = wv[k];
         }
-        uint4 cur[DY ? NP : 1];
+        uint4 cur[DY ? NP : 1], zcur[ZS ? NP : 1];
         if constexpr (DY) {
 #pragma unroll
             for (int q = 0; q < NP; ++q) cur[q] = dv[q];
+        }
+        if constexpr (ZS) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) zcur[q] = zv[q];
         }
         __syncthreads();
         if (t + int(gridDim.x) < ntile) fetch(t + gridDim.x);
@@ -155,7 +164,21 @@ __device__ __forceinline__ void stem_visit(const float* __restrict__ img, const 
             const int oh = T.oh0 + r, ow = T.ow0 + c;
             if (oh >= s.OH || ow >= s.OW) continue;
             float patch[9], zf[8], z[8];
-            stem_pix(wr, win, s.stride, r, c, patch, zf, z);
+            if constexpr (ZS) {
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw)
+                        patch[kh * 3 + kw] = win[(r * s.stride + kh) * SIW + c * s.stride + kw];
+                const uint32_t u[4] = {zcur[q].x, zcur[q].y, zcur[q].z, zcur[q].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    z[2 * e] = zf[2 * e] = h2f(uint16_t(u[e] & 0xffff));
+                    z[2 * e + 1] = zf[2 * e + 1] = h2f(uint16_t(u[e] >> 16));
+                }
+            } else {
+                stem_pix(wr, win, s.stride, r, c, patch, zf, z);
+            }
             fn(T.n, oh, ow, patch, zf, z, cur[DY ? q : 0]);
         }
     }
@@ -270,16 +293,22 @@ __global__ void __launch_bounds__(256) stem_bwd_reduce_kernel(const bf16_t* __re
 
 // dz = k1 (g - k2 - xhat k3), rounded to bf16 as the stored path stores it, straight into the
 // weight-gradient partials part[block][co * 9 + t] = sum over the block's pixels of dz[co] * patch[t]
-template <int G>
+template <int G, bool ZS = false>
 __global__ void __launch_bounds__(256) stem_bwd_wgrad_kernel(const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld,
                                                              const float* __restrict__ img, const float* __restrict__ w,
                                                              const float* __restrict__ bnv, const float* __restrict__ coef,
-                                                             float* __restrict__ part, StemGeo s) {
+                                                             float* __restrict__ part, StemGeo s,
+                                                             const uint16_t* __restrict__ zst = nullptr) {
     __shared__ float win[SIH * SIW];
     __shared__ float red[128 * 9];
     const int g = threadIdx.x % G, C = s.C;
     float wr[8][9], sc[8], sf[8], mu[8], rs[8], k1[8], k2[8], k3[8];
-    load_w8(w, g, wr);
+    if constexpr (!ZS) load_w8(w, g, wr);            // (the stored-z form never recomputes z)
+    else
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) wr[r][t] = 0.f;
     load8f(bnv + g * 8, sc);
     load8f(bnv + C + g * 8, sf);
     load8f(bnv + 2 * C + g * 8, mu);
@@ -292,7 +321,7 @@ __global__ void __launch_bounds__(256) stem_bwd_wgrad_kernel(const bf16_t* __res
     for (int r = 0; r < 8; ++r)
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[r][t] = 0.f;
-    stem_visit<G, true>(img, s, wr, win, dy, d_bs, d_ld, [&](int, int, int, const float* patch, const float*, const float* z, uint4 dv) {
+    auto body = [&](int, int, int, const float* patch, const float*, const float* z, uint4 dv) {
         float d[8];
         unpack_bf8(dv, d);
 #pragma unroll
@@ -303,7 +332,8 @@ __global__ void __launch_bounds__(256) stem_bwd_wgrad_kernel(const bf16_t* __res
 #pragma unroll
             for (int t = 0; t < 9; ++t) acc[r][t] += dz * patch[t];
         }
-    });
+    };
+    stem_visit<G, true, decltype(body), ZS>(img, s, wr, win, dy, d_bs, d_ld, body, zst);
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
@@ -368,6 +398,34 @@ extern "C" int ym_stem_stats(const float* img, const float* w_oihw, float* stat_
     const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
     YM_STEM_DISPATCH(cout, stem_stats_kernel, dim3(blocks), 0, as_stream(stream), img, w_oihw, stat_sum, stat_sq, g);
     YM_LAUNCH_CHECK("ym_stem_stats");
+    return YM_OK;
+}
+
+// the stored-z form: BatchNorm-backward apply + weight gradient of the stem in one pass over dy and
+// the stored z (dz never written; replaces ym_bn_bwd_apply + ym_conv_first_wgrad)
+extern "C" int ym_stem_bwd_wgrad_stored(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z,
+                                        const float* img, const float* bnv, const float* coef, float* dw_oihw,
+                                        float* workspace, size_t workspace_bytes, int n, int h, int w, int oh, int ow,
+                                        int cout, int stride, int pad, void* stream) {
+    YM_CHECK_ARG(dy && z && img && bnv && coef && dw_oihw, "ym_stem_bwd_wgrad_stored: null argument");
+    YM_CHECK_ARG(stem_shape_ok(n, h, w, oh, ow, cout, stride) && d_ld % 8 == 0 && d_bs % 8 == 0,
+                 "ym_stem_bwd_wgrad_stored: unsupported shape / unaligned view");
+    YM_CHECK_ARG(workspace && workspace_bytes >= size_t(STEM_WG_BLOCKS) * size_t(cout) * 9 * sizeof(float),
+                 "ym_stem_bwd_wgrad_stored: workspace too small");
+    const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
+    hipStream_t st = as_stream(stream);
+    const bf16_t* d = reinterpret_cast<const bf16_t*>(dy);
+    if (cout == 16)
+        hipLaunchKernelGGL((stem_bwd_wgrad_kernel<2, true>), dim3(STEM_WG_BLOCKS), dim3(256), 0, st, d, d_bs, d_ld, img,
+                           nullptr, bnv, coef, workspace, g, z);
+    else if (cout == 32)
+        hipLaunchKernelGGL((stem_bwd_wgrad_kernel<4, true>), dim3(STEM_WG_BLOCKS), dim3(256), 0, st, d, d_bs, d_ld, img,
+                           nullptr, bnv, coef, workspace, g, z);
+    else
+        hipLaunchKernelGGL((stem_bwd_wgrad_kernel<8, true>), dim3(STEM_WG_BLOCKS), dim3(256), 0, st, d, d_bs, d_ld, img,
+                           nullptr, bnv, coef, workspace, g, z);
+    colsum_launch(workspace, STEM_WG_BLOCKS, cout * 9, int64_t(cout) * 9, dw_oihw, 1, st);
+    YM_LAUNCH_CHECK("ym_stem_bwd_wgrad_stored");
     return YM_OK;
 }
 

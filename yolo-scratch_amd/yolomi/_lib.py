@@ -77,6 +77,7 @@ SIGNATURES = {
     "ym_stem_bwd_reduce": (R, [P, I64, I64, P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_stem_bwd_wgrad_workspace_size": (SZ, [INT]),
     "ym_stem_bwd_wgrad": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_stem_bwd_wgrad_stored": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_conv_first_fwd_bn": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P, P]),
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),

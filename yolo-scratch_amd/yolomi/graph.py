@@ -366,6 +366,12 @@ def stem_recompute_on():
     return os.environ.get("YM_STEM_RECOMPUTE", "0") == "1"
 
 
+def stem_fused_bwd_on():
+    """The stored-z stem backward's BatchNorm apply fused with its weight gradient
+    (ym_stem_bwd_wgrad_stored; YM_STEM_FUSED_BWD=0: ym_bn_bwd_apply + ym_conv_first_wgrad)."""
+    return os.environ.get("YM_STEM_FUSED_BWD", "1") != "0"
+
+
 class StemConvBN(ConvBN):
     """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
 
@@ -433,6 +439,26 @@ class StemConvBN(ConvBN):
 
     def backward(self, plan, st):
         dy = self.y.grad_for_read(st)
+        if not self.recompute and stem_fused_bwd_on() and self.co in (16, 32, 64):
+            # statistics pass + finalize as every Conv block, then the apply and the weight gradient in
+            # ONE pass over dy and the stored z (ym_stem_bwd_wgrad_stored: dz never written / re-read)
+            bn = self.m.bn
+            sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+            Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
+            ws = plan.private_ws(self, lib().ym_stem_bwd_wgrad_workspace_size(self.co))
+            e = self.M * self.co * 2
+
+            def run():
+                call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                     mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+                call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+                     _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
+                     plan.bn_ws.data_ptr(), st)
+                call("ym_stem_bwd_wgrad_stored", dy, self.y.bs, self.y.ld, self.z.data_ptr(), plan.img.data_ptr(),
+                     self.bnv.data_ptr(), self.coef.data_ptr(), plan.gptr(self.m.conv.weight), ws.data_ptr(),
+                     ws.numel() * 4, *self._geo(plan), st)
+            self._timed(plan, "bn", plan._cur_stream, run, 4 * e + 16 * Gb * self.co + 4 * plan.B * self.H * self.W)
+            return
         if not self.recompute:
             self._bn_bwd(plan, st, dy)
             ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
