@@ -30,12 +30,19 @@ class DPContext:
 
 
 def init_from_env(backend: str | None = None) -> DPContext | None:
-    """Initialise the process group when launched by torchrun (WORLD_SIZE > 1)."""
+    """Initialise the process group when launched by torchrun (WORLD_SIZE > 1).
+
+    Rehearsal overrides (a multi-rank run on a one-GPU box; never set for a real DP job):
+    YM_DIST_BACKEND=gloo all-reduces through the host, YM_DIST_DEVICE=0 puts every rank on GPU 0
+    (RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
         return None
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if os.environ.get("YM_DIST_DEVICE") is not None:
+        local = int(os.environ["YM_DIST_DEVICE"])
+    backend = backend or os.environ.get("YM_DIST_BACKEND") or None
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if not dist.is_initialized():
         if backend is None:
