@@ -310,6 +310,19 @@ int ym_bn_bwd_apply_res(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const ui
  * into the view yv.  Backward (gather over the argmax codes, no atomics):
  * out = init_view (bf16, optional) + sum of dy over the windows whose argmax is the pixel, written
  * to dx (dense fp32, optional) and/or the bf16 view dxv (added to it when accumulate). */
+/* SPPF's three chained 5x5 pools in one launch per direction (models/yolo11_modules.py:100-104),
+ * the chain kept in LDS (maps with h*w*cg*13 <= 96 KiB, cg = 8 or 4 channels per block; see
+ * ym_sppf_supported).  fwd: x = fp32 cv1 output (m, c); code = 3 argmax planes (m, c) each;
+ * y1..y3 = the fp16 concat slices (common bs / ld); p_out (optional) = the fp32 pool outputs as 3
+ * planes.  bwd: g1..g3 = the bf16 gradients of the slices (common bs / ld); the routed gradient of
+ * slice 0 written (or accumulated) into dxv, optionally also as fp32 into dx32.  Bit-identical to
+ * three chained ym_maxpool5_f32_fwd / _bwd calls. */
+int ym_sppf_supported(int h, int w, int c);
+int ym_sppf_fwd(const float* x, uint8_t* code, uint16_t* y1, uint16_t* y2, uint16_t* y3, int64_t y_bs, int64_t y_ld,
+                float* p_out, int n, int h, int w, int c, void* stream);
+int ym_sppf_bwd(const uint8_t* code, const uint16_t* g1, const uint16_t* g2, const uint16_t* g3, int64_t g_bs,
+                int64_t g_ld, uint16_t* dxv, int64_t v_bs, int64_t v_ld, int accumulate, float* dx32, int n, int h,
+                int w, int c, void* stream);
 int ym_maxpool5_f32_fwd(const float* x, float* y, uint8_t* code, uint16_t* yv, int64_t y_bs, int64_t y_ld, int n,
                         int h, int w, int c, void* stream);
 int ym_maxpool5_f32_bwd(const uint8_t* code, const float* dy, const uint16_t* init, int64_t i_bs, int64_t i_ld,

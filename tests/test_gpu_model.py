@@ -238,6 +238,57 @@ def test_sppf_pool_chain_exact(H, W, C):
     torch.testing.assert_close(cur_chk.cpu().view(B, H, W, C), xr2.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
 
 
+@pytest.mark.parametrize("H,W,C", [(20, 20, 16), (9, 7, 12), (40, 40, 8)])
+def test_sppf_fused_chain_bit_identical(H, W, C):
+    """ym_sppf_fwd / ym_sppf_bwd (the three pools in one launch, chain in LDS) against three chained
+    ym_maxpool5_f32_fwd / _bwd launches on the same inputs: pool values, argmax codes, fp16 slices,
+    the fp32 routed gradient and the accumulated bf16 slice-0 gradient all bit-identical.
+    Shapes: 8- and 4-channel blocks, odd maps, the m@1280 40x40 map."""
+    from yolomi._lib import call, lib, stream_ptr
+    assert lib().ym_sppf_supported(H, W, C)
+    g = torch.Generator().manual_seed(H * W + C)
+    B = 3
+    M = B * H * W
+    x = (torch.randint(-8, 8, (M, C), generator=g).float() / 4).cuda()    # exact ties, as chained pools make
+    st = stream_ptr()
+    # reference: chained per-pool launches
+    P = torch.zeros(4, M, C, device="cuda")
+    P[0] = x
+    code = torch.zeros(3, M, C, dtype=torch.uint8, device="cuda")
+    ybuf = torch.zeros(B, H, W, 4 * C, dtype=torch.float16, device="cuda")      # concat [s0 | s1 | s2 | s3]
+    bs, ld = H * W * 4 * C, 4 * C
+    sl = lambda t, j: t.data_ptr() + 2 * j * C
+    for j in range(3):
+        call("ym_maxpool5_f32_fwd", P[j].data_ptr(), P[j + 1].data_ptr(), code[j].data_ptr(), sl(ybuf, j + 1), bs, ld,
+             B, H, W, C, st)
+    P2 = torch.zeros(3, M, C, device="cuda")
+    code2 = torch.zeros(3, M, C, dtype=torch.uint8, device="cuda")
+    ybuf2 = torch.zeros_like(ybuf)
+    call("ym_sppf_fwd", x.data_ptr(), code2.data_ptr(), sl(ybuf2, 1), sl(ybuf2, 2), sl(ybuf2, 3), bs, ld,
+         P2.data_ptr(), B, H, W, C, st)
+    torch.cuda.synchronize()
+    assert torch.equal(P[1:], P2) and torch.equal(code, code2) and torch.equal(ybuf, ybuf2)
+    # backward: slice gradients in one bf16 concat gradient buffer, slice 0 accumulated onto a base
+    gbuf = torch.randn(B, H, W, 4 * C, generator=g).bfloat16().cuda()
+    gbuf[..., :C] = 0.25
+    gref = gbuf.clone()
+    cur = gbuf[..., 3 * C:].float().reshape(M, C).contiguous()
+    for j in (2, 1):
+        nxt = torch.empty(M, C, device="cuda")
+        call("ym_maxpool5_f32_bwd", code[j].data_ptr(), cur.data_ptr(), sl(gbuf, j), bs, ld, nxt.data_ptr(), None, 0,
+             0, 0, B, H, W, C, st)
+        cur = nxt
+    dx_ref = torch.empty(M, C, device="cuda")
+    call("ym_maxpool5_f32_bwd", code[0].data_ptr(), cur.data_ptr(), None, 0, 0, dx_ref.data_ptr(), gref.data_ptr(),
+         bs, ld, 1, B, H, W, C, st)
+    dx32 = torch.empty(M, C, device="cuda")
+    call("ym_sppf_bwd", code.data_ptr(), sl(gbuf, 1), sl(gbuf, 2), sl(gbuf, 3), bs, ld, gbuf.data_ptr(), bs, ld, 1,
+         dx32.data_ptr(), B, H, W, C, st)
+    torch.cuda.synchronize()
+    assert torch.equal(dx32, dx_ref)
+    assert torch.equal(gbuf, gref)
+
+
 def _emulated_heads(scale, img):
     from oracle import model as om
     from oracle.precision import hip_storage_rounding

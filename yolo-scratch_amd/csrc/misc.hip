@@ -234,6 +234,135 @@ __global__ void __launch_bounds__(256) maxpool5_lds_bwd_kernel(const uint8_t* __
     }
 }
 
+// SPPF's three chained pools in ONE launch per direction (yolo11_modules.py:100-104): a block owns
+// one image x CG channels of the map and keeps the chain in LDS — pool j+1 reads pool j's result
+// where it was computed, so the fp32 intermediates never go to memory (the forward writes only the
+// three argmax planes and the fp16 concat slices; the backward reads the three bf16 slice gradients
+// and the codes and writes slice 0's).  Same window scans, tie rules and summation order as
+// maxpool5_lds_fwd/bwd_kernel chained three times: bit-identical results.
+template <int CG>
+__global__ void __launch_bounds__(256) sppf_fwd_kernel(const float* __restrict__ x, uint8_t* __restrict__ code,
+                                                       int64_t plane, uint16_t* __restrict__ y1,
+                                                       uint16_t* __restrict__ y2, uint16_t* __restrict__ y3,
+                                                       int64_t y_bs, int64_t y_ld, float* __restrict__ p_out, int H,
+                                                       int W, int C) {
+    extern __shared__ float sm[];
+    const int HW = H * W, E = HW * CG;
+    float* xs = sm;                                            // pool input   [HW][CG]
+    float* ys = sm + E;                                        // pool output
+    float* rm = sm + 2 * E;                                    // row maxima
+    uint8_t* rk = reinterpret_cast<uint8_t*>(sm + 3 * E);      // their kw
+    const int n = blockIdx.y, c0 = blockIdx.x * CG;
+    const float* xb = x + (size_t(n) * HW) * C + c0;
+    for (int e = threadIdx.x; e < E; e += 256) xs[e] = xb[size_t(e / CG) * C + (e % CG)];
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 0; j < 3; ++j) {
+        uint16_t* yv = j == 0 ? y1 : j == 1 ? y2 : y3;
+        for (int e = threadIdx.x; e < E; e += 256) {
+            const int pix = e / CG, c = e % CG, h = pix / W, w = pix - h * W;
+            float mx = 0.f;
+            int k = 0;
+            bool first = true;
+#pragma unroll
+            for (int dw = -2; dw <= 2; ++dw) {
+                const int iw = w + dw;
+                if (iw < 0 || iw >= W) continue;
+                const float v = xs[(h * W + iw) * CG + c];
+                if (first || v > mx || v != v) { mx = v; k = dw + 2; }
+                first = false;
+            }
+            rm[e] = mx;
+            rk[e] = uint8_t(k);
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < E; e += 256) {
+            const int pix = e / CG, c = e % CG, h = pix / W, w = pix - h * W;
+            float mx = 0.f;
+            uint32_t cd = 0;
+            bool first = true;
+#pragma unroll
+            for (int dh = -2; dh <= 2; ++dh) {
+                const int ih = h + dh;
+                if (ih < 0 || ih >= H) continue;
+                const int q = (ih * W + w) * CG + c;
+                const float v = rm[q];
+                if (first || v > mx || v != v) { mx = v; cd = uint32_t((dh + 2) * 5) + rk[q]; }
+                first = false;
+            }
+            const size_t o = (size_t(n) * HW + pix) * C + c0 + c;
+            ys[e] = mx;
+            code[j * plane + o] = uint8_t(cd);
+            if (p_out) p_out[j * plane + o] = mx;
+            yv[n * y_bs + int64_t(pix) * y_ld + c0 + c] = f2h(mx);
+        }
+        __syncthreads();
+        float* t = xs; xs = ys; ys = t;
+    }
+}
+
+template <int CG>
+__global__ void __launch_bounds__(256) sppf_bwd_kernel(const uint8_t* __restrict__ code, int64_t plane,
+                                                       const uint16_t* __restrict__ g1, const uint16_t* __restrict__ g2,
+                                                       const uint16_t* __restrict__ g3, int64_t g_bs, int64_t g_ld,
+                                                       uint16_t* __restrict__ dxv, int64_t v_bs, int64_t v_ld,
+                                                       int accumulate, float* __restrict__ dx32, int H, int W, int C) {
+    extern __shared__ float sm[];
+    const int HW = H * W, E = HW * CG;
+    float* gs = sm;                                            // routed gradient of the current pool output
+    float* ns = sm + E;                                        // the next one
+    uint8_t* ks = reinterpret_cast<uint8_t*>(sm + 2 * E);      // the current pool's codes
+    const int n = blockIdx.y, c0 = blockIdx.x * CG;
+    const size_t base = (size_t(n) * HW) * C + c0;
+    for (int e = threadIdx.x; e < E; e += 256) {
+        const int pix = e / CG, c = e % CG;
+        gs[e] = bf2f(bf16_t(g3[n * g_bs + int64_t(pix) * g_ld + c0 + c]));
+        ks[e] = code[2 * plane + base + size_t(pix) * C + c];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 2; j >= 0; --j) {
+        const uint16_t* init = j == 2 ? g2 : j == 1 ? g1 : nullptr;
+        for (int e = threadIdx.x; e < E; e += 256) {
+            const int pix = e / CG, c = e % CG, h = pix / W, w = pix - h * W;
+            float acc = 0.f;
+            for (int qh = h - 2; qh <= h + 2; ++qh) {
+                if (qh < 0 || qh >= H) continue;
+#pragma unroll
+                for (int dq = -2; dq <= 2; ++dq) {
+                    const int qw = w + dq;
+                    if (qw < 0 || qw >= W) continue;
+                    const int q = (qh * W + qw) * CG + c;
+                    if (ks[q] == uint8_t((h - qh + 2) * 5 + (w - qw + 2))) acc += gs[q];
+                }
+            }
+            if (init) acc += bf2f(bf16_t(init[n * g_bs + int64_t(pix) * g_ld + c0 + c]));
+            if (j > 0) {
+                ns[e] = acc;
+            } else {
+                if (dx32) dx32[base + size_t(pix) * C + c] = acc;
+                uint16_t* p = dxv + n * v_bs + int64_t(pix) * v_ld + c0 + c;
+                if (accumulate) acc += bf2f(bf16_t(*p));
+                *p = f2bf(acc);
+            }
+        }
+        __syncthreads();
+        if (j > 0) {
+            float* t = gs; gs = ns; ns = t;
+            for (int e = threadIdx.x; e < E; e += 256) ks[e] = code[(j - 1) * plane + base + size_t(e / CG) * C + (e % CG)];
+            __syncthreads();
+        }
+    }
+}
+
+// channels per block of the fused chain (0: the map does not fit, use the per-pool launches)
+int sppf_cg(int h, int w, int c) {
+    const int64_t hw = int64_t(h) * w;
+    if (c % 8 == 0 && hw * 8 * 13 <= 96 * 1024) return 8;
+    if (c % 4 == 0 && hw * 4 * 13 <= 96 * 1024) return 4;
+    return 0;
+}
+
 // channels per block of the LDS forms (0: the map does not fit, use the direct kernels)
 int pool_cg(int h, int w, int c) {
     const int64_t hw = int64_t(h) * w;
@@ -470,6 +599,47 @@ extern "C" int ym_maxpool5_f32_bwd(const uint8_t* code, const float* dy, const u
         hipLaunchKernelGGL(maxpool5_f32_bwd_kernel, dim3(unsigned((t + 255) / 256)), dim3(256), 0, as_stream(stream),
                            code, dy, init, i_bs, i_ld, dx, dxv, v_bs, v_ld, accumulate, n, h, w, c);
     YM_LAUNCH_CHECK("ym_maxpool5_f32_bwd");
+    return YM_OK;
+}
+
+extern "C" int ym_sppf_supported(int h, int w, int c) { return sppf_cg(h, w, c) != 0; }
+
+extern "C" int ym_sppf_fwd(const float* x, uint8_t* code, uint16_t* y1, uint16_t* y2, uint16_t* y3, int64_t y_bs,
+                           int64_t y_ld, float* p_out, int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(x && code && y1 && y2 && y3, "ym_sppf_fwd: null argument");
+    const int cg = sppf_cg(h, w, c);
+    YM_CHECK_ARG(cg != 0, "ym_sppf_fwd: map %dx%d x %d channels does not fit the fused kernel", h, w, c);
+    YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_sppf_fwd: too large");
+    if (n == 0) return YM_OK;
+    const int64_t plane = int64_t(n) * h * w * c;
+    const size_t lds = size_t(h) * w * cg * 13;
+    if (cg == 8)
+        hipLaunchKernelGGL(sppf_fwd_kernel<8>, dim3(unsigned(c / 8), unsigned(n)), dim3(256), lds, as_stream(stream), x,
+                           code, plane, y1, y2, y3, y_bs, y_ld, p_out, h, w, c);
+    else
+        hipLaunchKernelGGL(sppf_fwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream), x,
+                           code, plane, y1, y2, y3, y_bs, y_ld, p_out, h, w, c);
+    YM_LAUNCH_CHECK("ym_sppf_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_sppf_bwd(const uint8_t* code, const uint16_t* g1, const uint16_t* g2, const uint16_t* g3,
+                           int64_t g_bs, int64_t g_ld, uint16_t* dxv, int64_t v_bs, int64_t v_ld, int accumulate,
+                           float* dx32, int n, int h, int w, int c, void* stream) {
+    YM_CHECK_ARG(code && g1 && g2 && g3 && dxv, "ym_sppf_bwd: null argument");
+    const int cg = sppf_cg(h, w, c);
+    YM_CHECK_ARG(cg != 0, "ym_sppf_bwd: map %dx%d x %d channels does not fit the fused kernel", h, w, c);
+    YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_sppf_bwd: too large");
+    if (n == 0) return YM_OK;
+    const int64_t plane = int64_t(n) * h * w * c;
+    const size_t lds = size_t(h) * w * cg * 9;
+    if (cg == 8)
+        hipLaunchKernelGGL(sppf_bwd_kernel<8>, dim3(unsigned(c / 8), unsigned(n)), dim3(256), lds, as_stream(stream),
+                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
+    else
+        hipLaunchKernelGGL(sppf_bwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream),
+                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
+    YM_LAUNCH_CHECK("ym_sppf_bwd");
     return YM_OK;
 }
 

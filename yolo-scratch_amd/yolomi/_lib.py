@@ -97,6 +97,9 @@ SIGNATURES = {
     "ym_bn_bwd_reduce_finalize": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply_res": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, I64, I64, INT, P]),
+    "ym_sppf_supported": (R, [INT, INT, INT]),
+    "ym_sppf_fwd": (R, [P, P, P, P, P, I64, I64, P, INT, INT, INT, INT, P]),
+    "ym_sppf_bwd": (R, [P, P, P, P, I64, I64, P, I64, I64, INT, P, INT, INT, INT, INT, P]),
     "ym_maxpool5_f32_fwd": (R, [P, P, P, P, I64, I64, INT, INT, INT, INT, P]),
     "ym_maxpool5_f32_bwd": (R, [P, P, P, I64, I64, P, P, I64, I64, INT, INT, INT, INT, INT, P]),
     "ym_upsample2_fwd": (R, [P, I64, I64, P, I64, I64, INT, INT, INT, INT, P]),

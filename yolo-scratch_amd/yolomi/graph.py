@@ -593,13 +593,33 @@ class SPPFPools:
         self.G = torch.empty(2, self.M, self.C, dtype=F32, device=plan.dev)   # grad ping-pong
         cv1_op.out32 = self.P[0]
 
+    def fused(self, plan):
+        """The whole chain in one launch per direction (ym_sppf_fwd / _bwd, chain kept in LDS) when
+        the map fits; YM_SPPF_FUSED=0: one launch per pool."""
+        sl = self.slices
+        return (os.environ.get("YM_SPPF_FUSED", "1") != "0" and lib().ym_sppf_supported(self.H, self.W, self.C)
+                and sl[1].bs == sl[2].bs == sl[3].bs and sl[1].ld == sl[2].ld == sl[3].ld)
+
     def forward(self, plan, st):
+        if self.fused(plan):
+            y1, y2, y3 = self.slices[1:]
+            call("ym_sppf_fwd", self.P[0].data_ptr(), self.code.data_ptr(), y1.ptr(), y2.ptr(), y3.ptr(), y1.bs, y1.ld,
+                 None, plan.B, self.H, self.W, self.C, st)
+            return
         for j in range(3):
             y = self.slices[j + 1]
             call("ym_maxpool5_f32_fwd", self.P[j].data_ptr(), self.P[j + 1].data_ptr(), self.code[j].data_ptr(),
                  y.ptr(), y.bs, y.ld, plan.B, self.H, self.W, self.C, st)
 
     def backward(self, plan, st):
+        if self.fused(plan):
+            s0, s1, s2, s3 = self.slices
+            g1, g2, g3 = s1.grad_for_read(st), s2.grad_for_read(st), s3.grad_for_read(st)
+            acc = s0.grad_for_write(st)
+            call("ym_sppf_bwd", self.code.data_ptr(), g1, g2, g3, s1.bs, s1.ld, s0.gptr(), s0.bs, s0.ld, acc, None,
+                 plan.B, self.H, self.W, self.C, st)
+            s0.mark()
+            return
         HW = self.H * self.W
         cur = self.G[0]
         s3 = self.slices[3]
