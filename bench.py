@@ -327,7 +327,7 @@ def main():
         except Exception as e:  # pragma: no cover
             out["cpu_baseline"] = {"value": None, "error": str(e)[:200]}
     if rank == 0:
-        log(f"loss {float(loss):.4f}  {value:.1f} img/s  {ms_step:.1f} ms/step (host enqueue {host_ms:.1f} ms)  "
+        log(f"loss {float(loss.detach()):.4f}  {value:.1f} img/s  {ms_step:.1f} ms/step (host enqueue {host_ms:.1f} ms)  "
             f"dominant kernel {kern_ms:.3f} ms ({dom_tf:.0f} TFLOP/s)")
         print(json.dumps(out), flush=True)
     ydist.shutdown()

@@ -41,6 +41,7 @@ def conv_kind(name):
     if n.startswith(("wgrad3_kernel", "wgrad1_kernel", "wgrad_generic_kernel", "wgrad_reduce_kernel")):
         return "wgrad"
     if n.startswith(("bn_apply_kernel", "bn_bwd_reduce_kernel", "bn_bwd_apply_kernel", "bn_finalize_fused_kernel",
+                     "stem_bwd_wgrad_kernel",
                      "partials_reduce_kernel", "bn_finalize_kernel", "bn_bwd_finalize_kernel")):
         return "bn"
     return None
