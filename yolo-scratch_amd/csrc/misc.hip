@@ -5,6 +5,8 @@
 // Activation buffers are fp16, gradient buffers bf16 (see yolomi/graph.py).
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "reduce.h"
 
@@ -355,12 +357,30 @@ __global__ void __launch_bounds__(256) sppf_bwd_kernel(const uint8_t* __restrict
     }
 }
 
-// channels per block of the fused chain (0: the map does not fit, use the per-pool launches)
+// channels per block of the fused chain (0: the map does not fit, use the per-pool launches);
+// YM_SPPF_CG=8 / 4 prefers that width (A/B runs)
 int sppf_cg(int h, int w, int c) {
+    static const int pref = [] {
+        const char* e = getenv("YM_SPPF_CG");
+        return e ? atoi(e) : 8;
+    }();
     const int64_t hw = int64_t(h) * w;
-    if (c % 8 == 0 && hw * 8 * 13 <= 96 * 1024) return 8;
+    if (pref == 8 && c % 8 == 0 && hw * 8 * 13 <= 96 * 1024) return 8;
     if (c % 4 == 0 && hw * 4 * 13 <= 96 * 1024) return 4;
     return 0;
+}
+// the backward's width: narrower blocks measured faster (s@640 64x20x20x256: 232 / 154 us at 8 / 4
+// channels; its three dependent gather levels per block want more blocks per CU); YM_SPPF_CGB A/B
+int sppf_cg_bwd(int h, int w, int c) {
+    static const int pref = [] {
+        const char* e = getenv("YM_SPPF_CGB");
+        return e ? atoi(e) : 4;
+    }();
+    if (!sppf_cg(h, w, c)) return 0;
+    const int64_t hw = int64_t(h) * w;
+    if (pref <= 2 && c % 2 == 0 && hw * 2 * 9 <= 96 * 1024) return 2;
+    if (pref <= 4 && c % 4 == 0 && hw * 4 * 9 <= 96 * 1024) return 4;
+    return c % 8 == 0 && hw * 8 * 9 <= 96 * 1024 ? 8 : 0;
 }
 
 // channels per block of the LDS forms (0: the map does not fit, use the direct kernels)
@@ -627,7 +647,7 @@ extern "C" int ym_sppf_bwd(const uint8_t* code, const uint16_t* g1, const uint16
                            int64_t g_bs, int64_t g_ld, uint16_t* dxv, int64_t v_bs, int64_t v_ld, int accumulate,
                            float* dx32, int n, int h, int w, int c, void* stream) {
     YM_CHECK_ARG(code && g1 && g2 && g3 && dxv, "ym_sppf_bwd: null argument");
-    const int cg = sppf_cg(h, w, c);
+    const int cg = sppf_cg_bwd(h, w, c);
     YM_CHECK_ARG(cg != 0, "ym_sppf_bwd: map %dx%d x %d channels does not fit the fused kernel", h, w, c);
     YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_sppf_bwd: too large");
     if (n == 0) return YM_OK;
@@ -636,8 +656,11 @@ extern "C" int ym_sppf_bwd(const uint8_t* code, const uint16_t* g1, const uint16
     if (cg == 8)
         hipLaunchKernelGGL(sppf_bwd_kernel<8>, dim3(unsigned(c / 8), unsigned(n)), dim3(256), lds, as_stream(stream),
                            code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
-    else
+    else if (cg == 4)
         hipLaunchKernelGGL(sppf_bwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream),
+                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
+    else
+        hipLaunchKernelGGL(sppf_bwd_kernel<2>, dim3(unsigned(c / 2), unsigned(n)), dim3(256), lds, as_stream(stream),
                            code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
     YM_LAUNCH_CHECK("ym_sppf_bwd");
     return YM_OK;
