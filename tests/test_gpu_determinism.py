@@ -65,3 +65,41 @@ def test_train_step_bit_reproducible():
         assert torch.equal(ref[1], other[1]) and torch.equal(ref[2], other[2])
         for i, (a, c) in enumerate(zip(ref[3], other[3])):
             assert torch.equal(a, c), f"parameter {i}: max |diff| {float((a - c).abs().max())}"
+
+
+def test_eval_graph_replay_matches_eager(monkeypatch):
+    """YM_EVAL_GRAPH=1 (opt-in HIP-graph replay of the eval forward): eager first call,
+    capture on the second, replays after — all bit-identical to eager; an in-place weight update
+    (optimizer step) is seen by the replay; new storage behind a parameter drops the graph (address key)."""
+    import yaml
+    from pathlib import Path
+    from models import build_yolo11
+    root = Path(__file__).resolve().parents[1] / "yolo-scratch_amd"
+    cfg = yaml.safe_load((root / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = "n"
+    torch.manual_seed(3)
+    m = build_yolo11(cfg, ch=1, nc=5).cuda().eval()
+    img = torch.rand(2, 1, 256, 256, generator=torch.Generator().manual_seed(4)).cuda()
+
+    def run():
+        with torch.no_grad():
+            y, _ = m(img)
+        return y.clone()
+    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
+    ref = run()
+    monkeypatch.setenv("YM_EVAL_GRAPH", "1")
+    outs = [run() for _ in range(3)]                  # eager, capture, replay
+    assert all(torch.equal(o, ref) for o in outs)
+    w = m.model[1].conv.weight
+    with torch.no_grad():
+        w.mul_(1.5)                                   # in place: same address
+    rep = run()
+    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
+    ref2 = run()
+    assert torch.equal(rep, ref2) and not torch.equal(rep, ref)
+    monkeypatch.setenv("YM_EVAL_GRAPH", "1")
+    w.data = w.detach().clone() * 0.5                # new storage behind the same Parameter
+    rep3 = run()
+    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
+    ref3 = run()
+    assert torch.equal(rep3, ref3) and not torch.equal(rep3, ref2)

@@ -452,12 +452,9 @@ const Variant kVariants[] = {
 
 // stride-2 data gradients as 2 row-parity classes over column pairs (default) or 4 parity classes
 // (YM_DIRECT_S2PAIR=0, A/B runs)
-bool s2_pairs() {
-    static const bool v = [] {
-        const char* e = getenv("YM_DIRECT_S2PAIR");
-        return !(e && e[0] == '0');
-    }();
-    return v;
+bool s2_pairs() {        // read per plan (tests run both forms in one process)
+    const char* e = getenv("YM_DIRECT_S2PAIR");
+    return !(e && e[0] == '0');
 }
 
 int direct_mode() {

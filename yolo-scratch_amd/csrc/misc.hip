@@ -357,31 +357,17 @@ __global__ void __launch_bounds__(256) sppf_bwd_kernel(const uint8_t* __restrict
     }
 }
 
-// channels per block of the fused chain (0: the map does not fit, use the per-pool launches);
-// YM_SPPF_CG=8 / 4 prefers that width (A/B runs)
+// channels per block of the fused chain (0: the map does not fit, use the per-pool launches): the
+// forward on 8-channel blocks where they fit, the backward on 4-channel blocks (measured at s@640
+// 64x20x20x256: 232 / 154 us on 8 / 4 channels — its three dependent gather levels per block want
+// more blocks per CU; 2-channel blocks 175 us)
 int sppf_cg(int h, int w, int c) {
-    static const int pref = [] {
-        const char* e = getenv("YM_SPPF_CG");
-        return e ? atoi(e) : 8;
-    }();
     const int64_t hw = int64_t(h) * w;
-    if (pref == 8 && c % 8 == 0 && hw * 8 * 13 <= 96 * 1024) return 8;
+    if (c % 8 == 0 && hw * 8 * 13 <= 96 * 1024) return 8;
     if (c % 4 == 0 && hw * 4 * 13 <= 96 * 1024) return 4;
     return 0;
 }
-// the backward's width: narrower blocks measured faster (s@640 64x20x20x256: 232 / 154 us at 8 / 4
-// channels; its three dependent gather levels per block want more blocks per CU); YM_SPPF_CGB A/B
-int sppf_cg_bwd(int h, int w, int c) {
-    static const int pref = [] {
-        const char* e = getenv("YM_SPPF_CGB");
-        return e ? atoi(e) : 4;
-    }();
-    if (!sppf_cg(h, w, c)) return 0;
-    const int64_t hw = int64_t(h) * w;
-    if (pref <= 2 && c % 2 == 0 && hw * 2 * 9 <= 96 * 1024) return 2;
-    if (pref <= 4 && c % 4 == 0 && hw * 4 * 9 <= 96 * 1024) return 4;
-    return c % 8 == 0 && hw * 8 * 9 <= 96 * 1024 ? 8 : 0;
-}
+int sppf_cg_bwd(int h, int w, int c) { return sppf_cg(h, w, c) ? 4 : 0; }
 
 // channels per block of the LDS forms (0: the map does not fit, use the direct kernels)
 int pool_cg(int h, int w, int c) {
@@ -653,15 +639,8 @@ extern "C" int ym_sppf_bwd(const uint8_t* code, const uint16_t* g1, const uint16
     if (n == 0) return YM_OK;
     const int64_t plane = int64_t(n) * h * w * c;
     const size_t lds = size_t(h) * w * cg * 9;
-    if (cg == 8)
-        hipLaunchKernelGGL(sppf_bwd_kernel<8>, dim3(unsigned(c / 8), unsigned(n)), dim3(256), lds, as_stream(stream),
-                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
-    else if (cg == 4)
-        hipLaunchKernelGGL(sppf_bwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream),
-                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
-    else
-        hipLaunchKernelGGL(sppf_bwd_kernel<2>, dim3(unsigned(c / 2), unsigned(n)), dim3(256), lds, as_stream(stream),
-                           code, plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
+    hipLaunchKernelGGL(sppf_bwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream), code,
+                       plane, g1, g2, g3, g_bs, g_ld, dxv, v_bs, v_ld, accumulate, dx32, h, w, c);
     YM_LAUNCH_CHECK("ym_sppf_bwd");
     return YM_OK;
 }

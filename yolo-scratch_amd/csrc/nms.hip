@@ -775,10 +775,8 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
         hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn), unsigned(Wn), unsigned(B)), dim3(64), 0, st, Nalloc, Wn,
                            iou_thr, w);
         static const int stamps = getenv("YM_NMS_STAMPS") != nullptr;
-        static const int old_scan = [] {         // YM_NMS_SCAN=0: the whole-triangle workgroup scan (A/B)
-            const char* e = getenv("YM_NMS_SCAN");
-            return e && e[0] == '0';
-        }();
+        const char* se = getenv("YM_NMS_SCAN");    // YM_NMS_SCAN=0: the whole-triangle workgroup scan (A/B,
+        const bool old_scan = se && se[0] == '0';   // read per launch so tests can compare the two)
         if (old_scan || stamps)
             hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), 0, st, Nalloc, KP, Wn, img_size, w,
                                out_count, out_boxes, out_scores, out_labels, out_index, stamps);
