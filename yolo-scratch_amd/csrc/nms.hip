@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "tile.h"
 
 namespace ym {
 namespace {
@@ -590,16 +591,31 @@ __global__ void __launch_bounds__(256) nms_scan_kernel(int64_t N, int64_t KP, in
 // removed bits come from two places:
 //  * NEAR rows (the previous group of 4 chunks and the earlier chunks of this group): the words
 //    D(c', c) = column c, rows 64c'..64c'+63 are loaded one group AHEAD (they do not depend on any
-//    decision; coalesced 512-B wave loads) and OR-ed under the kept bits of chunk c';
+//    decision; coalesced 512-B wave loads) and read under the kept bits of chunk c';
 //  * FAR rows (two or more groups back): each lane accumulates, for the column blocks it owns
 //    (cb = lane + 64k), the words of every kept row; a group's kept rows are gathered at the start
-//    of the group after next (the loads fly during a whole group of chunk work).
+//    of the next group and joined at the start of the one after (the loads fly during a group).
 // The per-chunk work is then one wave OR, the fixpoint of the chunk's 64x64 diagonal block and the
 // keep update: no workgroup barrier, and ~(kept x Wn + 26 x 64 x groups) words read instead of the
 // triangle.  Same decisions as nms_scan_kernel (a box is kept iff no earlier kept box has
 // IoU > thr with it): the removed bits of chunk c are the OR over ALL kept rows j < 64c of
 // mask[j][c], split into near and far.
 constexpr int SCAN_WL = (BM_MAX_WN + 63) / 64;      // column-block words per lane (far bits)
+
+// OR over the 64 lanes by DPP (row prefix-ORs, then row broadcasts 15 / 31; the total lands in lane
+// 63): a dozen VALU steps instead of a chain of 12 cross-lane permutes
+__device__ __forceinline__ uint32_t wave_or32_dpp(uint32_t v) {
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false));   // row_shr:1
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false));   // row_shr:2
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false));   // row_shr:4
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false));   // row_shr:8
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v |= uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+__device__ __forceinline__ uint64_t wave_or64_dpp(uint64_t v) {
+    return (uint64_t(wave_or32_dpp(uint32_t(v >> 32))) << 32) | wave_or32_dpp(uint32_t(v));
+}
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), l))) << 32) |
@@ -612,8 +628,19 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
                                                            float* __restrict__ out_boxes,
                                                            float* __restrict__ out_scores,
                                                            int64_t* __restrict__ out_labels,
-                                                           int64_t* __restrict__ out_index) {
+                                                           int64_t* __restrict__ out_index, int stamps) {
     __shared__ int rows_sh[256];
+    // diagnostic segment cycles (YM_NMS_STAMPS, image 0): [0] group start (prefetch + gather issue),
+    // [1] chunk decisions, [2] group end (far OR + prefetch rotation), [3] output epilogue
+    const bool st0 = stamps && blockIdx.x == 0;
+    unsigned long long tsum[4] = {0, 0, 0, 0}, tprev = st0 ? stamp_now() : 0;
+    auto stamp = [&](int seg) {
+        if (st0) {
+            const unsigned long long t = stamp_now();
+            tsum[seg] += t - tprev;
+            tprev = t;
+        }
+    };
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int K = w.kcount[b];
@@ -625,35 +652,64 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
     const int nch = (K + 63) / 64;
     const int ngr = (nch + 3) / 4;
     const uint64_t* mcol = w.mask + int64_t(b) * Wn * N;     // column cb: mcol + cb * N, row-indexed
+    // raw buffer loads over this image's mask: 32-bit byte offsets, and every guarded-off load reads 0
+    // through an out-of-range offset instead of a branch (one wave runs alone per image: its
+    // instruction count is the kernel's time)
+    const __amdgpu_buffer_rsrc_t mres = make_rsrc(mcol, int64_t(Wn) * N * 8);
+    auto ld8 = [&](uint32_t off) -> uint64_t {
+        const uint2 v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(mres, off, 0, 0));
+        return (uint64_t(v.y) << 32) | v.x;
+    };
 
     uint64_t far[SCAN_WL];
 #pragma unroll
     for (int k = 0; k < SCAN_WL; ++k) far[k] = 0;
     // D(c', c) for the 4 chunks q of a group: slot s <-> c' = 4g - 4 + s (s <= 4 + q)
-    uint64_t dcur[4][8], dnx[4][8], dnx2[4][8];
+    uint64_t dcur[4][8], dnx[4][8];
     auto load_group = [&](int g, uint64_t (&d)[4][8]) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q) {
+            const int c = 4 * g + q;
+            const uint32_t col = c < nch ? uint32_t(c * int(N) + lane) * 8u : OOB;
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                const int c = 4 * g + q, cp = 4 * g - 4 + s;
-                if (s <= 4 + q && c < nch && cp >= 0) d[q][s] = mcol[int64_t(c) * N + 64 * cp + lane];
-                else d[q][s] = 0;
+                if (s > 4 + q) {
+                    d[q][s] = 0;
+                    continue;
+                }
+                const int cp = 4 * g - 4 + s;
+                d[q][s] = ld8(col == OOB || cp < 0 ? OOB : col + uint32_t(cp) * 512u);
             }
+        }
     };
     uint64_t kprev[4] = {0, 0, 0, 0};                 // kept bits of the previous group's chunks
     uint64_t pend[SCAN_RB][SCAN_WL];                   // far words of the gathered rows, in flight
-    int npend = 0, pend_g = -1;                        // rows in flight, and the group they belong to
+#pragma unroll
+    for (int r = 0; r < SCAN_RB; ++r)
+#pragma unroll
+        for (int k = 0; k < SCAN_WL; ++k) pend[r][k] = 0;
     int nkept = 0;
     load_group(0, dcur);
-    if (1 < ngr) load_group(1, dnx);
     for (int g = 0; g < ngr; ++g) {
-        if (g + 2 < ngr) load_group(g + 2, dnx2);      // two groups ahead: a group's work < one load latency
-        // kept rows of group g-1 -> far words of the columns beyond the next group's near window
-        // (cb >= 4(g+1)); gathered now, OR-ed into far at the end of this group
-        npend = 0;
+        // Everything loaded at the previous group's start (this group's D blocks, the far words of
+        // group g-2's kept rows) has had a whole group of decisions to arrive: wait for it HERE, once,
+        // explicitly.  (Left to the compiler, the loop-carried loads got conservative vmcnt waits
+        // inside the chunk loop that also waited for the loads issued at THIS group's start.)
+        __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0), expcnt / lgkmcnt untouched
+#pragma unroll
+        for (int r = 0; r < SCAN_RB; ++r)
+#pragma unroll
+            for (int k = 0; k < SCAN_WL; ++k) far[k] |= pend[r][k];
+        if (g >= 1)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) dcur[q][s] = dnx[q][s];
+        // next group's D blocks, and the far words (columns cb >= 4(g+1), beyond group g's near window)
+        // of group g-1's kept rows: in flight during this group, used from the next group on
+        if (g + 1 < ngr) load_group(g + 1, dnx);
+        int nr = 0;
         if (g >= 1) {
-            int nr = 0;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint64_t kb = kprev[q];
@@ -662,42 +718,37 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
                 nr += __popcll(kb);
             }
             __builtin_amdgcn_wave_barrier();
-            const int cb_lo = 4 * (g + 1);
-            auto row_words = [&](int j, uint64_t* dst) {
-#pragma unroll
-                for (int k = 0; k < SCAN_WL; ++k) {
-                    const int cb = lane + 64 * k;
-                    dst[k] = (cb >= cb_lo && cb < Wn) ? mcol[int64_t(cb) * N + j] : 0;
-                }
-            };
-            npend = min(nr, SCAN_RB);
-#pragma unroll
-            for (int r = 0; r < SCAN_RB; ++r) {
-                if (r < npend) row_words(rows_sh[r], pend[r]);
-                else
-#pragma unroll
-                    for (int k = 0; k < SCAN_WL; ++k) pend[r][k] = 0;
-            }
-            for (int r = SCAN_RB; r < nr; ++r) {       // more than SCAN_RB kept rows: synchronously
-                uint64_t t[SCAN_WL];
-                row_words(rows_sh[r], t);
-#pragma unroll
-                for (int k = 0; k < SCAN_WL; ++k) far[k] |= t[k];
-            }
-            pend_g = g;
         }
+        const int cb_lo = 4 * (g + 1);
+        auto row_words = [&](int j, uint64_t* dst) {
+#pragma unroll
+            for (int k = 0; k < SCAN_WL; ++k) {
+                const int cb = lane + 64 * k;
+                dst[k] = ld8(j >= 0 && cb >= cb_lo && cb < Wn ? uint32_t(cb * int(N) + j) * 8u : OOB);
+            }
+        };
+        const int npend = stamps == 2 ? 0 : min(nr, SCAN_RB);   // stamps 2: timing ablation, no far gather
+#pragma unroll
+        for (int r = 0; r < SCAN_RB; ++r) row_words(r < npend ? rows_sh[r] : -1, pend[r]);
+        for (int r = SCAN_RB; r < (stamps == 2 ? 0 : nr); ++r) {   // > SCAN_RB kept rows: synchronously
+            uint64_t t[SCAN_WL];
+            row_words(rows_sh[r], t);
+#pragma unroll
+            for (int k = 0; k < SCAN_WL; ++k) far[k] |= t[k];
+        }
+        stamp(0);
         uint64_t kcur[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int c = 4 * g + q;
             if (c >= nch) break;
-            // near rows: previous group (slots 0..3) and this group's earlier chunks (slots 4..4+q-1);
-            // one lane read per KEPT row (a handful per window) instead of a wave-wide OR
-            uint64_t near = 0;
+            // near rows: previous group (slots 0..3) and this group's earlier chunks (slots 4..4+q-1):
+            // each lane ORs the words of its kept rows, then one DPP OR over the wave
+            uint64_t nl = 0;
 #pragma unroll
             for (int s = 0; s < 4 + q; ++s)
-                for (uint64_t kb = s < 4 ? kprev[s] : kcur[s - 4]; kb; kb &= kb - 1)
-                    near |= readlane64(dcur[q][s], __builtin_ctzll(kb));
+                if ((((s < 4 ? kprev[s] : kcur[s - 4]) >> lane) & 1)) nl |= dcur[q][s];
+            const uint64_t near = wave_or64_dpp(nl);
             // far rows: column c's word lives in lane c & 63, slot c >> 6
             const int kw = c >> 6;
             uint64_t fw = far[0];
@@ -720,22 +771,10 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
             nkept += __popcll(alive);
             kcur[q] = alive;
         }
-        // rows gathered at the start of this group join the far words (first use: group g+2)
-        if (pend_g == g)
-#pragma unroll
-            for (int r = 0; r < SCAN_RB; ++r)
-#pragma unroll
-                for (int k = 0; k < SCAN_WL; ++k) far[k] |= pend[r][k];
+        stamp(1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) kprev[q] = kcur[q];
-        if (g + 1 < ngr)
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int s = 0; s < 8; ++s) {
-                    dcur[q][s] = dnx[q][s];
-                    dnx[q][s] = dnx2[q][s];
-                }
+        stamp(2);
     }
     __syncthreads();                                 // this wave's out_index stores are visible to its loads
     // outputs in kept order (sorted position -> filtered index -> row)
@@ -754,6 +793,11 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
         out_index[base + k] = f;
     }
     if (lane == 0) out_count[b] = nkept;
+    if (st0) {
+        stamp(3);
+        if (lane == 0)
+            for (int k = 0; k < 4; ++k) g_nms_stamps[k] = tsum[k];
+    }
 }
 
 int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int clamp_norm, Ws w,
@@ -774,15 +818,18 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
         hipLaunchKernelGGL(nms_rank_scatter_kernel, dim3(nt, unsigned(B)), dim3(256), 0, st, Nalloc, KP, w);
         hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn), unsigned(Wn), unsigned(B)), dim3(64), 0, st, Nalloc, Wn,
                            iou_thr, w);
-        static const int stamps = getenv("YM_NMS_STAMPS") != nullptr;
+        static const int stamps = [] {           // diagnostics; 2 = timing ablation (wrong results)
+            const char* e = getenv("YM_NMS_STAMPS");
+            return e ? (e[0] == '2' ? 2 : 1) : 0;
+        }();
         const char* se = getenv("YM_NMS_SCAN");    // YM_NMS_SCAN=0: the whole-triangle workgroup scan (A/B,
         const bool old_scan = se && se[0] == '0';   // read per launch so tests can compare the two)
-        if (old_scan || stamps)
+        if (old_scan)
             hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), 0, st, Nalloc, KP, Wn, img_size, w,
                                out_count, out_boxes, out_scores, out_labels, out_index, stamps);
         else
             hipLaunchKernelGGL(nms_scan_wave_kernel, dim3(unsigned(B)), dim3(64), 0, st, Nalloc, KP, Wn, img_size, w,
-                               out_count, out_boxes, out_scores, out_labels, out_index);
+                               out_count, out_boxes, out_scores, out_labels, out_index, stamps);
         YM_LAUNCH_CHECK("nms bitmask path");
         return YM_OK;
     }
