@@ -420,12 +420,18 @@ __global__ void nms_rank_scatter_kernel(int64_t N, int64_t KP, Ws w) {
 
 // maskT[b][cb][i] bit j-64cb = (j > i) && !(IoU(i, j) <= thr) for sorted positions i, j < K; only
 // cb >= i/64 is written (the scan reads the upper triangle).  Block = 64 rows of one row block.
+// Grid: x = the upper triangle's Wn (Wn + 1) / 2 (row block, column block) pairs, t = cb (cb + 1) / 2 + rb
+// (half the blocks of a square grid, whose lower half only returned), z = image.
 __global__ void __launch_bounds__(64) nms_mask_kernel(int64_t N, int Wn, float iou_thr, Ws w) {
     __shared__ float4 cols[64];
-    const int cb = blockIdx.x, rb = blockIdx.y;
+    const int tri = blockIdx.x;
+    int cb = int((sqrtf(8.0f * float(tri) + 1.0f) - 1.0f) * 0.5f);
+    while (cb * (cb + 1) / 2 > tri) --cb;
+    while ((cb + 1) * (cb + 2) / 2 <= tri) ++cb;
+    const int rb = tri - cb * (cb + 1) / 2;
     const int64_t b = blockIdx.z;
     const int K = w.kcount[b];
-    if (cb < rb || rb * 64 >= K) return;
+    if (rb * 64 >= K || cb * 64 >= K) return;
     const int t = threadIdx.x;
     const int64_t base = b * N;
     const int j0 = cb * 64;
@@ -816,8 +822,8 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
         const unsigned nt = unsigned((Nalloc + 255) / 256);
         hipLaunchKernelGGL(nms_rank_kernel, dim3(nt, nt, unsigned(B)), dim3(256), 0, st, Nalloc, w);
         hipLaunchKernelGGL(nms_rank_scatter_kernel, dim3(nt, unsigned(B)), dim3(256), 0, st, Nalloc, KP, w);
-        hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn), unsigned(Wn), unsigned(B)), dim3(64), 0, st, Nalloc, Wn,
-                           iou_thr, w);
+        hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn * (Wn + 1) / 2), 1, unsigned(B)), dim3(64), 0, st, Nalloc,
+                           Wn, iou_thr, w);
         static const int stamps = [] {           // diagnostics; 2 = timing ablation (wrong results)
             const char* e = getenv("YM_NMS_STAMPS");
             return e ? (e[0] == '2' ? 2 : 1) : 0;
