@@ -264,11 +264,27 @@ class ConvBN:
         t.workspace = plan.bn_ws.data_ptr()
         return t
 
+    def _static_args(self, plan):
+        """Pointer arguments of this op's forward launches that never change for its plan (the plan's
+        own buffers), converted once: at bs1 the eval forward is host-bound and re-deriving them per
+        launch (tensor indexing, view offsets) was about half of its ~20 us of host time per conv block.
+        Parameters stay looked up per call (a replaced nn.Parameter is seen)."""
+        a = self.__dict__.get("_sa")
+        if a is None:
+            r = self.res
+            bnv = tuple(self.bnv[i].data_ptr() for i in range(4))
+            ss, sq = self.ps[0].data_ptr(), self.ps[1].data_ptr()
+            apply = (self.z.data_ptr(), self.M, self.co, self.HW, bnv[0], bnv[1], self.act,
+                     r.ptr() if r else None, r.bs if r else 0, r.ld if r else 0, self.y.ptr(), self.y.bs, self.y.ld,
+                     _p(getattr(self, "out32", None)))
+            a = self._sa = (bnv, ss, sq, apply)
+        return a
+
     def _bn_fwd(self, plan, st, ss, sq, finalized=False):
         """BatchNorm finalize + apply (+ SiLU, + residual) of the forward: 'bn' family, algorithmic bytes
         = the partial rows read + z read + y written (+ residual read)."""
         bn = self.m.bn
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        (sc, sh, mu, rs), ssp, sqp, apply = self._static_args(plan)
         r = self.res
         e = self.M * self.co * 2
         work = 8 * self.G * self.co * (1 if plan.training and not finalized else 0) + 2 * e + (e if r else 0)
@@ -277,15 +293,13 @@ class ConvBN:
             if finalized:
                 pass
             elif plan.training:
-                call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
+                call("ym_bn_finalize", ssp, sqp, self.G, self.co, float(self.M), _p(bn.weight),
                      _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
                      float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
             elif not plan.eval_coeff_batched:
                 call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
                      _p(bn.running_var), float(bn.eps), sc, sh, st)
-            call("ym_bn_apply", self.z.data_ptr(), self.M, self.co, self.HW, sc, sh, self.act,
-                 r.ptr() if r else None, r.bs if r else 0, r.ld if r else 0, self.y.ptr(), self.y.bs, self.y.ld,
-                 _p(getattr(self, "out32", None)), st)
+            call("ym_bn_apply", *apply, st)
         self._timed(plan, "bn", plan._cur_stream, run, work)
 
     def forward(self, plan, st):
@@ -297,9 +311,11 @@ class ConvBN:
                 ss.data_ptr(), sq.data_ptr(), ctypes.byref(bt), st))
             self._bn_fwd(plan, st, ss, sq, finalized=True)
             return
-        self._timed(plan, "fwd", plan._cur_stream, lambda: call(
-            "ym_conv_fwd", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
-            ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None, st))
+        conv = self.__dict__.get("_sc")
+        if conv is None:
+            conv = self._sc = (ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
+                               ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None)
+        self._timed(plan, "fwd", plan._cur_stream, lambda: call("ym_conv_fwd", *conv, st))
         self._bn_fwd(plan, st, ss, sq)
 
     def _bn_bwd(self, plan, st, dy):
