@@ -7,13 +7,15 @@ forward (HIP plan) + v8 loss (fused kernels) + backward + RCCL gradient all-redu
 
     python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torchrun)
 
-Rank 0 prints ONE JSON line.  `roofline` is the dominant kernel family by time (every conv
-forward / data-gradient / weight-gradient launch and every BatchNorm pass of a step bracketed with
-HIP events, in a pass that runs all launches on one stream); `roofline_probe` is the heaviest single conv launch (HIP events on the launch stream,
-HBM traffic from the committed counter pass); `roofline_step` prices the whole step against the
-same 16-bit MFMA peak.  `cpu_baseline`
-times the CPU oracle restatement (test infrastructure, fp32) on a bounded sample of the
-same workload on this host's cores.
+Rank 0 prints ONE JSON line.  `roofline` is the dense 3x3 conv family against the 16-bit MFMA peak
+(the north star's target: every fwd / dgrad / wgrad launch of a k=3 Conv block bracketed with HIP
+events on its launch stream, in a pass that runs all launches on one stream, algorithmic FLOPs
+summed / durations summed); `roofline_families` gives the same for every conv forward, data-gradient,
+weight-gradient launch and the BatchNorm passes (HBM); `roofline_probe` is the heaviest single conv
+launch; `roofline_step` prices the whole step against the MFMA peak.  `traffic` fields are read from
+the committed counter passes (profiles/traffic.json, labelled with their source and commit), not
+measured in this run.  `cpu_baseline` times the CPU oracle restatement (test infrastructure, fp32) on
+a bounded sample of the same workload on every usable host CPU.
 """
 from __future__ import annotations
 
@@ -40,6 +42,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def traffic_entry(key: str):
+    """The committed counter-pass entry for `key` (profiles/traffic.json), with its source labelled
+    '<profiles dir> @ <commit>' — the traffic is NOT measured in this run (rocprofv3 counters need their
+    own passes, tools/pmc_traffic.py / tools/pmc_layers.py), so the bench says where it comes from."""
+    try:
+        d = json.loads((ROOT / "profiles" / "traffic.json").read_text())
+    except (OSError, ValueError):
+        return None
+    e = d.get(key)
+    if not e:
+        return None
+    src = e.get("source", "profiles")
+    if e.get("commit"):
+        src += f" @ {e['commit']}"
+    return {"bytes_per_launch": e["bytes_per_launch"], "source": f"profiles/traffic.json ({src})"}
+
+
 def traffic_for(key: str):
     """HBM bytes per launch of the probe kernel from the committed rocprofv3 counter pass
     (profiles/traffic.json, written by tools/pmc_traffic.py: 2 x FETCH_SIZE + WRITE_SIZE per the
@@ -53,13 +72,44 @@ def traffic_for(key: str):
     return e["bytes_per_launch"] if e else None
 
 
+def host_cpus():
+    """(threads to use, description) for the CPU baseline: every CPU this process may run on —
+    os.cpu_count(), bounded by its affinity mask and its cgroup CPU quota (a GPU box shows the whole
+    machine's CPUs but grants a share of them) — plus the CPU model."""
+    n = os.cpu_count() or 1
+    usable = n
+    try:
+        usable = min(usable, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = -(-int(q) // int(per))
+            usable = min(usable, max(quota, 1))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, {"nproc": n, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
 def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 2, steps: int = 3):
-    """Oracle (fp32 CPU restatement of the reference) train step on a bounded sample."""
+    """Oracle (fp32 CPU restatement of the reference) train step on a bounded sample, on every usable
+    host CPU (SURVEY §8(d) CPU-baseline plan: torch.set_num_threads(os.cpu_count()), nproc and the CPU
+    model stated)."""
     import torch
     from oracle import model as om
     from oracle import loss as ol
     from datasets.synthetic import synth_batch
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = host_cpus()
     torch.set_num_threads(threads)
     layers, save, P = om.build(om.load_cfg("s"))
     params = [v.requires_grad_(True) for k, v in P.items()
@@ -77,7 +127,7 @@ def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 2, steps: int =
         opt.step()
         times.append(time.perf_counter() - t0)
     t = sorted(times[warmup:])[len(times[warmup:]) // 2]
-    return {"value": round(batch / t, 3), "unit": "images/sec", "cores": threads, "kind": "port",
+    return {"value": round(batch / t, 3), "unit": "images/sec", "cores": threads, "kind": "port", **host,
             "sample": f"YOLOv11-s {imgsz}x{imgsz} bs={batch} full train step (fwd+loss+bwd+clip+AdamW), "
                       f"oracle fp32 restatement, median of {steps} steps after {warmup} warm-up"}
 
@@ -203,7 +253,7 @@ def main():
     # the kernel's own, not stretched by kernels of other streams sharing the CUs
     saved = {k: os.environ.get(k) for k in ("YM_STREAMS", "YM_SIDE_STREAM")}
     os.environ.update(YM_STREAMS="1", YM_SIDE_STREAM="0")
-    plan.family_events = {"fwd": [], "dgrad": [], "wgrad": [], "bn": []}
+    plan.family_events = {"fwd": [], "dgrad": [], "wgrad": [], "bn": [], "fwd3": [], "dgrad3": [], "wgrad3": []}
     for i in range(PROBE_STEPS):
         step(args.warmup + args.steps + PROBE_STEPS + i)
     torch.cuda.synchronize()
@@ -262,15 +312,6 @@ def main():
     from yolomi._lib import lib as _yl
     probe_kernel = {2: "conv_pipe_kernel", 1: "conv_halo_kernel"}.get(
         _yl().ym_conv_algo(ctypes.byref(dom.desc), 0), "conv_gemm_kernel")
-    # the dominant kernel family by time (per step: summed launch durations; conv families against the
-    # MFMA peak with their algorithmic FLOPs, BatchNorm against HBM with its algorithmic bytes)
-    fam_kind = max(fams, key=lambda k: fams[k][0])
-    f_ms, f_work, f_n = fams[fam_kind]
-    names = {"fwd": "conv forward (pipelined / halo / implicit-GEMM kernels)",
-             "dgrad": "conv data gradient (pipelined / halo / implicit-GEMM kernels)",
-             "wgrad": "conv weight gradient (wgrad3 / wgrad1 + split-K reduce)",
-             "bn": "BatchNorm + SiLU passes (finalize + apply; bwd reduce + finalize + apply)"}
-
     def fam_rate(kind):
         ms, work, _ = fams[kind]
         if ms <= 0:
@@ -280,17 +321,37 @@ def main():
             return gbs, gbs / HBM_PEAK_GBS
         tf = work / (ms * 1e-3) / 1e12
         return tf, tf / PEAK_BF16_TFLOPS
-    f_rate, f_frac = fam_rate(fam_kind)
-    bn_fam = fam_kind == "bn"
-    roof_family = {"bound": "hbm" if bn_fam else "mfma", "achieved": round(f_rate, 2),
-                   "peak": HBM_PEAK_GBS if bn_fam else PEAK_BF16_TFLOPS, "unit": "GB/s" if bn_fam else "TFLOP/s",
-                   "frac": round(f_frac, 4), "traffic": traffic_for(f"family {fam_kind} bs{args.batch}"),
-                   "kernel": f"{names[fam_kind]}: {f_n} launch groups per step, "
-                             f"{f_work / 1e9:.0f} {'GB' if bn_fam else 'GFLOP'} algorithmic in {f_ms:.3f} ms summed "
-                             f"launch time (HIP events, all launches on one stream, {PROBE_STEPS} steps)",
-                   "families_ms_per_step": {k: round(v[0], 3) for k, v in fams.items()},
-                   "families_frac": {k: round(fam_rate(k)[1], 4) for k in fams},
-                   "families_bound": {k: ("hbm" if k == "bn" else "mfma") for k in fams}}
+    # `roofline`: the dense 3x3 conv kernels (every fwd / dgrad / wgrad launch of a k=3 Conv block, the
+    # north star's named target) against the 16-bit MFMA peak: algorithmic FLOPs summed over the launches
+    # of one step / their summed HIP-event durations (all launches on one stream, PROBE_STEPS steps)
+    c3 = [fams[k] for k in ("fwd3", "dgrad3", "wgrad3")]
+    c3_ms, c3_flop, c3_n = sum(v[0] for v in c3), sum(v[1] for v in c3), sum(v[2] for v in c3)
+    c3_tf = c3_flop / (c3_ms * 1e-3) / 1e12 if c3_ms > 0 else 0.0
+    t3 = traffic_entry(f"family conv3x3 bs{args.batch}")
+    roof_c3 = {"bound": "mfma", "achieved": round(c3_tf, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+               "frac": round(c3_tf / PEAK_BF16_TFLOPS, 4),
+               "traffic": t3["bytes_per_launch"] if t3 else None,
+               "traffic_unit": "HBM bytes per training step, summed over the family's launches",
+               "traffic_source": t3["source"] if t3 else None,
+               "kernel": f"dense 3x3 conv kernels (conv_pipe / conv_halo / conv_gemm / conv_direct fwd + dgrad, "
+                         f"wgrad3 + split-K reduce): {c3_n} launches per step, {c3_flop / 1e9:.0f} GFLOP algorithmic "
+                         f"in {c3_ms:.3f} ms summed launch time (HIP events on the launch stream, all launches on "
+                         f"one stream, {PROBE_STEPS} steps)",
+               "per_direction_frac": {k[:-1]: round(fam_rate(k)[1], 4) for k in ("fwd3", "dgrad3", "wgrad3")}}
+    names = {"fwd": "conv forward (pipelined / halo / implicit-GEMM / direct kernels)",
+             "dgrad": "conv data gradient (pipelined / halo / implicit-GEMM / direct kernels)",
+             "wgrad": "conv weight gradient (wgrad3 / wgrad1 + split-K reduce)",
+             "bn": "BatchNorm + SiLU passes (finalize + apply; bwd reduce + finalize + apply)"}
+    families = {}
+    for k in ("fwd", "dgrad", "wgrad", "bn"):
+        ms, work, n = fams[k]
+        rate, frac = fam_rate(k)
+        t = traffic_entry(f"family {k} bs{args.batch}")
+        families[k] = {"bound": "hbm" if k == "bn" else "mfma", "ms_per_step": round(ms, 3), "launch_groups": n,
+                       "achieved": round(rate, 2), "unit": "GB/s" if k == "bn" else "TFLOP/s", "frac": round(frac, 4),
+                       "work": f"{work / 1e9:.1f} {'GB' if k == 'bn' else 'GFLOP'} algorithmic per step",
+                       "traffic": t["bytes_per_launch"] if t else None, "traffic_source": t["source"] if t else None,
+                       "kernel": names[k]}
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -308,7 +369,8 @@ def main():
                                f"(fwd+loss+bwd+allreduce+clip+AdamW)",
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch, "imgsz": args.imgsz,
                    "parallelism": f"dp{world}"},
-        "roofline": roof_family,
+        "roofline": roof_c3,
+        "roofline_families": families,
         "roofline_probe": {**roof, "traffic": traffic_for(probe_key),
                      "kernel": f"{probe_kernel} fwd {dom.m.__class__.__name__} {dom.ci}->{dom.co} "
                                f"k{dom.k} s{dom.s} out {dom.y.H}x{dom.y.W}, {dom.flops() / 1e9:.1f} GFLOP and "

@@ -384,11 +384,12 @@ int ym_loss_assignment(void* workspace, int64_t B, int64_t A, int M, const int**
  * pixel xyxy, anc_points (A,2) pixels, gt_labels (B,M) float, gt_bboxes (B,M,4) (16-B aligned),
  * mask_gt (B,M) float.  Outputs: target_labels (B,A) float, target_bboxes (B,A,4), target_scores
  * (B,A,nc), fg_mask (B,A) uint8, target_gt_idx (B,A) int64 — the reference's 5-tuple.  Same kernels
- * (and quirks Q1-Q3) as ym_loss_fwd's fused assignment. */
+ * (and quirks Q1-Q3) as ym_loss_fwd's fused assignment; alpha / beta / eps are the class's (align =
+ * score^alpha * IoU^beta, norm eps; the fused loss uses 0.5 / 4 / 1e-9). */
 size_t ym_tal_assign_workspace_size(int64_t B, int64_t A, int M);
 int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, const float* anc_points, const float* gt_labels,
-                  const float* gt_bboxes, const float* mask_gt, int64_t B, int64_t A, int nc, int M, void* workspace,
-                  size_t workspace_bytes, float* target_labels, float* target_bboxes, float* target_scores,
+                  const float* gt_bboxes, const float* mask_gt, int64_t B, int64_t A, int nc, int M, float alpha,
+                  float beta, float eps, void* workspace, size_t workspace_bytes, float* target_labels, float* target_bboxes, float* target_scores,
                   uint8_t* fg_mask, int64_t* target_gt_idx, void* stream);
 /* BboxLoss.forward (losses/yolo_v8_loss.py:280-324): pred_dist (B,A,64), pred_bboxes / target_bboxes
  * (B,A,4) grid units, anchor_points (A,2), target_scores (B,A,nc), tss device scalar (target_scores_sum),
@@ -405,6 +406,11 @@ int ym_bbox_loss_bwd(const float* pred_dist, const float* pred_bboxes, const flo
 /* y (B, 4+nc, A): xywh * stride from the DFL projection with weights dfl_w[16], sigmoid(cls). */
 int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc, int nl, const int* level_h,
                      const int* level_w, const float* strides, const float* dfl_w, float* y, void* stream);
+/* DFL.forward (models/yolo11_modules.py:189-192) called standalone: x (B, 4*c1, A) fp32 -> softmax over the
+ * c1 bins of each side -> 1x1 conv with w[c1] -> y (B, 4, A).  ym_dfl_bwd writes dx = d(sum y*dy)/dx. */
+int ym_dfl_fwd(const float* x, int64_t B, int64_t A, int c1, const float* w, float* y, void* stream);
+int ym_dfl_bwd(const float* x, int64_t B, int64_t A, int c1, const float* w, const float* dy, float* dx,
+               void* stream);
 
 /* ------------------------------------------------------------------ data path
  * Stretch-resize of a batch of grayscale uint8 images (packed back to back in `src`; meta[3b..3b+2]

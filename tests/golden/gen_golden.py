@@ -473,6 +473,54 @@ def gen_assigner():
     save("assigner.npz", **arrs)
 
 
+def gen_modules():
+    """Module classes called on their own (models/__init__.py and losses/__init__.py exports):
+    Attention.forward (yolo11_modules.py:124-136) at the PSA head shape (heads=4) and at the class
+    default heads=8, train-mode forward + backward; DFL.forward (:189-192) with the arange weights
+    it is built with and with Kaiming weights (as _initialize_weights leaves them, Q5), forward +
+    input gradient; TaskAlignedAssigner with its class defaults (alpha=1.0, beta=6.0,
+    yolo_v8_loss.py:67) on the assigner fixture's inputs."""
+    arrs = {}
+    for name, (dim, heads, shape, seed) in {"attn_h4": (256, 4, (2, 256, 20, 20), 71),
+                                            "attn_h8": (512, 8, (1, 512, 10, 12), 72)}.items():
+        mod = ref_mods.Attention(dim, num_heads=heads, attn_ratio=0.5)
+        apply_seeded_weights(mod.state_dict())
+        mod.apply(lambda m: setattr(m, "eps", 1e-3) if isinstance(m, torch.nn.BatchNorm2d) else None)
+        mod.apply(lambda m: setattr(m, "momentum", 0.03) if isinstance(m, torch.nn.BatchNorm2d) else None)
+        # weights are key-seeded (oracle/weights.py) and x / dy come from seeded CPU generators
+        # (x: Generator(seed), dy: Generator(seed + 100)), so the test re-creates them; stored: outputs
+        x, ys, dys = _block_case(mod, torch.randn(shape, generator=torch.Generator().manual_seed(seed)), seed + 100)
+        arrs[f"{name}/y"], arrs[f"{name}/dx"] = ys[0], x.grad
+        for k, p in mod.named_parameters():
+            if p.grad.numel() > 65536:      # large weight gradients: strided fingerprint + norm
+                arrs[f"{name}/gfp:{k}"] = _fingerprint(p.grad)
+                arrs[f"{name}/gn:{k}"] = np.float64(p.grad.double().norm())
+            else:
+                arrs[f"{name}/g:{k}"] = p.grad
+        for k, v in mod.state_dict().items():
+            if "running" in k:
+                arrs[f"{name}/s:{k}"] = v.clone()
+    g = torch.Generator().manual_seed(73)
+    for name, kaiming in (("dfl_arange", False), ("dfl_kaiming", True)):
+        mod = ref_mods.DFL(16)
+        if kaiming:
+            torch.nn.init.kaiming_normal_(mod.conv.weight, generator=g, mode="fan_out", nonlinearity="relu")
+        x = (torch.randn(2, 64, 300, generator=g) * 3.0).requires_grad_(True)
+        y = mod(x)
+        dy = torch.randn(y.shape, generator=g)
+        y.backward(dy)
+        arrs.update({f"{name}/w": mod.conv.weight.detach().reshape(-1), f"{name}/x": x, f"{name}/y": y,
+                     f"{name}/dy": dy, f"{name}/dx": x.grad})
+    a = np.load(HERE / "assigner.npz")
+    ins = [torch.from_numpy(a["as_" + k]) for k in ("pd_scores", "pd_bboxes", "anc_points", "gt_labels", "gt_bboxes",
+                                                   "mask_gt")]
+    tal = ref_loss_mod.TaskAlignedAssigner(num_classes=5)
+    for nm, t in zip(("target_labels", "target_bboxes", "target_scores", "fg_mask", "target_gt_idx"), tal(*ins)):
+        arrs[f"tal_default/{nm}"] = t
+    arrs["tal_default/params"] = np.asarray([tal.alpha, tal.beta, tal.eps], np.float64)
+    save("modules.npz", **arrs)
+
+
 # --------------------------------------------------------------------------- loss curve
 def gen_curve(steps=20):
     torch.manual_seed(0)
@@ -497,7 +545,7 @@ def gen_curve(steps=20):
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["structure", "nms", "decode", "metrics", "model", "s_small", "m_small", "attn_big",
-                             "detect", "blocks", "assigner", "curve"]
+                             "detect", "blocks", "assigner", "modules", "curve"]
     if "structure" in which:
         gen_structure()
     if "nms" in which:
@@ -521,5 +569,7 @@ if __name__ == "__main__":
         gen_blocks()
     if "assigner" in which:
         gen_assigner()
+    if "modules" in which:
+        gen_modules()
     if "curve" in which:
         gen_curve()

@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=int, nargs="*", help="plan op indices to time (default: every ConvBN)")
+    ap.add_argument("--seq-out", help="counter-pass mode: write the (op, kind, k, flops, launches) order of the "
+                                      "timed groups here and separate the groups with a marker kernel "
+                                      "(tools/pmc_layers.py splits a rocprofv3 --pmc pass on the markers)")
     args = ap.parse_args()
     import torch
     import yaml
@@ -46,6 +49,15 @@ def main():
     ws = plan.wgrad_ws()
     rows = []
     tot = [0.0, 0.0, 0.0]
+    seq = []
+    marker = torch.zeros(1, device=dev)
+
+    def sep(n=1):
+        for _ in range(n):
+            marker.add_(1.0)              # one elementwise torch kernel: the group separator of a counter pass
+    if args.seq_out:
+        torch.cuda.synchronize()
+        sep(3)                            # start marker: three separators in a row
     for i, op in enumerate(plan.ops):
         if type(op) is not ConvBN or (args.only and i not in args.only):
             continue
@@ -71,6 +83,10 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             ms.append(e0.elapsed_time(e1) / args.reps)
+            if args.seq_out:
+                sep()
+                seq.append({"op": i, "kind": kind, "k": d.k, "s": d.stride, "cin": d.cin, "cout": d.cout,
+                            "out": [d.oh, d.ow], "flops": fl, "launches": args.reps + 2})
         for j in range(3):
             tot[j] += ms[j]
         tf = [fl / (m * 1e-3) / 1e12 if m > 0 else 0.0 for m in ms]
@@ -91,6 +107,10 @@ def main():
         print(f"{i:4d} {ci:4d} {co:4d} {k} {s} {oh:3d}x{ow:<3d} {gf:7.1f} {roof:>4} | {ms[0]:7.3f} {tf[0]:5.0f} {fr[0]:5.2f} | "
               f"{ms[1]:7.3f} {tf[1]:5.0f} {fr[1]:5.2f} | {ms[2]:7.3f} {tf[2]:5.0f} {fr[2]:5.2f}")
     print(f"total ms: fwd {tot[0]:.3f}  dgrad {tot[1]:.3f}  wgrad {tot[2]:.3f}")
+    if args.seq_out:
+        import json
+        Path(args.seq_out).write_text(json.dumps({"batch": args.batch, "imgsz": args.imgsz, "scale": args.scale,
+                                                  "groups": seq}))
 
 
 if __name__ == "__main__":

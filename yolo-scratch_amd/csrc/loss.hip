@@ -308,10 +308,12 @@ __global__ void __launch_bounds__(RES_THREADS) assign_resolve_kernel(const float
     }
 }
 
-// target-score magnitude: align = sigmoid(cls[label])^0.5 * IoU^4 (:206), norm = align*IoU/(align+eps)
+// target-score magnitude: align = sigmoid(cls[label])^alpha * IoU^beta (:206), norm = align*IoU/(align+eps)
+// (v8DetectionLoss: alpha 0.5, beta 4, eps 1e-9; the class defaults alpha 1, beta 6 for a standalone assigner)
 template <class Src>
 __global__ void assign_norm_kernel(Src src, int64_t A, const float4* __restrict__ gt_box,
-                                   const float* __restrict__ gt_lab, int M, AssignWs w) {
+                                   const float* __restrict__ gt_lab, int M, AssignWs w, float alpha, float beta,
+                                   float eps) {
     const int b = blockIdx.y;
     const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (a >= A) return;
@@ -324,8 +326,8 @@ __global__ void assign_norm_kernel(Src src, int64_t A, const float4* __restrict_
     iou = iou < 0.f ? 0.f : iou;
     int lab = int(gt_lab[b * M + t]);
     float sc = src.score(b, a, lab);
-    float align = sqrtf(sc) * powf(iou, 4.0f);
-    w.norm[i] = align * iou / (align + EPS_TAL);
+    float align = (alpha == 0.5f ? sqrtf(sc) : powf(sc, alpha)) * powf(iou, beta);
+    w.norm[i] = align * iou / (align + eps);
 }
 
 // ---------------------------------------------------------------- loss terms
@@ -788,7 +790,7 @@ extern "C" int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int 
         hipLaunchKernelGGL(assign_resolve_kernel, dim3(unsigned(B)), dim3(RES_THREADS), size_t(M) * 5 * sizeof(int),
                            st, head, A, no, nc, reinterpret_cast<const float4*>(gt_box), gt_lab, gt_valid, M, w);
         hipLaunchKernelGGL(assign_norm_kernel<HeadSrc>, ga, dim3(256), 0, st, src, A,
-                           reinterpret_cast<const float4*>(gt_box), gt_lab, M, w);
+                           reinterpret_cast<const float4*>(gt_box), gt_lab, M, w, 0.5f, 4.0f, EPS_TAL);
     } else {
         // no targets in the batch (:100-108 early return): all background
         if (hipMemsetAsync(w.fg, 0, size_t(B) * A * 4, st) != hipSuccess) return YM_ERR_HIP;
@@ -840,6 +842,66 @@ extern "C" int ym_detect_decode(const float* head, int64_t B, int64_t A, int nc,
     return YM_OK;
 }
 
+// DFL.forward (yolo11_modules.py:189-192) on its own: x (B, 4*c1, A) -> softmax over the c1 bins of each
+// side -> 1x1 conv with the module's c1 weights -> y (B, 4, A).  One thread per (anchor, side, image); the
+// bins of a side are c1 rows A apart, so a wave's loads of one bin are one contiguous 256-B segment.
+constexpr int DFL_MAX = 64;
+
+__global__ void dfl_fwd_kernel(const float* __restrict__ x, int64_t A, int c1, const float* __restrict__ w,
+                               float* __restrict__ y) {
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int q = blockIdx.y, b = blockIdx.z;
+    if (a >= A) return;
+    const float* xs = x + (int64_t(b) * 4 + q) * c1 * A + a;
+    float v[DFL_MAX];
+    float m = -INFINITY;
+    for (int j = 0; j < c1; ++j) { v[j] = xs[int64_t(j) * A]; m = fmaxf(m, v[j]); }
+    float s = 0.f;
+    for (int j = 0; j < c1; ++j) { v[j] = expf(v[j] - m); s += v[j]; }
+    float acc = 0.f;
+    for (int j = 0; j < c1; ++j) acc += (v[j] / s) * w[j];
+    y[(int64_t(b) * 4 + q) * A + a] = acc;
+}
+
+// softmax backward in autograd's order: dp_j = w_j * dy, dx_j = p_j * (dp_j - sum_k p_k dp_k)
+__global__ void dfl_bwd_kernel(const float* __restrict__ x, int64_t A, int c1, const float* __restrict__ w,
+                               const float* __restrict__ dy, float* __restrict__ dx) {
+    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int q = blockIdx.y, b = blockIdx.z;
+    if (a >= A) return;
+    const int64_t base = (int64_t(b) * 4 + q) * c1 * A + a;
+    float v[DFL_MAX];
+    float m = -INFINITY;
+    for (int j = 0; j < c1; ++j) { v[j] = x[base + int64_t(j) * A]; m = fmaxf(m, v[j]); }
+    float s = 0.f;
+    for (int j = 0; j < c1; ++j) { v[j] = expf(v[j] - m); s += v[j]; }
+    const float g = dy[(int64_t(b) * 4 + q) * A + a];
+    float e = 0.f;
+    for (int j = 0; j < c1; ++j) { v[j] = v[j] / s; e += v[j] * (w[j] * g); }
+    for (int j = 0; j < c1; ++j) dx[base + int64_t(j) * A] = v[j] * (w[j] * g - e);
+}
+
+extern "C" int ym_dfl_fwd(const float* x, int64_t B, int64_t A, int c1, const float* w, float* y, void* stream) {
+    YM_CHECK_ARG(c1 >= 1 && c1 <= DFL_MAX, "ym_dfl_fwd: c1=%d out of range (1..%d)", c1, DFL_MAX);
+    YM_CHECK_ARG(B >= 0 && A >= 0 && B <= 65535, "ym_dfl_fwd: B=%lld A=%lld", (long long)B, (long long)A);
+    if (B == 0 || A == 0) return YM_OK;
+    dim3 g(unsigned((A + 255) / 256), 4, unsigned(B));
+    hipLaunchKernelGGL(dfl_fwd_kernel, g, dim3(256), 0, as_stream(stream), x, A, c1, w, y);
+    YM_LAUNCH_CHECK("ym_dfl_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_dfl_bwd(const float* x, int64_t B, int64_t A, int c1, const float* w, const float* dy, float* dx,
+                          void* stream) {
+    YM_CHECK_ARG(c1 >= 1 && c1 <= DFL_MAX, "ym_dfl_bwd: c1=%d out of range (1..%d)", c1, DFL_MAX);
+    YM_CHECK_ARG(B >= 0 && A >= 0 && B <= 65535, "ym_dfl_bwd: B=%lld A=%lld", (long long)B, (long long)A);
+    if (B == 0 || A == 0) return YM_OK;
+    dim3 g(unsigned((A + 255) / 256), 4, unsigned(B));
+    hipLaunchKernelGGL(dfl_bwd_kernel, g, dim3(256), 0, as_stream(stream), x, A, c1, w, dy, dx);
+    YM_LAUNCH_CHECK("ym_dfl_bwd");
+    return YM_OK;
+}
+
 // TaskAlignedAssigner.forward (yolo_v8_loss.py:78-180) on explicit tensors; M >= 1 (the M = 0 early return
 // :100-108 is the caller's).  Outputs: target_labels (B,A) f32, target_bboxes (B,A,4), target_scores
 // (B,A,nc), fg_mask (B,A) u8, target_gt_idx (B,A) i64.
@@ -849,7 +911,8 @@ extern "C" size_t ym_tal_assign_workspace_size(int64_t B, int64_t A, int M) {
 
 extern "C" int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, const float* anc_points,
                              const float* gt_labels, const float* gt_bboxes, const float* mask_gt, int64_t B,
-                             int64_t A, int nc, int M, void* workspace, size_t workspace_bytes, float* target_labels,
+                             int64_t A, int nc, int M, float alpha, float beta, float eps, void* workspace,
+                             size_t workspace_bytes, float* target_labels,
                              float* target_bboxes, float* target_scores, uint8_t* fg_mask, int64_t* target_gt_idx,
                              void* stream) {
     YM_CHECK_ARG(M >= 1 && M <= 4096, "ym_tal_assign: M=%d out of range (1..4096)", M);
@@ -871,7 +934,8 @@ extern "C" int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, con
     hipLaunchKernelGGL(assign_scan_kernel<PlainSrc>, ga, dim3(256), size_t(M) * 12, st, src, A, gb, valid, M, w);
     hipLaunchKernelGGL(assign_resolve_kernel, dim3(unsigned(B)), dim3(RES_THREADS), size_t(M) * 5 * sizeof(int), st,
                        nullptr, A, 0, nc, gb, gt_labels, valid, M, w);
-    hipLaunchKernelGGL(assign_norm_kernel<PlainSrc>, ga, dim3(256), 0, st, src, A, gb, gt_labels, M, w);
+    hipLaunchKernelGGL(assign_norm_kernel<PlainSrc>, ga, dim3(256), 0, st, src, A, gb, gt_labels, M, w, alpha, beta,
+                       eps);
     hipLaunchKernelGGL(assign_targets_kernel, ga, dim3(256), 0, st, A, nc, gb, gt_labels, M, w, target_labels,
                        reinterpret_cast<float4*>(target_bboxes), target_scores, fg_mask, target_gt_idx);
     YM_LAUNCH_CHECK("ym_tal_assign");

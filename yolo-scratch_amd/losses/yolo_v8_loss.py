@@ -108,9 +108,6 @@ class TaskAlignedAssigner(nn.Module):
         """-> (target_labels (B,A), target_bboxes (B,A,4), target_scores (B,A,nc), fg_mask (B,A) bool,
         target_gt_idx (B,A) int64), reference :78-180 (including its M = 0 early return :100-108)."""
         require_device(pd_scores, pd_bboxes, anc_points, gt_labels, gt_bboxes, mask_gt)
-        if (self.alpha, self.beta, self.eps) != (0.5, 4.0, 1e-9):
-            raise YolomiError("the HIP assigner is specialised for alpha=0.5, beta=4.0, eps=1e-9 "
-                              "(v8DetectionLoss's TaskAlignedAssigner(topk=50, alpha=0.5, beta=4.0))")
         self.bs = B = pd_scores.shape[0]
         self.n_max_boxes = M = gt_bboxes.shape[1]
         A, nc = pd_scores.shape[1], pd_scores.shape[2]
@@ -132,7 +129,7 @@ class TaskAlignedAssigner(nn.Module):
         fg = torch.empty(B, A, dtype=torch.bool, device=dev)
         tgi = torch.empty(B, A, dtype=torch.int64, device=dev)
         call("ym_tal_assign", sc.data_ptr(), pb.data_ptr(), an.data_ptr(), gl.data_ptr(), gb.data_ptr(), mg.data_ptr(),
-             B, A, nc, M, ws.data_ptr(), ws_n, t_lab.data_ptr(), t_box.data_ptr(), t_sc.data_ptr(), fg.data_ptr(),
+             B, A, nc, M, float(self.alpha), float(self.beta), float(self.eps), ws.data_ptr(), ws_n, t_lab.data_ptr(), t_box.data_ptr(), t_sc.data_ptr(), fg.data_ptr(),
              tgi.data_ptr(), stream_ptr(dev))
         return t_lab.to(gt_labels.dtype), t_box, t_sc, fg, tgi
 

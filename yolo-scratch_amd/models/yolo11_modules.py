@@ -102,8 +102,10 @@ class SPPF(_Block):
             raise NotImplementedError("SPPF pool kernel is specialised for k=5 (the only size the graph uses)")
 
 
-class Attention(nn.Module):
-    """Multi-head attention with positional dw-conv (reference :108-136); runs inside PSA's plan."""
+class Attention(_Block):
+    """Multi-head attention with positional dw-conv (reference :108-136).  Inside PSA it runs in PSA's
+    plan; called on its own, `forward` lowers qkv 1x1 -> attention core -> + pe(v) -> proj 1x1 into a
+    plan of its own (yolomi.graph._attention without the PSA residual)."""
 
     def __init__(self, dim, num_heads=8, attn_ratio=0.5):
         super().__init__()
@@ -153,6 +155,12 @@ class DFL(nn.Module):
         x = torch.arange(c1, dtype=torch.float)
         self.conv.weight.data[:] = nn.Parameter(x.view(1, c1, 1, 1))
         self.c1 = c1
+
+    def forward(self, x):
+        """(b, 4*c1, a) -> softmax over the c1 bins of each side -> 1x1 conv with this module's weight ->
+        (b, 4, a) (reference :189-192), ym_dfl_fwd; differentiable in x (ym_dfl_bwd)."""
+        from yolomi.head import dfl
+        return dfl(x, self.conv.weight, self.c1)
 
 
 class Detect(nn.Module):

@@ -118,8 +118,10 @@ SIGNATURES = {
     "ym_loss_bwd": (R, [P, I64, I64, INT, INT, P, P, P, INT, P, SZ, P, P, P, P, P, P]),
     "ym_loss_assignment": (R, [P, I64, I64, INT, P, P, P]),
     "ym_detect_decode": (R, [P, I64, I64, INT, INT, P, P, P, P, P, P]),
+    "ym_dfl_fwd": (R, [P, I64, I64, INT, P, P, P]),
+    "ym_dfl_bwd": (R, [P, I64, I64, INT, P, P, P, P]),
     "ym_tal_assign_workspace_size": (SZ, [I64, I64, INT]),
-    "ym_tal_assign": (R, [P, P, P, P, P, P, I64, I64, INT, INT, P, SZ, P, P, P, P, P, P]),
+    "ym_tal_assign": (R, [P, P, P, P, P, P, I64, I64, INT, INT, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
     "ym_bbox_loss_workspace_size": (SZ, [I64, I64]),
     "ym_bbox_loss_fwd": (R, [P, P, P, P, P, P, P, I64, I64, INT, P, SZ, P, P]),
     "ym_bbox_loss_bwd": (R, [P, P, P, P, P, P, P, I64, I64, INT, P, P, P, P]),

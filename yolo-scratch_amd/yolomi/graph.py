@@ -250,7 +250,10 @@ class ConvBN:
         if probe:
             plan.probe_events.append((ev0, ev1))
         if fam is not None and kind in fam:
-            fam[kind].append((ev0, ev1, self.flops() if work is None else work))
+            ent = (ev0, ev1, self.flops() if work is None else work)
+            fam[kind].append(ent)
+            if kind != "bn" and self.k == 3 and f"{kind}3" in fam:     # the dense 3x3 convs on their own
+                fam[f"{kind}3"].append(ent)
 
     def _bn_train(self, plan):
         """ym_bn_train for the fused finalize (pointers only; the workspace is the current stream's)."""
@@ -1230,8 +1233,13 @@ def _detect(plan, m, xs, head):
         a_off += x.H * x.W
 
 
+def _attention_block(plan, m, x: View, out=None):
+    """Attention.forward on its own (yolo11_modules.py:124-136): proj(attn(x) + pe(v)), no residual."""
+    return _attention(plan, m, x, out, res=None)
+
+
 LOWER = {"Conv": _conv, "Bottleneck": _bottleneck, "C3k": _c3k, "C2f": _c2f, "C3k2": _c2f, "SPPF": _sppf,
-         "C2PSA": _c2psa, "PSA": _psa}
+         "C2PSA": _c2psa, "PSA": _psa, "Attention": _attention_block}
 
 
 def lower_block(plan, m, x: View):
