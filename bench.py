@@ -184,8 +184,6 @@ def main():
     for i in range(n_batches):
         b = synth_batch(args.batch, args.imgsz, seed=1000 * rank + i)
         b = prepare_batch(b, dev)                  # the data path's H2D (records max_gt on the host)
-        if os.environ.get("YM_LOSS_SYNC") == "1":      # A/B: the loss counts M with a device sync
-            b.pop("max_gt", None)
         batches.append(b)
 
     def step(i):

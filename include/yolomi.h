@@ -12,11 +12,9 @@
  *  - All pointers are DEVICE pointers unless stated; buffers are allocated by
  *    the caller (PyTorch caching allocator); the library never allocates or
  *    frees caller memory and keeps no TENSOR state between calls.  The only
- *    process-wide state is configuration and diagnostics: the conv kernel
- *    selection policies (ym_conv_set_halo / ym_conv_set_pipe / ym_conv_set_direct, YM_CONV_HALO /
- *    YM_CONV_PIPE / YM_CONV_DIRECT read once) and the
- *    NMS segment counters (ym_debug_nms_stamps, written when YM_NMS_STAMPS is
- *    set); neither changes a result.
+ *    process-wide state is configuration: the conv kernel selection policies
+ *    (ym_conv_set_halo / ym_conv_set_pipe / ym_conv_set_direct); it never changes a result
+ *    beyond fp32 summation order.  The library reads no environment variables.
  *  - `stream` is a hipStream_t (0 = legacy default stream); every call is
  *    asynchronous on it and performs no device-wide synchronisation.
  *  - Activations are NHWC.  An "activation view" is (base pointer, batch
@@ -107,11 +105,6 @@ int ym_eval_detections(const float* pred_boxes, const float* pred_scores, const 
 int ym_eval_ap(const float* scores, const uint8_t* is_tp, int64_t n, int64_t n_gt, void* workspace,
                size_t workspace_bytes, double* out, void* stream);
 
-/* Diagnostics: segment cycle totals (s_memtime) of the last small-batch NMS scan, recorded when
- * YM_NMS_STAMPS is set in the environment: [0] between chunks, [1] removed-bits reduction,
- * [2] diagonal resolve, [3] keep update. */
-int ym_debug_nms_stamps(unsigned long long* out4);
-
 /* calculate_iou_batch (utils/metrics.py:49-81): out[i*m+j] = IoU(boxes1[i], boxes2[j]),
  * xyxy fp32 in the reference's op order. */
 int ym_iou_matrix(const float* boxes1, const float* boxes2, int64_t n, int64_t m, float* out, void* stream);
@@ -176,73 +169,26 @@ int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt,
 size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d);
 int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, void* workspace,
                   size_t workspace_bytes, float* dw_oihw, int accumulate, void* stream);
-/* Training BatchNorm2d state and outputs for the fused finalize of ym_conv_fwd_bn /
- * ym_conv_first_fwd_bn / ym_dw3x3_fwd_bn: the kernel that produces the batch statistics also
- * reduces them (fixed order, fp64; ticket-elected last workgroups, no spinning) and writes what
- * ym_bn_finalize would — scale, shift, mean, rstd, running stats, num_batches_tracked — so no
- * finalize launch sits between the conv and ym_bn_apply.  workspace: ym_bn_workspace_size(cout)
- * bytes, shared with the other BN calls of the same stream (counters left at zero). */
-typedef struct {
-    const float* gamma;
-    const float* beta;
-    float* running_mean;       /* may be NULL (no running stats) */
-    float* running_var;
-    int64_t* num_batches_tracked;   /* may be NULL */
-    float momentum, eps;
-    float* scale;
-    float* shift;
-    float* mean;
-    float* rstd;
-    void* workspace;
-} ym_bn_train;
-/* ym_conv_fwd (out_f32 = 2, statistics required) + ym_bn_finalize in one launch; count = n*oh*ow. */
-int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* z, float* stat_sum,
-                   float* stat_sq, const ym_bn_train* bn, void* stream);
 /* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0); y = NULL: statistics only. */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
 /* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
  * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). cout <= 128. */
 size_t ym_conv_first_wgrad_workspace_size(int cout);
-/* ym_conv_first_fwd + ym_bn_finalize in one launch (count = n*oh*ow). */
-int ym_conv_first_fwd_bn(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
-                         int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
-                         const ym_bn_train* bn, void* stream);
 int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
                         int cout, int stride, int pad, float* workspace, size_t workspace_bytes, void* stream);
-/* The stem Conv block with its pre-BatchNorm z recomputed from the image instead of stored (z is
- * the step's largest tensor; 9 MACs per element): ym_stem_stats gives the forward statistics
- * ([blocks][cout] partials for ym_bn_finalize), ym_stem_apply writes act = SiLU(z*scale + shift) (fp16) into the y view; the
- * backward's ym_stem_bwd_reduce gives the [blocks][cout] partials of sum(g), sum(g*xhat) for
- * ym_bn_bwd_finalize, and ym_stem_bwd_wgrad forms dz and adds the weight gradient into dw_oihw
- * without storing dz.  bnv: [4][cout] scale, shift, mean, rstd; coef: ym_bn_bwd_finalize's. */
-int ym_stem_stats(const float* img, const float* w_oihw, float* stat_sum, float* stat_sq, int blocks, int n, int h,
-                  int w, int oh, int ow, int cout, int stride, int pad, void* stream);
-int ym_stem_apply(const float* img, const float* w_oihw, const float* scale, const float* shift, uint16_t* y,
-                  int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
-                  void* stream);
-int ym_stem_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
-                       const float* bnv, float* part_sum, float* part_dot, int blocks, int n, int h, int w, int oh,
-                       int ow, int cout, int stride, int pad, void* stream);
 size_t ym_stem_bwd_wgrad_workspace_size(int cout);
 /* Stored-z stem backward: dz = BatchNorm-backward apply of dy on the STORED fp16 z (dense
  * [m][cout]) straight into the weight-gradient partials (dz never written) — replaces
- * ym_bn_bwd_apply + ym_conv_first_wgrad for the stored path; workspace as ym_stem_bwd_wgrad. */
+ * ym_bn_bwd_apply + ym_conv_first_wgrad; cout 16 / 32 / 64; workspace ym_stem_bwd_wgrad_workspace_size(cout). */
 int ym_stem_bwd_wgrad_stored(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, const float* img,
                              const float* bnv, const float* coef, float* dw_oihw, float* workspace,
                              size_t workspace_bytes, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
                              void* stream);
-int ym_stem_bwd_wgrad(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
-                      const float* bnv, const float* coef, float* dw_oihw, float* workspace, size_t workspace_bytes,
-                      int n, int h, int w, int oh, int ow, int cout, int stride, int pad, void* stream);
 /* Depthwise 3x3 s1 p1 (Attention.pe, yolo11_modules.py:122); input channel c reads source
  * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
 int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks, void* stream);
-/* ym_dw3x3_fwd + ym_bn_finalize in one launch (count = n*h*wd). */
-int ym_dw3x3_fwd_bn(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
-                    uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks,
-                    const ym_bn_train* bn, void* stream);
 size_t ym_dw3x3_bwd_workspace_size(int c);
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
@@ -284,12 +230,6 @@ int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint1
 int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                        const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
                        float* coef, void* workspace, void* stream);
-/* ym_bn_bwd_reduce + ym_bn_bwd_finalize in one launch (the statistics pass's last workgroups fold
- * the partials, fixed order): part_* hold ym_bn_bwd_blocks(m, c) rows; count = m. */
-int ym_bn_bwd_reduce_finalize(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
-                              int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
-                              int act, float* part_sum, float* part_dot, const float* gamma, float* dgamma,
-                              float* dbeta, int accumulate, float* coef, void* workspace, void* stream);
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                     const float* coef, uint16_t* dz, void* stream);

@@ -306,14 +306,9 @@ DIRECT = [
 
 
 @pytest.mark.parametrize("shape", DIRECT, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in DIRECT])
-@pytest.mark.parametrize("s2form", ["pairs", "classes"])
-def test_direct_kernel_vs_torch(shape, s2form, monkeypatch):
-    """s2form: the stride-2 data gradient over column pairs (default) or as 4 parity classes
-    (YM_DIRECT_S2PAIR=0, read per plan)."""
-    if s2form == "classes":
-        if shape[6] != 2:
-            pytest.skip("stride-2 data-gradient form only")
-        monkeypatch.setenv("YM_DIRECT_S2PAIR", "0")
+def test_direct_kernel_vs_torch(shape):
+    """The direct register-weight kernel forced on (the stride-2 data gradient by row-parity class over
+    column pairs) vs PyTorch fp32 on the same rounded operands."""
     from yolomi._lib import call, lib, ConvDesc
     n, h, w, cin, cout, k, s, xe, ye = shape
     p = k // 2

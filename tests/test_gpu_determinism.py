@@ -67,10 +67,11 @@ def test_train_step_bit_reproducible():
             assert torch.equal(a, c), f"parameter {i}: max |diff| {float((a - c).abs().max())}"
 
 
-def test_eval_graph_replay_matches_eager(monkeypatch):
-    """YM_EVAL_GRAPH=1 (opt-in HIP-graph replay of the eval forward): eager first call,
-    capture on the second, replays after — all bit-identical to eager; an in-place weight update
-    (optimizer step) is seen by the replay; new storage behind a parameter drops the graph (address key)."""
+def test_eval_coefficients_follow_replaced_buffers():
+    """The eval forward computes every BatchNorm's scale / shift in one launch over a pointer table built
+    once per plan (ym_bn_eval_coeff_batch).  The table is keyed on every pointer it holds, so a buffer or
+    parameter REPLACED by a new tensor (bn.running_var = ..., load_state_dict(assign=True)) is read from
+    its new storage, never from the freed one: the output equals a fresh model's with the same state."""
     import yaml
     from pathlib import Path
     from models import build_yolo11
@@ -81,25 +82,18 @@ def test_eval_graph_replay_matches_eager(monkeypatch):
     m = build_yolo11(cfg, ch=1, nc=5).cuda().eval()
     img = torch.rand(2, 1, 256, 256, generator=torch.Generator().manual_seed(4)).cuda()
 
-    def run():
+    def run(model):
         with torch.no_grad():
-            y, _ = m(img)
+            y, _ = model(img)
         return y.clone()
-    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
-    ref = run()
-    monkeypatch.setenv("YM_EVAL_GRAPH", "1")
-    outs = [run() for _ in range(3)]                  # eager, capture, replay
-    assert all(torch.equal(o, ref) for o in outs)
-    w = m.model[1].conv.weight
-    with torch.no_grad():
-        w.mul_(1.5)                                   # in place: same address
-    rep = run()
-    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
-    ref2 = run()
-    assert torch.equal(rep, ref2) and not torch.equal(rep, ref)
-    monkeypatch.setenv("YM_EVAL_GRAPH", "1")
-    w.data = w.detach().clone() * 0.5                # new storage behind the same Parameter
-    rep3 = run()
-    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
-    ref3 = run()
-    assert torch.equal(rep3, ref3) and not torch.equal(rep3, ref2)
+    y0 = run(m)
+    bn = m.model[1].bn
+    bn.running_var = bn.running_var.detach().clone() * 2.0          # new storage
+    bn.bias = torch.nn.Parameter(bn.bias.detach().clone() + 0.25)   # new Parameter
+    y1 = run(m)
+    torch.manual_seed(3)
+    m2 = build_yolo11(cfg, ch=1, nc=5).cuda().eval()
+    m2.load_state_dict(m.state_dict())
+    y2 = run(m2)
+    assert not torch.equal(y1, y0)
+    assert torch.equal(y1, y2)

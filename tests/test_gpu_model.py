@@ -379,56 +379,36 @@ def test_loss_with_host_max_gt_matches_synced_count():
         assert torch.equal(a, c)
 
 
-def test_stem_recompute_matches_stored(golden, monkeypatch):
-    """The stem Conv block (1 -> 32, 3x3 s2) with z recomputed from the image (ym_stem_stats / _apply /
-    _bwd_reduce / _bwd_wgrad) against the stored-z path on the same input and output gradient: the
-    same fp16 / bf16 roundings at the same points, the statistics summed in a different fixed order
-    (so a few fp16 outputs differ by one ulp): y within 1e-3, parameter gradients and running
-    statistics within 1e-4 (relative L2)."""
+@pytest.mark.parametrize("c,shape", [(32, (2, 64, 64)), (32, (3, 47, 61)), (24, (2, 40, 36))])
+def test_stem_block_vs_torch_fp32(c, shape):
+    """The stem Conv(1, c, 3, 2) block on its own vs PyTorch fp32 (CPU) on the same input / output gradient:
+    c = 32 runs the fused stored-z backward (ym_stem_bwd_wgrad_stored, BN apply inside the weight gradient;
+    odd map sizes give partial 8x32 tiles), c = 24 the generic one (ym_bn_bwd_apply + ym_conv_first_wgrad).
+    y within 1e-2, parameter gradients within 2e-2, running statistics within 1e-2 (relative L2)."""
     import models as M
-    d = golden("blocks.npz")
-    sd = {k[len("conv0") + 3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("conv0/p:")}
-    out = []
-    monkeypatch.setenv("YM_STEM_FUSED_BWD", "0")           # stored path: separate BN apply + weight gradient
-    for flag in ("0", "1"):
-        monkeypatch.setenv("YM_STEM_RECOMPUTE", flag)      # read when the block's plan is built
-        mod = M.Conv(1, 32, 3, 2)
-        mod.load_state_dict(sd)
-        mod.bn.eps, mod.bn.momentum = 1e-3, 0.03
-        mod = mod.cuda().train()
-        y = mod(torch.from_numpy(d["conv0/x"]).cuda())
-        y.backward(torch.from_numpy(d["conv0/dy"]).cuda())
-        out.append((y.detach().float().cpu(), {k: p.grad.detach().cpu() for k, p in mod.named_parameters()},
-                    {k: v.detach().cpu() for k, v in mod.state_dict().items() if "running" in k}))
-    (y0, g0, s0), (y1, g1, s1) = out
-    assert rel(y1, y0) < 1e-3, rel(y1, y0)
-    for k in g0:
-        assert rel(g1[k], g0[k]) < 1e-4, (k, rel(g1[k], g0[k]))
-    for k in s0:
-        assert rel(s1[k], s0[k]) < 1e-5, k
-
-
-@pytest.mark.parametrize("shape", [(2, 64, 64), (3, 47, 61)])
-def test_stem_fused_bwd_matches_unfused(monkeypatch, shape):
-    """The stored-z stem backward with the BatchNorm apply fused into the weight gradient
-    (ym_stem_bwd_wgrad_stored: dz never written) against ym_bn_bwd_apply + ym_conv_first_wgrad on the
-    same input and output gradient (odd map sizes: partial 8x32 tiles): the same bf16 dz rounding,
-    weight-gradient partials summed in a different fixed order — parameter gradients within 1e-5."""
-    import models as M
-    g = torch.Generator().manual_seed(sum(shape))
+    g = torch.Generator().manual_seed(sum(shape) + c)
     B, H, W = shape
     x = torch.rand(B, 1, H, W, generator=g)
-    mod0 = M.Conv(1, 32, 3, 2)
-    sd = mod0.state_dict()
-    out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("YM_STEM_FUSED_BWD", flag)
-        mod = M.Conv(1, 32, 3, 2)
-        mod.load_state_dict(sd)
-        mod = mod.cuda().train()
-        y = mod(x.cuda())
-        dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(7)).cuda()
-        y.backward(dy)
-        out.append({k: p.grad.detach().cpu() for k, p in mod.named_parameters()})
-    for k in out[0]:
-        assert rel(out[1][k], out[0][k]) < 1e-5, (k, rel(out[1][k], out[0][k]))
+    ref = M.Conv(1, c, 3, 2)
+    torch.nn.init.normal_(ref.conv.weight, std=0.5, generator=g)
+    ref.bn.eps, ref.bn.momentum = 1e-3, 0.03
+    mod = M.Conv(1, c, 3, 2)
+    mod.load_state_dict(ref.state_dict())
+    mod.bn.eps, mod.bn.momentum = 1e-3, 0.03
+    mod = mod.cuda().train()
+    y = mod(x.cuda())
+    dy = torch.randn(y.shape, generator=torch.Generator().manual_seed(7))
+    y.backward(dy.cuda())
+    # fp32 reference of Conv.forward (yolo11_modules.py:32-33) with autograd on the CPU
+    w = ref.conv.weight.detach().clone().requires_grad_(True)
+    gm = ref.bn.weight.detach().clone().requires_grad_(True)
+    bt = ref.bn.bias.detach().clone().requires_grad_(True)
+    rm, rv = ref.bn.running_mean.clone(), ref.bn.running_var.clone()
+    z = torch.nn.functional.conv2d(x, w, stride=2, padding=1)
+    yr = torch.nn.functional.silu(torch.nn.functional.batch_norm(z, rm, rv, gm, bt, True, 0.03, 1e-3))
+    yr.backward(dy)
+    assert rel(y.detach(), yr.detach()) < 1e-2
+    for k, r in (("conv.weight", w.grad), ("bn.weight", gm.grad), ("bn.bias", bt.grad)):
+        p = dict(mod.named_parameters())[k]
+        assert rel(p.grad, r) < 2e-2, (k, rel(p.grad, r))
+    assert rel(mod.bn.running_mean, rm) < 1e-2 and rel(mod.bn.running_var, rv) < 1e-2

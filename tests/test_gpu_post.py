@@ -16,17 +16,8 @@ def test_iou_row_bitexact(golden):
     np.testing.assert_array_equal(out.view(np.uint32), d["iou_out"].astype(np.float32).view(np.uint32))
 
 
-@pytest.fixture(params=["wave", "triangle"])
-def nms_scan(request, monkeypatch):
-    """Both greedy scans of the small-batch bitmask path: the one-wave scan (default) and the
-    whole-triangle workgroup scan (YM_NMS_SCAN=0, read per launch)."""
-    if request.param == "triangle":
-        monkeypatch.setenv("YM_NMS_SCAN", "0")
-    return request.param
-
-
 @pytest.mark.parametrize("n", [0, 1, 2, 100, 1000, 6700])
-def test_nms_keep_bitexact(golden, n, nms_scan):
+def test_nms_keep_bitexact(golden, n):
     from yolomi import post
     d = golden("nms.npz")
     keep = post.nms(torch.from_numpy(d[f"n{n}_boxes"]).cuda(), torch.from_numpy(d[f"n{n}_scores"]).cuda(), 0.45)
@@ -34,7 +25,7 @@ def test_nms_keep_bitexact(golden, n, nms_scan):
 
 
 @pytest.mark.parametrize("kind", ["am", "lit"])
-def test_decode_nms_bitexact(golden, kind, nms_scan):
+def test_decode_nms_bitexact(golden, kind):
     import train_yolo11_cuda as T
     d = golden("decode.npz")
     pred = torch.from_numpy(d[f"{kind}_in"]).cuda()

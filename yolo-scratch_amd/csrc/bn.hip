@@ -21,11 +21,25 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "bnfold.h"
 #include "common.h"
+
+// The one-launch finalize's hand-off (below) rests on relaxed agent-scope atomics being lowered to
+// `sc1` vector stores / loads and on vmcnt(0) + barrier + an agent fetch_add ordering them, as
+// MI355X_MICROARCH.md's "valid forms" table records for gfx950 / ROCm 7.2; no other target was checked.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "bn.hip: the fence-free finalize hand-off is verified on gfx950 only"
+#endif
 
 namespace ym {
 namespace {
+
+// write-through store / L1-bypassing load of hand-off data (sc1 vector memory operations)
+__device__ __forceinline__ void st_wt(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ void unpack8(uint4 v, float* f) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -59,94 +73,6 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
 __device__ __forceinline__ float dsilu(float u) {
     const float sg = __builtin_amdgcn_rcpf(1.0f + __expf(-u));
     return sg * (1.0f + u * (1.0f - sg));
-}
-
-// ---------------------------------------------------------------- two-level reduction of [G][C] partials
-// level 1: grid (ceil(C/64), R), 256 threads = 64 channels x 4 row groups -> out [R][2][C] fp64
-__global__ void __launch_bounds__(256) partials_reduce_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                              int G, int C, int R, double* __restrict__ out) {
-    __shared__ double sh[2][4][64];
-    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    const int c = blockIdx.x * 64 + cl;
-    const int per = (G + R - 1) / R;
-    const int g0 = blockIdx.y * per, g1 = min(G, g0 + per);
-    double s = 0.0, q = 0.0;
-    if (c < C) {
-#pragma unroll 4
-        for (int g = g0 + rg; g < g1; g += 4) {
-            s += a[int64_t(g) * C + c];
-            q += b[int64_t(g) * C + c];
-        }
-    }
-    sh[0][rg][cl] = s;
-    sh[1][rg][cl] = q;
-    __syncthreads();
-    if (rg == 0 && c < C) {
-        s = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-        q = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
-        out[(int64_t(blockIdx.y) * 2 + 0) * C + c] = s;
-        out[(int64_t(blockIdx.y) * 2 + 1) * C + c] = q;
-    }
-}
-
-// second level: 64 channels per block, the R level-1 rows split over the 4 waves, combined in
-// LDS; returns true on the wave-0 lanes that own a channel (s, q valid there)
-__device__ __forceinline__ bool fold(const double* p, int R, int C, double& s, double& q, int& c) {
-    __shared__ double sh[2][4][64];
-    const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
-    c = blockIdx.x * 64 + cl;
-    s = 0.0;
-    q = 0.0;
-    if (c < C)
-        for (int r = rg; r < R; r += 4) {
-            s += p[(int64_t(r) * 2 + 0) * C + c];
-            q += p[(int64_t(r) * 2 + 1) * C + c];
-        }
-    sh[0][rg][cl] = s;
-    sh[1][rg][cl] = q;
-    __syncthreads();
-    if (rg != 0 || c >= C) return false;
-    s = (sh[0][0][cl] + sh[0][1][cl]) + (sh[0][2][cl] + sh[0][3][cl]);
-    q = (sh[1][0][cl] + sh[1][1][cl]) + (sh[1][2][cl] + sh[1][3][cl]);
-    return true;
-}
-
-__global__ void bn_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
-                                   float* __restrict__ scale, float* __restrict__ shift, float* __restrict__ mean_out,
-                                   float* __restrict__ rstd_out) {
-    if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
-    double s, q;
-    int c;
-    if (!fold(p2, R, C, s, q, c)) return;
-    double mean = s / count;
-    double var = q / count - mean * mean;
-    if (var < 0) var = 0;
-    double rstd = 1.0 / sqrt(var + double(eps));
-    float sc = float(double(gamma[c]) * rstd);
-    scale[c] = sc;
-    shift[c] = float(double(beta[c]) - mean * double(sc));
-    mean_out[c] = float(mean);
-    rstd_out[c] = float(rstd);
-    if (running_mean) {
-        double unb = count > 1 ? var * count / (count - 1) : var;
-        running_mean[c] = float((1.0 - momentum) * running_mean[c] + momentum * mean);
-        running_var[c] = float((1.0 - momentum) * running_var[c] + momentum * unb);
-    }
-}
-
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ p2, int R, int C, double count,
-                                       const float* __restrict__ gamma, const float* __restrict__ rstd, float* dgamma,
-                                       float* dbeta, int accumulate, float* __restrict__ coef) {
-    double s, q;
-    int c;
-    if (!fold(p2, R, C, s, q, c)) return;
-    if (dgamma) dgamma[c] = float(accumulate ? dgamma[c] + q : q);
-    if (dbeta) dbeta[c] = float(accumulate ? dbeta[c] + s : s);
-    coef[c] = gamma[c] * rstd[c];               // k1
-    coef[C + c] = float(s / count);             // k2 = mean(g)
-    coef[2 * C + c] = float(q / count);         // k3 = mean(g * xhat)
 }
 
 // ---------------------------------------------------------------- one-launch finalize
@@ -328,8 +254,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
                                                             const float* __restrict__ shift,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ rstd, int act,
-                                                            float* __restrict__ ps, float* __restrict__ pg,
-                                                            BnFold fold) {
+                                                            float* __restrict__ ps, float* __restrict__ pg) {
     extern __shared__ float red[];   // [2][rows][C]
     const Lanes L = lanes(C);
     const int c0 = L.g * 8;
@@ -378,10 +303,9 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
             a += red[r * C + c];
             b += red[(L.rows + r) * C + c];
         }
-        st_row(&ps[int64_t(blockIdx.x) * C + c], a, fold.cnt != nullptr);
-        st_row(&pg[int64_t(blockIdx.x) * C + c], b, fold.cnt != nullptr);
+        ps[int64_t(blockIdx.x) * C + c] = a;
+        pg[int64_t(blockIdx.x) * C + c] = b;
     }
-    if (fold.cnt) bn_fold_tail(fold, ps, pg, C, blockIdx.x, red);
 }
 
 // dz[m][c] = k1*(g - k2 - xhat*k3), dz dense [M][C] (may alias z)
@@ -449,21 +373,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
 
 constexpr int RED_R = 32;   // level-1 row splits of the partials reduction
 
-// grid caps of the streaming kernels (measured in the training step: 2048 / 512 with the conv
-// forward's 1024 stat rows, +0.3 % over 4096 / 1024 / 2048); YM_BN_APPLY_BLOCKS /
-// YM_BN_REDUCE_BLOCKS override them (A/B runs)
-int env_cap(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? std::max(8, atoi(e)) : dflt;
-}
-int apply_cap() {
-    static const int v = env_cap("YM_BN_APPLY_BLOCKS", 2048);
-    return v;
-}
-int reduce_cap() {
-    static const int v = env_cap("YM_BN_REDUCE_BLOCKS", 512);
-    return v;
-}
+// grid caps of the streaming kernels (measured in the training step: 2048 / 512 with the conv forward's
+// 1024 stat rows, +0.3 % over 4096 / 1024 / 2048)
+constexpr int APPLY_CAP = 2048, REDUCE_CAP = 512;
 
 int stream_blocks(int64_t M, int C, int cap) {
     int rows = 256 / (C / 8);
@@ -485,14 +397,6 @@ using namespace ym;
 constexpr size_t BN_CNT_BYTES = 256;
 extern "C" size_t ym_bn_workspace_size(int c) { return BN_CNT_BYTES + size_t(RED_R) * 2 * c * sizeof(double); }
 
-static bool bn_fused() {
-    static const int on = [] {
-        const char* e = getenv("YM_BN_FUSED");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
-
 extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count,
                               const float* gamma, const float* beta, float* running_mean, float* running_var,
                               int64_t* num_batches_tracked, float momentum, float eps, float* scale, float* shift,
@@ -500,19 +404,11 @@ extern "C" int ym_bn_finalize(const float* part_sum, const float* part_sq, int p
     YM_CHECK_ARG(count > 0 && workspace, "ym_bn_finalize: count must be > 0, workspace required");
     hipStream_t st = as_stream(stream);
     double* p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
-    if (bn_fused()) {
-        unsigned* cnt = static_cast<unsigned*>(workspace);
-        hipLaunchKernelGGL((bn_finalize_fused_kernel<false>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
-                           part_sq, parts, c, RED_R, count, p2, cnt, gamma, beta, running_mean, running_var,
-                           num_batches_tracked, momentum, eps, scale, shift, mean, rstd, nullptr, nullptr, nullptr, 0,
-                           nullptr);
-        YM_LAUNCH_CHECK("ym_bn_finalize");
-        return YM_OK;
-    }
-    hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_sq, parts,
-                       c, RED_R, p2);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma, beta,
-                       running_mean, running_var, num_batches_tracked, momentum, eps, scale, shift, mean, rstd);
+    unsigned* cnt = static_cast<unsigned*>(workspace);
+    hipLaunchKernelGGL((bn_finalize_fused_kernel<false>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
+                       part_sq, parts, c, RED_R, count, p2, cnt, gamma, beta, running_mean, running_var,
+                       num_batches_tracked, momentum, eps, scale, shift, mean, rstd, nullptr, nullptr, nullptr, 0,
+                       nullptr);
     YM_LAUNCH_CHECK("ym_bn_finalize");
     return YM_OK;
 }
@@ -541,13 +437,13 @@ extern "C" int ym_bn_apply(const uint16_t* z, int64_t m, int c, int hw, const fl
     CHECK_VIEW(o_bs, o_ld, hw);
     if (res) CHECK_VIEW(r_bs, r_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0, as_stream(stream), z, m, c,
+    hipLaunchKernelGGL(bn_apply_kernel, dim3(stream_blocks(m, c, APPLY_CAP)), dim3(256), 0, as_stream(stream), z, m, c,
                        scale, shift, act, res, r_ld, out, o_ld, out32);
     YM_LAUNCH_CHECK("ym_bn_apply");
     return YM_OK;
 }
 
-extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, reduce_cap()); }
+extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, REDUCE_CAP); }
 
 extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
                                 int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
@@ -557,34 +453,8 @@ extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, 
     int blocks = ym_bn_bwd_blocks(m, c);
     int rows = 256 / (c / 8);
     hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2) * rows * c * sizeof(float),
-                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot,
-                       BnFold{});
+                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot);
     YM_LAUNCH_CHECK("ym_bn_bwd_reduce");
-    return YM_OK;
-}
-
-extern "C" int ym_bn_bwd_reduce_finalize(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m,
-                                         int c, int hw, const float* scale, const float* shift, const float* mean,
-                                         const float* rstd, int act, float* part_sum, float* part_dot,
-                                         const float* gamma, float* dgamma, float* dbeta, int accumulate, float* coef,
-                                         void* workspace, void* stream) {
-    CHECK_C(c);
-    CHECK_VIEW(d_bs, d_ld, hw);
-    YM_CHECK_ARG(m > 0 && workspace && gamma && rstd && coef && part_sum && part_dot,
-                 "ym_bn_bwd_reduce_finalize: null argument / no pixels");
-    const int blocks = ym_bn_bwd_blocks(m, c);
-    const int rows = 256 / (c / 8);
-    BnFold f{};
-    f.cnt = static_cast<unsigned*>(workspace);
-    f.p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
-    f.bwd = 1;
-    f.count = double(m);
-    f.gamma = gamma; f.rstd_in = rstd;
-    f.dgamma = dgamma; f.dbeta = dbeta; f.accumulate = accumulate; f.coef = coef;
-    bn_fold_groups(f, blocks, 1);
-    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(blocks), dim3(256), size_t(2) * rows * c * sizeof(float),
-                       as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, part_sum, part_dot, f);
-    YM_LAUNCH_CHECK("ym_bn_bwd_reduce_finalize");
     return YM_OK;
 }
 
@@ -594,18 +464,10 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
     YM_CHECK_ARG(workspace, "ym_bn_bwd_finalize: workspace required");
     hipStream_t st = as_stream(stream);
     double* p2 = reinterpret_cast<double*>(static_cast<char*>(workspace) + BN_CNT_BYTES);
-    if (bn_fused()) {
-        unsigned* cnt = static_cast<unsigned*>(workspace);
-        hipLaunchKernelGGL((bn_finalize_fused_kernel<true>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
-                           part_dot, parts, c, RED_R, count, p2, cnt, gamma, nullptr, nullptr, nullptr, nullptr, 0.f,
-                           0.f, nullptr, nullptr, nullptr, nullptr, rstd, dgamma, dbeta, accumulate, coef);
-        YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
-        return YM_OK;
-    }
-    hipLaunchKernelGGL(partials_reduce_kernel, dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum, part_dot, parts,
-                       c, RED_R, p2);
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((c + 63) / 64), dim3(256), 0, st, p2, RED_R, c, count, gamma,
-                       rstd, dgamma, dbeta, accumulate, coef);
+    unsigned* cnt = static_cast<unsigned*>(workspace);
+    hipLaunchKernelGGL((bn_finalize_fused_kernel<true>), dim3((c + 63) / 64, RED_R), dim3(256), 0, st, part_sum,
+                       part_dot, parts, c, RED_R, count, p2, cnt, gamma, nullptr, nullptr, nullptr, nullptr, 0.f,
+                       0.f, nullptr, nullptr, nullptr, nullptr, rstd, dgamma, dbeta, accumulate, coef);
     YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
     return YM_OK;
 }
@@ -616,7 +478,7 @@ extern "C" int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, c
     CHECK_C(c);
     CHECK_VIEW(d_bs, d_ld, hw);
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<false>, dim3(stream_blocks(m, c, APPLY_CAP)), dim3(256), 0,
                        as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, coef, dz, nullptr, 0, 0);
     YM_LAUNCH_CHECK("ym_bn_bwd_apply");
     return YM_OK;
@@ -631,7 +493,7 @@ extern "C" int ym_bn_bwd_apply_res(const uint16_t* dy, int64_t d_bs, int64_t d_l
     CHECK_VIEW(r_bs, r_ld, hw);
     YM_CHECK_ARG(dres, "ym_bn_bwd_apply_res: null residual gradient");
     if (m == 0) return YM_OK;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(stream_blocks(m, c, apply_cap())), dim3(256), 0,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<true>, dim3(stream_blocks(m, c, APPLY_CAP)), dim3(256), 0,
                        as_stream(stream), dy, d_ld, z, m, c, scale, shift, mean, rstd, act, coef, dz, dres, r_ld,
                        r_accumulate);
     YM_LAUNCH_CHECK("ym_bn_bwd_apply_res");

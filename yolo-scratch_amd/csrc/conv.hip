@@ -31,7 +31,6 @@
 #include "conv_direct.h"
 #include "conv_epi.h"
 #include "conv_halo.h"
-#include "bnfold.h"
 #include "conv_pipe.h"
 #include "reduce.h"
 #include "tile.h"
@@ -58,7 +57,6 @@ struct GemmArgs {
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
     int ntl;                                 // channel tiles interleaved into grid x (0: they are grid y)
     int ep_lds;                              // data gradient: LDS-transposed 16-B epilogue (conv_epi.h)
-    BnFold fold;                             // fused BN finalize (fold.cnt null: none)
 };
 
 // LDS images are lane-linear (LDS-DMA writes lane l of a wave-instruction at base + 16*l): 128-B
@@ -93,7 +91,7 @@ __device__ __forceinline__ void raw_barrier() {
 
 // WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile; KB-deep K stages
 // (rows of KB*2 bytes), an NS-stage LDS ring with NS-1 stages in flight
-template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE, int ABL = 0>
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NS * (BM + BN) * KB * 2 <= 72 * 1024) ? 2 : 1)
 conv_gemm_kernel(GemmArgs a) {
     constexpr int BK = KB;
@@ -236,7 +234,7 @@ conv_gemm_kernel(GemmArgs a) {
         raw_barrier();                     // previous tile's readers are done with every stage
 #pragma unroll
         for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
-            if (s0 < nk && ABL != 2) issue(s0);
+            if (s0 < nk) issue(s0);
         for (int k = 0; k < nk; ++k) {
             const int buf = k % NSTAGE;
             // this wave's DMAs of stage k have landed (the later stages may stay in flight)
@@ -245,7 +243,7 @@ conv_gemm_kernel(GemmArgs a) {
             else if (NSTAGE >= 3 && ahead >= 1) wait_vmcnt<(NSTAGE >= 3 ? 1 : 0) * (AI + BI)>();
             else wait_vmcnt<0>();
             raw_barrier();                 // ... everyone's, and everyone finished reading stage k-1
-            if (k + NSTAGE - 1 < nk && ABL != 2) issue((k + NSTAGE - 1) % NSTAGE);   // ABL 2: no staging
+            if (k + NSTAGE - 1 < nk) issue((k + NSTAGE - 1) % NSTAGE);
             const char* As = smem + buf * STAGE;
             const char* Bs = As + BN * RB;
             // fragments of both 32-deep halves first, then the MFMAs (two register sets; the order is
@@ -273,9 +271,7 @@ conv_gemm_kernel(GemmArgs a) {
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j) {
-                        if constexpr (ABL == 1) {          // ABL 1 (timing only): no MFMA
-                            acc[i][j][0] += float(af[kk][i][0]) * float(bfr[kk][j][0]);
-                        } else if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
+                        if constexpr (MODE == MODE_FWD)   // fp16 activations x fp16 weights
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
                                 __builtin_bit_cast(f16x8, af[kk][i]), __builtin_bit_cast(f16x8, bfr[kk][j]), acc[i][j],
                                 0, 0, 0);
@@ -401,11 +397,10 @@ conv_gemm_kernel(GemmArgs a) {
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                st_row(&a.st_sum[int64_t(bx) * a.Nout + ch], ps, a.fold.cnt != nullptr);
-                st_row(&a.st_sq[int64_t(bx) * a.Nout + ch], pq, a.fold.cnt != nullptr);
+                a.st_sum[int64_t(bx) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(bx) * a.Nout + ch] = pq;
             }
         }
-        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, bx, smem);
     }
 }
 
@@ -415,7 +410,7 @@ conv_gemm_kernel(GemmArgs a) {
 __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                              uint16_t* __restrict__ y, float* __restrict__ st_sum,
                                                              float* __restrict__ st_sq, int N, int H, int W, int OH,
-                                                             int OW, int Cout, int stride, int pad, BnFold fold) {
+                                                             int OW, int Cout, int stride, int pad) {
     __shared__ float red[2][512];
     const int G = Cout >> 3;                 // channel groups (divides 64)
     const int g = threadIdx.x % G;
@@ -466,10 +461,9 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < Cout; c += 256) {
-        st_row(&st_sum[int64_t(blockIdx.x) * Cout + c], red[0][c], fold.cnt != nullptr);
-        st_row(&st_sq[int64_t(blockIdx.x) * Cout + c], red[1][c], fold.cnt != nullptr);
+        st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
     }
-    if (fold.cnt) bn_fold_tail(fold, st_sum, st_sq, Cout, blockIdx.x, &red[0][0]);
 }
 
 // part[block][co*9 + t] = sum over the block's pixels p of dz[p][co] * patch(p)[t]  (no dgrad: the
@@ -553,7 +547,7 @@ __device__ __forceinline__ void unpack8(uint4 u, float* f, bool half) {
     }
 }
 
-__global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq, BnFold fold) {
+__global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
     __shared__ float red[2][512];
     const int G = a.C >> 3, g = threadIdx.x % G;
     const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
@@ -600,10 +594,9 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < a.C; c += 256) {
-        st_row(&st_sum[int64_t(blockIdx.x) * a.C + c], red[0][c], fold.cnt != nullptr);
-        st_row(&st_sq[int64_t(blockIdx.x) * a.C + c], red[1][c], fold.cnt != nullptr);
+        st_sum[int64_t(blockIdx.x) * a.C + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * a.C + c] = red[1][c];
     }
-    if (fold.cnt) bn_fold_tail(fold, st_sum, st_sq, a.C, blockIdx.x, &red[0][0]);
 }
 
 // dx (mapped channels, overwrite or accumulate into the view) and dW (+=) from dense dz (N,H,W,C)
@@ -698,14 +691,8 @@ __global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int 
 
 // grid x: a multiple of 8 (the kernel groups m-tiles per XCD); with BatchNorm statistics the
 // partials are one row per grid-x block, so the grid is bounded and blocks loop over tiles
-// grid-x bound of the forward with BN statistics (rows of its partials); YM_CONV_FWD_BLOCKS overrides
-static int fwd_stat_blocks() {
-    static const int v = [] {
-        const char* e = getenv("YM_CONV_FWD_BLOCKS");
-        return e ? std::max(64, atoi(e)) : 1024;
-    }();
-    return v;
-}
+// grid-x bound of the forward with BN statistics (rows of its partials)
+constexpr int FWD_STAT_BLOCKS = 1024;
 
 static int grid_x(int mtiles, int ntiles, bool stats, int max_blocks) {
     int gx = (mtiles + 7) & ~7;
@@ -727,25 +714,10 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     a.mtiles = int((Mc + BM - 1) / BM);
     int ntiles = (a.Nout + BN - 1) / BN;
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
-    if (a.fold.cnt) bn_fold_groups(a.fold, gx, ntiles);
-    // YM_CONV_ABLATE=nomma|nodma: timing-only builds without the MFMAs / without the staging
-    static const int abl = [] {
-        const char* e = getenv("YM_CONV_ABLATE");
-        return !e ? 0 : std::string(e) == "nomma" ? 1 : std::string(e) == "nodma" ? 2 : 0;
-    }();
-    // YM_CONV_NMAP=0: channel tiles as grid y (dispatched one after another) instead of interleaved
-    static const int nmap = [] {
-        const char* e = getenv("YM_CONV_NMAP");
-        return !(e && e[0] == '0');
-    }();
-    a.ntl = nmap && ntiles > 1 ? ntiles : 0;
+    // channel tiles of one m-tile sequence interleaved into grid x (dispatched together)
+    a.ntl = ntiles > 1 ? ntiles : 0;
     const dim3 grid(a.ntl ? gx * ntiles : gx, a.ntl ? 1 : ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
-    if (abl == 1)
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, 1>), grid, block, 0, st, a);
-    else if (abl == 2)
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, 2>), grid, block, 0, st, a);
-    else
-        hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), grid, block, 0, st, a);
     return gx;
 }
 
@@ -777,24 +749,11 @@ static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t 
     return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
 }
 
-// K-stage depth x ring depth; YM_CONV_CFG=32x4 / 32x3 / 64x3 / 32x2 selects the alternatives (A/B runs)
+// K-stage depth x ring depth, measured per layer (tools/layer_bench.py): 64-channel tiles prefer 32-deep stages
 template <int MODE>
 static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
-    static const int cfg = [] {
-        const char* e = getenv("YM_CONV_CFG");
-        if (!e) return 0;
-        const std::string v(e);
-        return v == "32x4" ? 1 : v == "32x3" ? 2 : v == "64x3" ? 3 : v == "32x2" ? 4 : 0;
-    }();
-    switch (cfg) {
-        case 4: return launch_tile_k<32, 2, MODE>(a, t, max_blocks, st);
-        case 1: return launch_tile_k<32, 4, MODE>(a, t, max_blocks, st);
-        case 2: return launch_tile_k<32, 3, MODE>(a, t, max_blocks, st);
-        case 3: return launch_tile_k<64, 3, MODE>(a, t, max_blocks, st);
-        default:   // measured per layer (tools/layer_bench.py): 64-channel tiles prefer 32-deep stages
-            return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE>(a, t, max_blocks, st)
-                                             : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
-    }
+    return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE>(a, t, max_blocks, st)
+                                     : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
 }
 
 static int pick_and_launch(GemmArgs a, int mode, int max_blocks, hipStream_t st) {
@@ -808,7 +767,7 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
     // grid-x used for the stats partials by ym_conv_fwd (callers size the partial buffers with it)
     const Tile t = pick_tile(M, 1, Cout);
     const int mtiles = int((M + t.bm - 1) / t.bm);
-    return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, fwd_stat_blocks());
+    return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, FWD_STAT_BLOCKS);
 }
 
 extern "C" int ym_conv_set_halo(int mode) {
@@ -857,7 +816,7 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
 }
 
 static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
-                         float* stat_sum, float* stat_sq, const BnFold* fold, void* stream) {
+                         float* stat_sum, float* stat_sq, void* stream) {
     YM_CHECK_ARG(d && x && w && y, "ym_conv_fwd: null argument");
     YM_CHECK_ARG(d->cin % 8 == 0, "ym_conv_fwd: Cin %% 8 != 0 (Cin=%d)", d->cin);
     YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_fwd: kernel size %d unsupported (1..3)", d->k);
@@ -876,17 +835,9 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     a.out_f32 = d->out_f32; a.accumulate = d->accumulate;
     a.N = d->n;
     a.ostep = 1;
-    if (fold) a.fold = *fold;
-    {
-        static const int ep_env = [] {             // YM_CONV_EPI: 0 fragment stores, 1 data gradient, 2 also forward
-            const char* e = getenv("YM_CONV_EPI");
-            return e ? atoi(e) : 1;
-        }();
-        a.ep_lds = ep_env >= 2 && d->out_f32 == 2 && !bias && !fold && d->y_ld % 8 == 0 && d->y_bs % 8 == 0 &&
-                   int64_t(d->n) * d->y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
-    }
+    a.ep_lds = 0;                 // forward: fragment stores (the LDS-transposed epilogue measured equal)
     if (a.M == 0) return YM_OK;
-    const DirectPlan dp = fold ? DirectPlan{} : direct_plan(d, 0);
+    const DirectPlan dp = direct_plan(d, 0);
     if (dp.ok) {
         direct_launch(dp, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (direct)");
@@ -896,36 +847,24 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) {
-        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, fold, as_stream(stream));
+        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (pipe)");
         return YM_OK;
     }
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) {
-        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, fold, as_stream(stream));
+        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
-    pick_and_launch(a, MODE_FWD, fwd_stat_blocks(), as_stream(stream));
+    pick_and_launch(a, MODE_FWD, FWD_STAT_BLOCKS, as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
 }
 
 extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                            float* stat_sum, float* stat_sq, void* stream) {
-    return conv_fwd_impl(d, x, w, y, bias, stat_sum, stat_sq, nullptr, stream);
-}
-
-extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* z,
-                              float* stat_sum, float* stat_sq, const ym_bn_train* bn, void* stream) {
-    YM_CHECK_ARG(d && bn && bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd,
-                 "ym_conv_fwd_bn: null argument");
-    YM_CHECK_ARG(stat_sum && stat_sq && d->out_f32 == 2, "ym_conv_fwd_bn: needs statistics and fp16 z (out_f32 = 2)");
-    YM_CHECK_ARG(d->cout <= 2048, "ym_conv_fwd_bn: cout > 2048");
-    const int64_t M = int64_t(d->n) * d->oh * d->ow;
-    YM_CHECK_ARG(M > 0, "ym_conv_fwd_bn: no pixels");
-    const BnFold f = bn_fold_fwd(bn, double(M));
-    return conv_fwd_impl(d, x, w, z, nullptr, stat_sum, stat_sq, &f, stream);
+    return conv_fwd_impl(d, x, w, y, bias, stat_sum, stat_sq, stream);
 }
 
 extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream) {
@@ -948,11 +887,7 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_dgrad: kernel size %d unsupported (1..3)", d->k);
     YM_CHECK_ARG(d->stride == 1 || d->stride == 2, "ym_conv_dgrad: stride %d unsupported (1, 2)", d->stride);
     a.ostep = d->stride;
-    static const int ep_env = [] {                 // YM_CONV_EPI=0: fragment stores (A/B runs)
-        const char* e = getenv("YM_CONV_EPI");
-        return e ? atoi(e) : 1;
-    }();
-    a.ep_lds = ep_env && int64_t(d->n) * d->x_bs * 2 < (int64_t(1) << 31) && d->x_ld % 8 == 0 && d->x_bs % 8 == 0 &&
+    a.ep_lds = int64_t(d->n) * d->x_bs * 2 < (int64_t(1) << 31) && d->x_ld % 8 == 0 && d->x_bs % 8 == 0 &&
                reinterpret_cast<uintptr_t>(dx) % 16 == 0;     // 16-B stores of whole 8-channel runs
     if (a.M == 0) return YM_OK;
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_dgrad: too many pixels");
@@ -966,13 +901,13 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     }
     const PipePlan pp = pipe_plan(d, 1);
     if (pp.ok) {
-        pipe_launch(pp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, nullptr, as_stream(stream));
+        pipe_launch(pp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_dgrad (pipe)");
         return YM_OK;
     }
     const HaloPlan hp = halo_plan(d, 1);
     if (hp.ok) {
-        halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, nullptr, as_stream(stream));
+        halo_launch(hp, d, 1, dz, wt, dx, nullptr, nullptr, nullptr, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_dgrad (halo)");
         return YM_OK;
     }
@@ -981,39 +916,17 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     return YM_OK;
 }
 
-static int conv_first_fwd_impl(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
-                               int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
-                               const ym_bn_train* bn, void* stream) {
+extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
+                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
+                                 void* stream) {
     YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd: cout=%d unsupported", cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd: too many pixels");
     YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_conv_first_fwd: statistics buffers / blocks");
-    BnFold f{};
-    if (bn) {
-        YM_CHECK_ARG(bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd &&
-                     int64_t(n) * oh * ow > 0, "ym_conv_first_fwd_bn: null argument / no pixels");
-        f = bn_fold_fwd(bn, double(int64_t(n) * oh * ow));
-        bn_fold_groups(f, blocks, 1);
-    }
     hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
-                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, f);
+                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad);
     YM_LAUNCH_CHECK("ym_conv_first_fwd");
     return YM_OK;
-}
-
-extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
-                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
-                                 void* stream) {
-    return conv_first_fwd_impl(img, w_oihw, y, stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, blocks, nullptr,
-                               stream);
-}
-
-extern "C" int ym_conv_first_fwd_bn(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum,
-                                    float* stat_sq, int n, int h, int w, int oh, int ow, int cout, int stride, int pad,
-                                    int blocks, const ym_bn_train* bn, void* stream) {
-    YM_CHECK_ARG(bn, "ym_conv_first_fwd_bn: null BN state");
-    return conv_first_fwd_impl(img, w_oihw, y, stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad, blocks, bn,
-                               stream);
 }
 
 extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
@@ -1043,37 +956,16 @@ static bool dw_shape_ok(int64_t x_bs, int64_t x_ld, int gsz, int gstride, int go
            goff % 8 == 0 && x_bs % 8 == 0 && x_ld % 8 == 0;
 }
 
-static int dw3x3_fwd_impl(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
-                          const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
-                          int blocks, const ym_bn_train* bn, void* stream) {
+extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
+                            const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
+                            int blocks, void* stream) {
     YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
                  "ym_dw3x3_fwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
     YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_dw3x3_fwd: statistics buffers / blocks");
     DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
-    BnFold f{};
-    if (bn) {
-        YM_CHECK_ARG(bn->workspace && bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd &&
-                     int64_t(n) * h * wd > 0, "ym_dw3x3_fwd_bn: null argument / no pixels");
-        f = bn_fold_fwd(bn, double(int64_t(n) * h * wd));
-        bn_fold_groups(f, blocks, 1);
-    }
-    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq, f);
+    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
     YM_LAUNCH_CHECK("ym_dw3x3_fwd");
     return YM_OK;
-}
-
-extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
-                            const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
-                            int blocks, void* stream) {
-    return dw3x3_fwd_impl(x, x_bs, x_ld, gsz, gstride, goff, w, y, stat_sum, stat_sq, n, h, wd, c, blocks, nullptr,
-                          stream);
-}
-
-extern "C" int ym_dw3x3_fwd_bn(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
-                               const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd,
-                               int c, int blocks, const ym_bn_train* bn, void* stream) {
-    YM_CHECK_ARG(bn, "ym_dw3x3_fwd_bn: null BN state");
-    return dw3x3_fwd_impl(x, x_bs, x_ld, gsz, gstride, goff, w, y, stat_sum, stat_sq, n, h, wd, c, blocks, bn, stream);
 }
 
 extern "C" size_t ym_dw3x3_bwd_workspace_size(int c) {

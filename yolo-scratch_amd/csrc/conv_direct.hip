@@ -384,20 +384,12 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
     const int64_t lo = a.tpc * xcd / 8, hi = a.tpc * (xcd + 1) / 8;
     const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
-    if constexpr (S == 2 && MODE == 1 && KS == 3 && (NT == 2 || NT == 4)) {
-        if (a.ncls == 2) {           // row-parity classes, column pairs per task (direct_body_s2dg)
-            if (blockIdx.y == 0) direct_body_s2dg<NT, KC, TP, 0>(a, first, step, hi, epl[wave]);
-            else direct_body_s2dg<NT, KC, TP, 1>(a, first, step, hi, epl[wave]);
-            return;
-        }
-    }
     if constexpr (S == 2 && MODE == 1) {
-        switch (blockIdx.y) {
-            case 0: direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]); break;
-            case 1: direct_body<NT, KC, KS, S, MODE, TP, 0, 1>(a, ssum, ssq, first, step, hi, epl[wave]); break;
-            case 2: direct_body<NT, KC, KS, S, MODE, TP, 1, 0>(a, ssum, ssq, first, step, hi, epl[wave]); break;
-            default: direct_body<NT, KC, KS, S, MODE, TP, 1, 1>(a, ssum, ssq, first, step, hi, epl[wave]); break;
-        }
+        static_assert(KS == 3 && (NT == 2 || NT == 4), "stride-2 data gradient: 3x3, 32 / 64 output channels");
+        // row-parity classes (blockIdx.y), column pairs per task (direct_body_s2dg)
+        if (blockIdx.y == 0) direct_body_s2dg<NT, KC, TP, 0>(a, first, step, hi, epl[wave]);
+        else direct_body_s2dg<NT, KC, TP, 1>(a, first, step, hi, epl[wave]);
+        return;
     } else {
         direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]);
     }
@@ -434,37 +426,23 @@ struct Variant {
     KernFn fn;
 };
 
-#define YM_DIR(NT, KC, KS, S, MODE, TP) {NT, KC, KS, S, MODE, TP, conv_direct_kernel<NT, KC, KS, S, MODE, TP>}
+#define DIR_VARIANT(NT, KC, KS, S, MODE, TP) {NT, KC, KS, S, MODE, TP, conv_direct_kernel<NT, KC, KS, S, MODE, TP>}
 // the YOLOv11 stem-stage layers (s@640: stem 1->32 s2 has its own kernel; model.1 32->64 3x3 s2,
 // C3k2 64->64 1x1 / 32->32 3x3 / 96->128 1x1) in both directions (an 80x80 128->128 1x1 variant
 // measured slower than the implicit GEMM: 0.083 vs 0.076 ms)
 const Variant kVariants[] = {
-    YM_DIR(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
-    YM_DIR(2, 2, 3, 2, 1, 1),   // dgrad of it: dz 64 -> dx 32, row-parity classes x column pairs
-    YM_DIR(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
-    YM_DIR(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
-    YM_DIR(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
-    YM_DIR(4, 2, 1, 1, 1, 4),
-    YM_DIR(8, 3, 1, 1, 0, 2),   // fwd 96 -> 128 1x1
-    YM_DIR(6, 4, 1, 1, 1, 2),   // dgrad: dz 128 -> dx 96
+    DIR_VARIANT(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
+    DIR_VARIANT(2, 2, 3, 2, 1, 1),   // dgrad of it: dz 64 -> dx 32, row-parity classes x column pairs
+    DIR_VARIANT(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
+    DIR_VARIANT(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
+    DIR_VARIANT(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
+    DIR_VARIANT(4, 2, 1, 1, 1, 4),
+    DIR_VARIANT(8, 3, 1, 1, 0, 2),   // fwd 96 -> 128 1x1
+    DIR_VARIANT(6, 4, 1, 1, 1, 2),   // dgrad: dz 128 -> dx 96
 };
-#undef YM_DIR
+#undef DIR_VARIANT
 
-// stride-2 data gradients as 2 row-parity classes over column pairs (default) or 4 parity classes
-// (YM_DIRECT_S2PAIR=0, A/B runs)
-bool s2_pairs() {        // read per plan (tests run both forms in one process)
-    const char* e = getenv("YM_DIRECT_S2PAIR");
-    return !(e && e[0] == '0');
-}
-
-int direct_mode() {
-    if (g_direct_force >= 0) return g_direct_force;
-    static const int v = [] {
-        const char* e = getenv("YM_CONV_DIRECT");
-        return e ? atoi(e) : 1;
-    }();
-    return v;
-}
+int direct_mode() { return g_direct_force >= 0 ? g_direct_force : 1; }
 
 }  // namespace
 
@@ -495,12 +473,10 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
         const int os = dgrad ? d->stride : 1;
         const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
         const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
-        p.classes = os == 2 && s2_pairs() ? 2 : os * os;
-        static const int gcap = [] {     // total workgroups over the classes (YM_DIRECT_GRID: A/B runs)
-            const char* e = getenv("YM_DIRECT_GRID");
-            return e ? std::max(64, atoi(e)) : 1024;
-        }();
-        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(gcap / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
+        // stride-2 data gradients as 2 row-parity classes over column pairs
+        p.classes = os == 2 ? 2 : 1;
+        constexpr int64_t GCAP = 1024;    // total workgroups over the classes (512-4096 measured within 3 %)
+        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(GCAP / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
         return p;
     }
     return p;

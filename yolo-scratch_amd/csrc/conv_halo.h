@@ -5,7 +5,6 @@
 
 namespace ym {
 
-struct BnFold;
 
 struct HaloPlan {
     int ok;              // the halo kernel handles this conv
@@ -22,6 +21,6 @@ extern int g_halo_force;
 // dgrad = 0: forward conv described by d; 1: its data gradient
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad);
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, const struct BnFold* fold, hipStream_t st);
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st);
 
 }  // namespace ym

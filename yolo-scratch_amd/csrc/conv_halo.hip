@@ -21,7 +21,6 @@
 // and flipped tap offsets.
 #include <algorithm>
 
-#include "bnfold.h"
 #include "common.h"
 #include "conv_epi.h"
 #include "conv_halo.h"
@@ -46,7 +45,6 @@ struct HaloArgs {
     int ntiles;
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
     int ep_lds;                               // 16-bit output via the LDS-transposed epilogue (conv_epi.h)
-    BnFold fold;                              // fused BN finalize (fold.cnt null: none)
 };
 
 // 64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1).
@@ -83,8 +81,7 @@ __device__ __forceinline__ void raw_barrier() {
 
 // WPX x WCO waves; wave tile TPW x 16 pixels by TCW x 16 channels; HI halo DMA instructions per
 // wave (halo capacity HI * waves * 16 rows); NW-deep weight ring
-// ABL (timing-only builds, YM_HALO_ABL): 1 = no MFMA (fragment reads kept live), 2 = no DMA issue
-template <int WPX, int WCO, int TPW, int TCW, int HI, int NW, int MODE, int ABL = 0>
+template <int WPX, int WCO, int TPW, int TCW, int HI, int NW, int MODE>
 __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_per_eu(1, 2))) conv_halo_kernel(HaloArgs a) {
     constexpr int NWV = WPX * WCO, NT = NWV * 64;
     constexpr int BN = WCO * TCW * 16;            // output channels per tile
@@ -187,12 +184,10 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
             for (int j = 0; j < TPW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
         raw_barrier();                    // every wave is done with the previous tile's buffers
-        if (ABL != 2) {
-            issue_halo(0);
+        issue_halo(0);
 #pragma unroll
-            for (int s = 0; s < NW - 1; ++s)
-                if (s < nk) issue_w(s);
-        }
+        for (int s = 0; s < NW - 1; ++s)
+            if (s < nk) issue_w(s);
         int cc = 0, kh = 0;
         for (int k = 0; k < nk; ++k) {
             // pending after the wait: the younger weight slots, and the next chunk's halo when it was
@@ -201,8 +196,8 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
             const int pend = WI * yw + ((kh >= 1 && kh < NW - 1 && cc + 1 < CC) ? HI : 0);
             wait_vm_dyn<WI * (NW - 2) + HI>(pend);
             raw_barrier();
-            if (ABL != 2 && kh == 0 && cc + 1 < CC) issue_halo(cc + 1);
-            if (ABL != 2 && k + NW - 1 < nk) issue_w(k + NW - 1);
+            if (kh == 0 && cc + 1 < CC) issue_halo(cc + 1);
+            if (k + NW - 1 < nk) issue_w(k + NW - 1);
 
             const char* As = wring + (k % NW) * WSLOT;
             const char* Hs = hbuf + (cc & 1) * HBUF;
@@ -230,9 +225,7 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 for (int i = 0; i < TCW; ++i)
 #pragma unroll
                     for (int j = 0; j < TPW; ++j) {
-                        if constexpr (ABL == 1)
-                            asm volatile("" ::"v"(af[i]), "v"(bfr[j]));
-                        else if constexpr (MODE == H_FWD)
+                        if constexpr (MODE == H_FWD)
                             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, af[i]),
                                                                                __builtin_bit_cast(f16x8, bfr[j]),
                                                                                acc[i][j], 0, 0, 0);
@@ -362,11 +355,10 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WPX; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                st_row(&a.st_sum[int64_t(blockIdx.x) * a.Nout + ch], ps, a.fold.cnt != nullptr);
-                st_row(&a.st_sq[int64_t(blockIdx.x) * a.Nout + ch], pq, a.fold.cnt != nullptr);
+                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = pq;
             }
         }
-        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, blockIdx.x, smem);
     }
 }
 
@@ -396,15 +388,10 @@ int g_halo_force = -1;
 
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
     HaloPlan p{};
-    // YM_CONV_HALO=0: never, =1: wherever it applies, =2: maps <= 24 wide (the 20x20 layers), unset (3):
-    // maps <= 48 wide or <= 64 output channels — with the pipelined kernel taking the >= 128-channel
-    // layers first, this rule measured 2953 vs 2940 img/s over rule 2 (s@640 bs64); in round 1, before
-    // the pipelined kernel, it was 0.5 % slower
-    static const int mode = [] {
-        const char* e = getenv("YM_CONV_HALO");
-        return !e ? 3 : (e[0] == '0' ? 0 : e[0] == '2' ? 2 : e[0] == '3' ? 3 : 1);
-    }();
-    const int force = g_halo_force >= 0 ? g_halo_force : mode;
+    // policy (ym_conv_set_halo): 0 never, 1 wherever it applies, 2 maps <= 24 wide (the 20x20 layers), 3 (the
+    // default) maps <= 48 wide or <= 64 output channels — with the pipelined kernel taking the >= 128-channel
+    // layers first, this rule measured 2953 vs 2940 img/s over rule 2 (s@640 bs64)
+    const int force = g_halo_force >= 0 ? g_halo_force : 3;
     if (force == 0) return p;
     const int ow_ = dgrad ? d->w : d->ow, cout_ = dgrad ? d->cin : d->cout;
     if (force == 2 && ow_ > 24) return p;
@@ -441,7 +428,7 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, const BnFold* fold, hipStream_t st) {
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
     HaloArgs a{};
     a.x = x;
     a.w = w;
@@ -460,33 +447,11 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     }
     a.accumulate = d->accumulate;
     a.TH = p.TH; a.TW = p.TW; a.HWd = p.TW + 2; a.HP = (p.TH + 2) * (p.TW + 2);
-    static const int ep_env = [] {   // YM_HALO_EPI: 0 fragment stores, 1 data gradient only, 2 both (default:
-        const char* e = getenv("YM_HALO_EPI");   // 64-ch 80x80 fwd 0.076 -> 0.070 ms, dgrad 0.066 -> 0.058)
-        return e ? atoi(e) : 2;
-    }();
-    a.ep_lds = (dgrad ? ep_env >= 1 : ep_env >= 2) && !bias && a.out_mode != 1 && a.y_ld % 8 == 0 && a.y_bs % 8 == 0 &&
+    // LDS-transposed 16-B epilogue stores (64-ch 80x80 fwd 0.076 -> 0.070 ms, dgrad 0.066 -> 0.058)
+    a.ep_lds = !bias && a.out_mode != 1 && a.y_ld % 8 == 0 && a.y_bs % 8 == 0 &&
                int64_t(d->n) * a.y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
-    if (fold && st_sum) {
-        a.fold = *fold;
-        bn_fold_groups(a.fold, p.gx, p.nco);
-    }
     const dim3 grid(p.gx, p.nco);
-    static const int abl = [] {
-        const char* e = getenv("YM_HALO_ABL");
-        return e ? atoi(e) : 0;
-    }();
-    static const int nw6 = [] {   // YM_HALO_NW=4: 4-deep weight ring
-        const char* e = getenv("YM_HALO_NW");
-        return e && atoi(e) == 4;
-    }();
-    if (abl == 1 || abl == 2 || nw6) {       // timing experiments (forward, 8-wave config only)
-        if (p.cfg != 0 || dgrad) return -1;
-        if (abl == 1) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD, 1>), grid, dim3(512), 0, st, a);
-        else if (abl == 2) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD, 2>), grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 4, H_FWD>), grid, dim3(512), 0, st, a);
-        return 0;
-    }
     if (p.cfg == 0) {
         if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_DGRAD>), grid, dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD>), grid, dim3(512), 0, st, a);

@@ -6,7 +6,6 @@
 
 namespace ym {
 
-struct BnFold;
 
 struct PipePlan {
     int ok;          // the pipelined kernel handles this conv
@@ -22,6 +21,6 @@ extern int g_pipe_force;
 // dgrad = 0: forward conv described by d; 1: its data gradient
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, const struct BnFold* fold, hipStream_t st);
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st);
 
 }  // namespace ym

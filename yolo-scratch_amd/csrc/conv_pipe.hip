@@ -28,14 +28,13 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "bnfold.h"
 #include "common.h"
 #include "conv_pipe.h"
 #include "tile.h"
 
 namespace ym {
 
-// selection policy: -1 YM_CONV_PIPE / default (3); 0 never; 1 layers of >= 1024 tiles with >= 128
+// selection policy (ym_conv_set_pipe): -1 default (3); 0 never; 1 layers of >= 1024 tiles with >= 128
 // output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
 // wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
 int g_pipe_force = -1;
@@ -59,7 +58,6 @@ struct PipeArgs {
     int ntiles;                               // channel tiles
     int mt_pre[5];                            // first m-tile of each class (prefix), mt_pre[ncls] = total
     int ncls;
-    BnFold fold;                              // fused BN finalize (fold.cnt null: none)
 };
 
 struct Cls {
@@ -193,11 +191,10 @@ struct Issuer {
     }
 
     // one stage into `st`, then advance the stream position
-    template <int ABL>
     __device__ __forceinline__ void issue(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off) {
         if (kci == 0) tap_setup();
         const uint32_t kb = uint32_t(kci) * 128u;
-        if constexpr (ABL < 2) {
+        {
             // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
             const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
             const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
@@ -222,8 +219,7 @@ struct Issuer {
     }
 };
 
-// ABL (timing ablations only, YM_PIPE_ABL): 1 = no MFMAs (fragments kept live), 2 = no DMA issue
-template <int BM, int BN, int WM, int WN, int MODE, int ABL = 0>
+template <int BM, int BN, int WM, int WN, int MODE>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
     constexpr int NS = 3;                     // LDS ring: stage g computing, g+1 and g+2 in flight
     constexpr int RB = 128;                   // 64 K x 2 B per LDS row
@@ -282,9 +278,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     }
     bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
     auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) __device__ {
-        if constexpr (ABL >= 4) {
-            if (buf >= 0) return;
-        }
         const char* As = smem + buf * STAGE + offA[kk];
         const char* Bs = smem + buf * STAGE + offB[kk];
 #pragma unroll
@@ -294,13 +287,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     };
     f32x4 acc[TM][TN];
     auto mma = [&](const bf16x8* fa, const bf16x8* fb) __device__ {
-        if constexpr (ABL == 1) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
-#pragma unroll
-            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
-            return;
-        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -326,7 +312,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     // prologue: stages 0..2 in flight; stage 0 landed everywhere; its first-half fragments read
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-        if (s < total) is.template issue<ABL>(smem + s * STAGE, wres, a_off);
+        if (s < total) is.issue(smem + s * STAGE, wres, a_off);
     if (total >= 3) vm_wait<2 * DPS>();
     else if (total == 2) vm_wait<DPS>();
     else vm_wait<0>();
@@ -356,9 +342,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
             if (g + 2 < total) vm_wait<DPS>();
             else vm_wait<0>();
         }
-        if constexpr (ABL != 3) step_barrier();
+        step_barrier();
         // the slot of stage g is free again (every wave's reads of it returned before the barrier)
-        if (g + 3 < total) is.template issue<ABL>(smem + buf * STAGE, wres, a_off);
+        if (g + 3 < total) is.issue(smem + buf * STAGE, wres, a_off);
         const int nbuf = buf == NS - 1 ? 0 : buf + 1;
         if (g + 1 < total) read_frags(f0a, f0b, nbuf, 0);
         mma(f1a, f1b);
@@ -371,13 +357,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         // transposed through this wave's LDS area 16 pixels at a time, so every store is a 16-B piece of
         // a pixel's contiguous channel run (8 lanes = one 128-B segment), issued as buffer stores whose
         // out-of-tile pixels fall out of range (no branches, a fixed count per tile)
-        if constexpr (ABL == 5) {             // timing only: no epilogue at all
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-            continue;
-        }
         {
             char* ep = smem + NS * STAGE + wave * EPW;
             const int wch0 = n0 + wr * WCH;                   // first channel of this wave
@@ -474,11 +453,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
-                st_row(&a.st_sum[int64_t(row) * a.Nout + ch], ps, a.fold.cnt != nullptr);
-                st_row(&a.st_sq[int64_t(row) * a.Nout + ch], pq, a.fold.cnt != nullptr);
+                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
             }
         }
-        if (a.fold.cnt) bn_fold_tail(a.fold, a.st_sum, a.st_sq, a.Nout, row, smem);
     }
 }
 
@@ -488,35 +466,7 @@ struct Cfg {
 };
 constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
 
-static int pipe_mode() {
-    static const int env = [] {
-        const char* e = getenv("YM_CONV_PIPE");
-        return e ? atoi(e) : 3;
-    }();
-    return g_pipe_force >= 0 ? g_pipe_force : env;
-}
-
-template <int ABL>
-void launch_abl(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
-    if (mode == PF) {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PF, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PF, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
-    } else {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PD, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PD, ABL><<<dim3(grid), dim3(512), 0, st>>>(a);
-    }
-}
-
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
-    static const int abl = [] {
-        const char* e = getenv("YM_PIPE_ABL");
-        return e ? atoi(e) : 0;
-    }();
-    if (abl == 1) return launch_abl<1>(mode, cfg, a, grid, st);
-    if (abl == 2) return launch_abl<2>(mode, cfg, a, grid, st);
-    if (abl == 3) return launch_abl<3>(mode, cfg, a, grid, st);
-    if (abl == 4) return launch_abl<4>(mode, cfg, a, grid, st);
-    if (abl == 5) return launch_abl<5>(mode, cfg, a, grid, st);
     if (mode == PF) {
         if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
         else conv_pipe_kernel<256, 64, 1, 8, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
@@ -530,7 +480,7 @@ void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) 
 
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     PipePlan p{};
-    const int mode = pipe_mode();
+    const int mode = g_pipe_force >= 0 ? g_pipe_force : 3;
     if (!d || mode == 0) return p;
     const int kin = dgrad ? d->cout : d->cin, nout = dgrad ? d->cin : d->cout;
     if (kin % 64 != 0 || nout % 8 != 0) return p;
@@ -569,7 +519,7 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, const BnFold* fold, hipStream_t st) {
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
     PipeArgs a{};
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
     if (!dgrad) {
@@ -592,10 +542,6 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
     a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad; a.N = d->n;
     a.accumulate = d->accumulate;
     a.ntiles = (a.Nout + bn - 1) / bn;
-    if (fold && st_sum) {
-        a.fold = *fold;
-        bn_fold_groups(a.fold, p.rows, a.ntiles);
-    }
     a.ncls = a.os == 2 ? 4 : 1;
     int acc = 0;
     for (int c = 0; c < a.ncls; ++c) {

@@ -449,150 +449,7 @@ __global__ void __launch_bounds__(64) nms_mask_kernel(int64_t N, int Wn, float i
     w.mask[(b * Wn + cb) * N + i] = word;          // column-major: column cb, row i
 }
 
-// diagnostic segment timers of nms_scan_kernel (block 0, thread 0), read by ym_debug_nms_stamps;
-// enabled only when YM_NMS_STAMPS is set (a wave-uniform branch otherwise)
-__device__ unsigned long long g_nms_stamps[8];
-__device__ __forceinline__ unsigned long long stamp_now() {
-    unsigned long long t;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    return t;
-}
-
-// Greedy scan over 64-candidate chunks, one 256-thread workgroup per image, on the column-major
-// mask: chunk c's column holds, for every earlier sorted position j, the bits of chunk c that j
-// suppresses.  Removed bits of chunk c = OR over KEPT j < 64c of column c; then the chunk's own
-// 64x64 diagonal block is resolved.  Thread tid owns rows j = tid + 256 q of every column: it keeps
-// the column in registers (two sets: column c+1 streams in while chunk c is processed) and its
-// rows' keep decisions in a bit mask, so the removed-bits reduction is registers + one wave OR +
-// a 4-entry LDS combine; the diagonal segment of chunk c (rows 64c..64c+63) is exactly the register
-// q = c/4 of wave c%4, which resolves the chunk.  Same keep-lists as the one-workgroup greedy loop
-// (a box is kept iff no earlier kept box has IoU > thr with it).
-__device__ __forceinline__ uint64_t wave_or64(uint64_t m) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t lo = uint32_t(m), hi = uint32_t(m >> 32);
-        m |= (uint64_t(uint32_t(__shfl_xor(int(hi), o, 64))) << 32) | uint32_t(__shfl_xor(int(lo), o, 64));
-    }
-    return m;
-}
-
-__global__ void __launch_bounds__(256) nms_scan_kernel(int64_t N, int64_t KP, int Wn, float img_size, Ws w,
-                                                       int32_t* __restrict__ out_count, float* __restrict__ out_boxes,
-                                                       float* __restrict__ out_scores, int64_t* __restrict__ out_labels,
-                                                       int64_t* __restrict__ out_index, int stamps) {
-    __shared__ uint64_t red[4];
-    __shared__ uint64_t kept_sh;
-    __shared__ int nkept_sh;
-    const bool st0 = stamps && blockIdx.x == 0 && threadIdx.x == 0;
-    unsigned long long tsum[4] = {0, 0, 0, 0}, tprev = 0;
-    auto stamp = [&](int seg) {
-        if (st0) {
-            const unsigned long long t = stamp_now();
-            if (seg >= 0) tsum[seg] += t - tprev;
-            tprev = t;
-        }
-    };
-    const int64_t b = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int K = w.kcount[b];
-    const int64_t base = b * N;
-    if (K == 0) {
-        if (tid == 0) out_count[b] = 0;
-        return;
-    }
-    const int nch = (K + 63) / 64;
-    if (tid == 0) nkept_sh = 0;
-    constexpr int LQ = (64 * BM_MAX_WN + 255) / 256;
-    static_assert(LQ <= 64, "keep mask is one 64-bit word per thread");
-    uint64_t colA[LQ], colB[LQ];
-    uint64_t mykeep = 0;                                  // bit q: row tid + 256 q was kept
-    // column c = rows 0 .. min(64(c+1), K) - 1; loads guarded by a wave-uniform bound (scalar
-    // branch) with a clamped index, so they issue back to back.  (hipcc still waits vmcnt(0) for the
-    // older column — measured: an exact-count variant with LQ unguarded loads is slower.)
-    auto load_col = [&](int c, uint64_t* dst) {
-        const uint64_t* src = w.mask + (b * Wn + c) * N;
-        const int L = min(64 * (c + 1), K);
-        const int qn = (L + 255) / 256;
-#pragma unroll
-        for (int q = 0; q < LQ; ++q)
-            if (q < qn) dst[q] = src[min(tid + 256 * q, L - 1)];
-    };
-    auto chunk = [&](int c, const uint64_t* cur) {
-        stamp(0);
-        // removed bits of chunk c: kept rows j < 64c
-        const int qj = (64 * c + 255) / 256;
-        uint64_t acc = 0;
-#pragma unroll
-        for (int q = 0; q < LQ; ++q)
-            if (q < qj && ((mykeep >> q) & 1) && tid + 256 * q < 64 * c) acc |= cur[q];
-        acc = wave_or64(acc);
-        if (lane == 0) red[wave] = acc;
-        __syncthreads();
-        stamp(1);
-        const int qc = c >> 2;
-        if (wave == (c & 3)) {
-            const uint64_t rem = red[0] | red[1] | red[2] | red[3];
-            uint64_t diag = 0;
-#pragma unroll
-            for (int q = 0; q < LQ; ++q)
-                if (q == qc) diag = cur[q];
-            const int rows = min(64, K - 64 * c);
-            if (lane >= rows) diag = 0;
-            // the chunk's decisions are the unique fixpoint of alive = init & ~OR{diag_s : s alive}
-            // (diag_s only has bits after s: acyclic); Jacobi rounds from alive = init reach it in
-            // (longest suppression chain + 1) rounds; two equal rounds mean the fixpoint
-            const uint64_t init = ~rem & (rows == 64 ? ~uint64_t(0) : ((uint64_t(1) << rows) - 1));
-            uint64_t alive = init;
-            for (int it = 0; it <= 64; ++it) {
-                const uint64_t nxt = init & ~wave_or64(((alive >> lane) & 1) ? diag : 0);
-                if (nxt == alive) break;
-                alive = nxt;
-            }
-            const int before = __popcll(alive & ((uint64_t(1) << lane) - 1));
-            if ((alive >> lane) & 1) out_index[base + nkept_sh + before] = 64 * c + lane;
-            if (lane == 0) kept_sh = alive;
-        }
-        __syncthreads();
-        stamp(2);
-        const uint64_t kept = kept_sh;
-        if (wave == (c & 3)) mykeep |= ((kept >> lane) & 1) << qc;
-        if (tid == 0) nkept_sh += __popcll(kept);
-        // nkept_sh / kept_sh are rewritten only after the next chunk's first barrier
-        stamp(3);
-    };
-    load_col(0, colA);
-    stamp(-1);
-    for (int c = 0; c < nch; c += 2) {
-        if (c + 1 < nch) load_col(c + 1, colB);      // in flight while chunk c is processed
-        chunk(c, colA);
-        if (c + 1 >= nch) break;
-        if (c + 2 < nch) load_col(c + 2, colA);
-        chunk(c + 1, colB);
-    }
-    if (st0)
-        for (int k = 0; k < 4; ++k) g_nms_stamps[k] = tsum[k];
-    __syncthreads();
-    // outputs in kept order (sorted position -> filtered index -> row)
-    const int nk = nkept_sh;
-    for (int k = tid; k < nk; k += 256) {
-        const int spos = int(out_index[base + k]);
-        const int f = int(uint32_t(w.keys[b * KP + spos]));
-        const int64_t row = base + w.frow[base + f];
-        float4 bx = w.box[row];
-        bx.x = fminf(fmaxf(bx.x / img_size, 0.0f), 1.0f);
-        bx.y = fminf(fmaxf(bx.y / img_size, 0.0f), 1.0f);
-        bx.z = fminf(fmaxf(bx.z / img_size, 0.0f), 1.0f);
-        bx.w = fminf(fmaxf(bx.w / img_size, 0.0f), 1.0f);
-        reinterpret_cast<float4*>(out_boxes)[base + k] = bx;
-        out_scores[base + k] = w.score[row];
-        out_labels[base + k] = w.label[row];
-    }
-    __syncthreads();
-    for (int k = tid; k < nk; k += 256) out_index[base + k] = int(uint32_t(w.keys[b * KP + out_index[base + k]]));
-    if (tid == 0) out_count[b] = nk;
-}
-
-// Greedy scan, ONE wave per image, visiting only what the kept rows need (nms_scan_kernel reads the
+// Greedy scan, ONE wave per image, visiting only what the kept rows need (round 1's workgroup scan read the
 // whole upper triangle: every earlier row of every column, ~K^2/128 words per image).  A chunk c's
 // removed bits come from two places:
 //  * NEAR rows (the previous group of 4 chunks and the earlier chunks of this group): the words
@@ -634,19 +491,8 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
                                                            float* __restrict__ out_boxes,
                                                            float* __restrict__ out_scores,
                                                            int64_t* __restrict__ out_labels,
-                                                           int64_t* __restrict__ out_index, int stamps) {
+                                                           int64_t* __restrict__ out_index) {
     __shared__ int rows_sh[256];
-    // diagnostic segment cycles (YM_NMS_STAMPS, image 0): [0] group start (prefetch + gather issue),
-    // [1] chunk decisions, [2] group end (far OR + prefetch rotation), [3] output epilogue
-    const bool st0 = stamps && blockIdx.x == 0;
-    unsigned long long tsum[4] = {0, 0, 0, 0}, tprev = st0 ? stamp_now() : 0;
-    auto stamp = [&](int seg) {
-        if (st0) {
-            const unsigned long long t = stamp_now();
-            tsum[seg] += t - tprev;
-            tprev = t;
-        }
-    };
     const int64_t b = blockIdx.x;
     const int lane = threadIdx.x;
     const int K = w.kcount[b];
@@ -733,16 +579,15 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
                 dst[k] = ld8(j >= 0 && cb >= cb_lo && cb < Wn ? uint32_t(cb * int(N) + j) * 8u : OOB);
             }
         };
-        const int npend = stamps == 2 ? 0 : min(nr, SCAN_RB);   // stamps 2: timing ablation, no far gather
+        const int npend = min(nr, SCAN_RB);
 #pragma unroll
         for (int r = 0; r < SCAN_RB; ++r) row_words(r < npend ? rows_sh[r] : -1, pend[r]);
-        for (int r = SCAN_RB; r < (stamps == 2 ? 0 : nr); ++r) {   // > SCAN_RB kept rows: synchronously
+        for (int r = SCAN_RB; r < nr; ++r) {   // > SCAN_RB kept rows: synchronously
             uint64_t t[SCAN_WL];
             row_words(rows_sh[r], t);
 #pragma unroll
             for (int k = 0; k < SCAN_WL; ++k) far[k] |= t[k];
         }
-        stamp(0);
         uint64_t kcur[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -777,10 +622,8 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
             nkept += __popcll(alive);
             kcur[q] = alive;
         }
-        stamp(1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) kprev[q] = kcur[q];
-        stamp(2);
     }
     __syncthreads();                                 // this wave's out_index stores are visible to its loads
     // outputs in kept order (sorted position -> filtered index -> row)
@@ -799,22 +642,13 @@ __global__ void __launch_bounds__(64) nms_scan_wave_kernel(int64_t N, int64_t KP
         out_index[base + k] = f;
     }
     if (lane == 0) out_count[b] = nkept;
-    if (st0) {
-        stamp(3);
-        if (lane == 0)
-            for (int k = 0; k < 4; ++k) g_nms_stamps[k] = tsum[k];
-    }
 }
 
 int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int clamp_norm, Ws w,
                int32_t* out_count, float* out_boxes, float* out_scores, int64_t* out_labels, int64_t* out_index,
                hipStream_t st) {
     size_t lds = size_t(SORT_LDS_KEYS) * sizeof(uint64_t);
-    static const int no_bitmask = [] {
-        const char* e = getenv("YM_NMS_BITMASK");
-        return e && e[0] == '0';
-    }();
-    if (w.mask && clamp_norm && !no_bitmask) {
+    if (w.mask && clamp_norm) {
         const int Wn = int((Nalloc + 63) / 64);
         const int64_t KP = pow2_at_least(Nalloc);
         hipLaunchKernelGGL(nms_image_kernel<true>, dim3(unsigned(B)), dim3(NMS_THREADS), lds, st, Nalloc, KP, iou_thr,
@@ -824,18 +658,8 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
         hipLaunchKernelGGL(nms_rank_scatter_kernel, dim3(nt, unsigned(B)), dim3(256), 0, st, Nalloc, KP, w);
         hipLaunchKernelGGL(nms_mask_kernel, dim3(unsigned(Wn * (Wn + 1) / 2), 1, unsigned(B)), dim3(64), 0, st, Nalloc,
                            Wn, iou_thr, w);
-        static const int stamps = [] {           // diagnostics; 2 = timing ablation (wrong results)
-            const char* e = getenv("YM_NMS_STAMPS");
-            return e ? (e[0] == '2' ? 2 : 1) : 0;
-        }();
-        const char* se = getenv("YM_NMS_SCAN");    // YM_NMS_SCAN=0: the whole-triangle workgroup scan (A/B,
-        const bool old_scan = se && se[0] == '0';   // read per launch so tests can compare the two)
-        if (old_scan)
-            hipLaunchKernelGGL(nms_scan_kernel, dim3(unsigned(B)), dim3(256), 0, st, Nalloc, KP, Wn, img_size, w,
-                               out_count, out_boxes, out_scores, out_labels, out_index, stamps);
-        else
-            hipLaunchKernelGGL(nms_scan_wave_kernel, dim3(unsigned(B)), dim3(64), 0, st, Nalloc, KP, Wn, img_size, w,
-                               out_count, out_boxes, out_scores, out_labels, out_index, stamps);
+        hipLaunchKernelGGL(nms_scan_wave_kernel, dim3(unsigned(B)), dim3(64), 0, st, Nalloc, KP, Wn, img_size, w,
+                           out_count, out_boxes, out_scores, out_labels, out_index);
         YM_LAUNCH_CHECK("nms bitmask path");
         return YM_OK;
     }
@@ -852,13 +676,6 @@ int launch_nms(int64_t B, int64_t Nalloc, float iou_thr, float img_size, int cla
 using namespace ym;
 
 extern "C" size_t ym_nms_workspace_size(int64_t B, int64_t N) { return 2 * ws_bytes(B, N); }
-
-// diagnostics: segment cycle totals of the last bitmask-path scan (YM_NMS_STAMPS set):
-// [0] between chunks (load issue), [1] removed-bits reduction, [2] diagonal resolve, [3] keep update
-extern "C" int ym_debug_nms_stamps(unsigned long long* out4) {
-    return hipMemcpyFromSymbol(out4, HIP_SYMBOL(ym::g_nms_stamps), 4 * sizeof(unsigned long long)) == hipSuccess
-               ? YM_OK : YM_ERR_HIP;
-}
 
 __global__ void ym_iou_row_kernel(const float4* __restrict__ b1, const float4* __restrict__ b2, int64_t m,
                                   float* __restrict__ out) {

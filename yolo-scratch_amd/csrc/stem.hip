@@ -1,16 +1,13 @@
-// The stem Conv block (model.0: 1 -> 32 channels, 3x3 stride 2 on the fp32 image, BatchNorm2d,
-// SiLU — /root/reference/yolo_scratch_cuda/models/yolo11_modules.py:21-33, yaml backbone row 0)
-// with its pre-BatchNorm output z RECOMPUTED instead of stored.
+// The stem Conv block's backward (model.0: 1 -> c channels, 3x3 stride 2 on the fp32 image, BatchNorm2d,
+// SiLU — /root/reference/yolo_scratch_cuda/models/yolo11_modules.py:21-33, yaml backbone row 0): the
+// BatchNorm-backward apply fused into the weight gradient over the stored z.
 //
-// z of the stem is the largest tensor of the step (64 x 320 x 320 x 32 fp16 = 420 MB at s@640 bs64)
-// and costs 9 multiply-adds per element to recompute from a 26 MB single-channel image.  Storing it
-// means writing it once and reading it three times (BN apply, BN backward statistics, BN backward
-// apply), and the backward's dz another write + read for the weight gradient: 2.5 GB of HBM traffic
-// per step.  Here the forward runs the statistics pass without the z store (stem_stats_kernel) and
-// stem_apply_kernel recomputes z to write the activation; the backward's two passes
-// recompute z from the image, and the second one turns dz straight into the weight-gradient
-// partials (dz never touches memory).  z is rounded to fp16 and dz to bf16 exactly where the
-// stored path rounds them, so the results match the stored path (tests/test_gpu_model.py).
+// z of the stem is the largest tensor of the step (64 x 320 x 320 x 32 fp16 = 420 MB at s@640 bs64).
+// The backward reads dy and the stored z once, forms dz = k1 (g - k2 - xhat k3) in registers (rounded
+// to bf16 where the generic path stores it) and turns it straight into the weight-gradient partials
+// against the image patches staged in LDS: dz never touches memory (0.45 -> 0.22 ms at s@640 bs64).
+// (Round 2 also recomputed z from the image in the forward instead of storing it: 2.5 GB/step less
+// traffic but VALU-bound passes, equal step time — removed)
 #include <algorithm>
 
 #include "common.h"
@@ -184,110 +181,12 @@ __device__ __forceinline__ void stem_visit(const float* __restrict__ img, const 
     }
 }
 
-// forward statistics only: per-block channel sums / square sums of z (fp32, as the stored path)
-template <int G>
-__global__ void __launch_bounds__(256) stem_stats_kernel(const float* __restrict__ img, const float* __restrict__ w,
-                                                         float* __restrict__ st_sum, float* __restrict__ st_sq,
-                                                         StemGeo s) {
-    __shared__ float win[SIH * SIW];
-    __shared__ float red[2][512];
-    const int g = threadIdx.x % G;
-    float wr[8][9];
-    load_w8(w, g, wr);
-    float ls[8], lq[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) ls[r] = lq[r] = 0.f;
-    stem_visit<G, false>(img, s, wr, win, nullptr, 0, 0, [&](int, int, int, const float*, const float* zf, const float*, uint4) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            ls[r] += zf[r];
-            lq[r] += zf[r] * zf[r];
-        }
-    });
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-        for (int o = G; o < 64; o <<= 1) {
-            ls[r] += __shfl_xor(ls[r], o, 64);
-            lq[r] += __shfl_xor(lq[r], o, 64);
-        }
-    ordered_wave_add8(red[0], red[1], ls, lq, g, G);
-    for (int c = threadIdx.x; c < s.C; c += 256) {
-        st_sum[int64_t(blockIdx.x) * s.C + c] = red[0][c];
-        st_sq[int64_t(blockIdx.x) * s.C + c] = red[1][c];
-    }
-}
-
-// y view = silu(z * scale + shift), fp16
-template <int G>
-__global__ void __launch_bounds__(256) stem_apply_kernel(const float* __restrict__ img, const float* __restrict__ w,
-                                                         const float* __restrict__ scale, const float* __restrict__ shift,
-                                                         uint16_t* __restrict__ y, int64_t y_bs, int64_t y_ld, StemGeo s) {
-    __shared__ float win[SIH * SIW];
-    const int g = threadIdx.x % G;
-    float wr[8][9], sc[8], sf[8];
-    load_w8(w, g, wr);
-    load8f(scale + g * 8, sc);
-    load8f(shift + g * 8, sf);
-    stem_visit<G, false>(img, s, wr, win, nullptr, 0, 0, [&](int n, int oh, int ow, const float*, const float*, const float* z, uint4) {
-        uint32_t o[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float a = silu_f(z[2 * e] * sc[2 * e] + sf[2 * e]);
-            const float b = silu_f(z[2 * e + 1] * sc[2 * e + 1] + sf[2 * e + 1]);
-            o[e] = uint32_t(f2h(a)) | (uint32_t(f2h(b)) << 16);
-        }
-        *reinterpret_cast<uint4*>(y + int64_t(n) * y_bs + int64_t(oh * s.OW + ow) * y_ld + g * 8) =
-            make_uint4(o[0], o[1], o[2], o[3]);
-    });
-}
-
 __device__ __forceinline__ void unpack_bf8(uint4 v, float* d) {
     const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         d[2 * e] = bf2f(bf16_t(u[e] & 0xffff));
         d[2 * e + 1] = bf2f(bf16_t(u[e] >> 16));
-    }
-}
-
-// per-block partials of sum(g) and sum(g * xhat), g = dy * silu'(z * scale + shift)
-template <int G>
-__global__ void __launch_bounds__(256) stem_bwd_reduce_kernel(const bf16_t* __restrict__ dy, int64_t d_bs, int64_t d_ld,
-                                                              const float* __restrict__ img, const float* __restrict__ w,
-                                                              const float* __restrict__ bnv, float* __restrict__ ps,
-                                                              float* __restrict__ pg, StemGeo s) {
-    __shared__ float win[SIH * SIW];
-    __shared__ float red[2][512];
-    const int g = threadIdx.x % G, C = s.C;
-    float wr[8][9], sc[8], sf[8], mu[8], rs[8];
-    load_w8(w, g, wr);
-    load8f(bnv + g * 8, sc);
-    load8f(bnv + C + g * 8, sf);
-    load8f(bnv + 2 * C + g * 8, mu);
-    load8f(bnv + 3 * C + g * 8, rs);
-    float ls[8], lx[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) ls[r] = lx[r] = 0.f;
-    stem_visit<G, true>(img, s, wr, win, dy, d_bs, d_ld, [&](int, int, int, const float*, const float*, const float* z, uint4 dv) {
-        float d[8];
-        unpack_bf8(dv, d);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const float gg = d[r] * stem_dsilu(z[r] * sc[r] + sf[r]);
-            ls[r] += gg;
-            lx[r] += gg * ((z[r] - mu[r]) * rs[r]);
-        }
-    });
-#pragma unroll
-    for (int r = 0; r < 8; ++r)
-        for (int o = G; o < 64; o <<= 1) {
-            ls[r] += __shfl_xor(ls[r], o, 64);
-            lx[r] += __shfl_xor(lx[r], o, 64);
-        }
-    ordered_wave_add8(red[0], red[1], ls, lx, g, G);
-    for (int c = threadIdx.x; c < C; c += 256) {
-        ps[int64_t(blockIdx.x) * C + c] = red[0][c];
-        pg[int64_t(blockIdx.x) * C + c] = red[1][c];
     }
 }
 
@@ -345,14 +244,6 @@ __global__ void __launch_bounds__(256) stem_bwd_wgrad_kernel(const bf16_t* __res
 
 constexpr int STEM_WG_BLOCKS = 1024;   // weight-gradient partial rows
 
-// channel counts with a kernel instance: 16, 32, 64 (G = 2, 4, 8 lanes per pixel)
-#define YM_STEM_DISPATCH(C, K, GRID, SHM, ST, ...)                                                   \
-    do {                                                                                             \
-        if ((C) == 16) hipLaunchKernelGGL(K<2>, GRID, dim3(256), SHM, ST, __VA_ARGS__);               \
-        else if ((C) == 32) hipLaunchKernelGGL(K<4>, GRID, dim3(256), SHM, ST, __VA_ARGS__);          \
-        else hipLaunchKernelGGL(K<8>, GRID, dim3(256), SHM, ST, __VA_ARGS__);                         \
-    } while (0)
-
 bool stem_shape_ok(int n, int h, int w, int oh, int ow, int c, int stride) {
     return (c == 16 || c == 32 || c == 64) && (stride == 1 || stride == 2) &&
            int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31);
@@ -362,44 +253,6 @@ bool stem_shape_ok(int n, int h, int w, int oh, int ow, int c, int stride) {
 }  // namespace ym
 
 using namespace ym;
-
-extern "C" int ym_stem_apply(const float* img, const float* w_oihw, const float* scale, const float* shift,
-                             uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh, int ow, int cout,
-                             int stride, int pad, void* stream) {
-    YM_CHECK_ARG(img && w_oihw && scale && shift && y, "ym_stem_apply: null argument");
-    YM_CHECK_ARG(stem_shape_ok(n, h, w, oh, ow, cout, stride) && y_ld % 8 == 0 && y_bs % 8 == 0,
-                 "ym_stem_apply: unsupported shape / unaligned view");
-    const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
-    const int blocks = int(std::min<int64_t>(4096, int64_t(n) * ((oh + STH - 1) / STH) * ((ow + STW - 1) / STW)));
-    if (blocks == 0) return YM_OK;
-    YM_STEM_DISPATCH(cout, stem_apply_kernel, dim3(blocks), 0, as_stream(stream), img, w_oihw, scale, shift, y, y_bs,
-                     y_ld, g);
-    YM_LAUNCH_CHECK("ym_stem_apply");
-    return YM_OK;
-}
-
-extern "C" int ym_stem_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
-                                  const float* bnv, float* part_sum, float* part_dot, int blocks, int n, int h, int w,
-                                  int oh, int ow, int cout, int stride, int pad, void* stream) {
-    YM_CHECK_ARG(dy && img && w_oihw && bnv && part_sum && part_dot && blocks >= 1, "ym_stem_bwd_reduce: null argument");
-    YM_CHECK_ARG(stem_shape_ok(n, h, w, oh, ow, cout, stride) && d_ld % 8 == 0 && d_bs % 8 == 0,
-                 "ym_stem_bwd_reduce: unsupported shape / unaligned view");
-    const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
-    YM_STEM_DISPATCH(cout, stem_bwd_reduce_kernel, dim3(blocks), 0, as_stream(stream),
-                     reinterpret_cast<const bf16_t*>(dy), d_bs, d_ld, img, w_oihw, bnv, part_sum, part_dot, g);
-    YM_LAUNCH_CHECK("ym_stem_bwd_reduce");
-    return YM_OK;
-}
-
-extern "C" int ym_stem_stats(const float* img, const float* w_oihw, float* stat_sum, float* stat_sq, int blocks, int n,
-                             int h, int w, int oh, int ow, int cout, int stride, int pad, void* stream) {
-    YM_CHECK_ARG(img && w_oihw && stat_sum && stat_sq && blocks >= 1, "ym_stem_stats: null argument");
-    YM_CHECK_ARG(stem_shape_ok(n, h, w, oh, ow, cout, stride), "ym_stem_stats: unsupported shape");
-    const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
-    YM_STEM_DISPATCH(cout, stem_stats_kernel, dim3(blocks), 0, as_stream(stream), img, w_oihw, stat_sum, stat_sq, g);
-    YM_LAUNCH_CHECK("ym_stem_stats");
-    return YM_OK;
-}
 
 // the stored-z form: BatchNorm-backward apply + weight gradient of the stem in one pass over dy and
 // the stored z (dz never written; replaces ym_bn_bwd_apply + ym_conv_first_wgrad)
@@ -431,22 +284,4 @@ extern "C" int ym_stem_bwd_wgrad_stored(const uint16_t* dy, int64_t d_bs, int64_
 
 extern "C" size_t ym_stem_bwd_wgrad_workspace_size(int cout) {
     return size_t(STEM_WG_BLOCKS) * size_t(cout > 0 ? cout : 0) * 9 * sizeof(float);
-}
-
-extern "C" int ym_stem_bwd_wgrad(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const float* img, const float* w_oihw,
-                                 const float* bnv, const float* coef, float* dw_oihw, float* workspace,
-                                 size_t workspace_bytes, int n, int h, int w, int oh, int ow, int cout, int stride,
-                                 int pad, void* stream) {
-    YM_CHECK_ARG(dy && img && w_oihw && bnv && coef && dw_oihw, "ym_stem_bwd_wgrad: null argument");
-    YM_CHECK_ARG(stem_shape_ok(n, h, w, oh, ow, cout, stride) && d_ld % 8 == 0 && d_bs % 8 == 0,
-                 "ym_stem_bwd_wgrad: unsupported shape / unaligned view");
-    YM_CHECK_ARG(workspace && workspace_bytes >= ym_stem_bwd_wgrad_workspace_size(cout),
-                 "ym_stem_bwd_wgrad: workspace too small");
-    const StemGeo g{n, h, w, oh, ow, cout, stride, pad};
-    hipStream_t st = as_stream(stream);
-    YM_STEM_DISPATCH(cout, stem_bwd_wgrad_kernel, dim3(STEM_WG_BLOCKS), 0, st, reinterpret_cast<const bf16_t*>(dy),
-                     d_bs, d_ld, img, w_oihw, bnv, coef, workspace, g);
-    colsum_launch(workspace, STEM_WG_BLOCKS, cout * 9, int64_t(cout) * 9, dw_oihw, 1, st);
-    YM_LAUNCH_CHECK("ym_stem_bwd_wgrad");
-    return YM_OK;
 }

@@ -478,15 +478,10 @@ WgPlan wg_plan(const ym_conv_desc* d) {
         p.units = int64_t(d->n) * ((d->oh + 7) / 8) * ((d->ow + 7) / 8);
     } else if (d->k == 1 && d->stride == 1 && d->pad == 0 && whole) {
         p.kind = 1;
-        // 128-wide tiles once both channel counts reach t128 (YM_WGRAD1_T128, default 96): fewer
-        // tiles re-read dz and x fewer times, at the cost of padding a channel count below 128 —
-        // the 96 -> 128 1x1 at 160x160 measured 0.357 ms on 64-wide tiles (x and dz read twice
-        // each from HBM), 0.142 ms on one padded 128-wide tile
-        static const int t128 = [] {
-            const char* e = getenv("YM_WGRAD1_T128");
-            return e ? atoi(e) : 96;
-        }();
-        p.T = (d->cout >= t128 && d->cin >= t128) ? 128 : 64;
+        // 128-wide tiles once both channel counts reach 96: fewer tiles re-read dz and x fewer times, at
+        // the cost of padding a channel count below 128 — the 96 -> 128 1x1 at 160x160 measured 0.357 ms
+        // on 64-wide tiles (x and dz read twice each from HBM), 0.142 ms on one padded 128-wide tile
+        p.T = (d->cout >= 96 && d->cin >= 96) ? 128 : 64;
         p.units = (M + 63) / 64;
     } else {
         p.kind = 0;
@@ -502,10 +497,7 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     // workgroups per launch: 256 measured best in the training step (2800 img/s vs 2767 at 512 and
     // 2725 at 1024): the weight gradients run on the side stream beside the data gradients, and
     // fewer, longer split-K blocks leave the main stream room and halve the partials to reduce
-    static const int64_t target = [] {           // YM_WGRAD_BLOCKS overrides (A/B runs)
-        const char* e = getenv("YM_WGRAD_BLOCKS");
-        return int64_t(e ? std::max(8, atoi(e)) : 256);
-    }();
+    constexpr int64_t target = 256;
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(target / cols, p.units / min_units));
     splits = std::min<int64_t>(splits, p.kind == 0 ? 65535 : 256);
     if (p.kind != 0 && splits >= 8) splits &= ~int64_t(7);      // whole XCD groups (wg_tile)
@@ -558,28 +550,21 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
         splits = 0;
     } else if (p.kind == 3) {
         YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
-        static const bool w4 = [] {            // YM_WGRAD_WAVES=4: the one-wave-per-SIMD form (A/B runs)
-            const char* e = getenv("YM_WGRAD_WAVES");
-            return e && atoi(e) == 4;
-        }();
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
-#define YM_WG3(S_)                                                                                        \
+#define WG3_LAUNCH(S_)                                                                                        \
         switch (tc) {                                                                                     \
-            case 0:                                                                                       \
-                if (w4) hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 64, 64>), grid, dim3(256), 0, st, a);     \
-                else hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 64, 64>), grid, dim3(512), 0, st, a);        \
-                break;                                                                                    \
+            case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 64, 64>), grid, dim3(512), 0, st, a); break;  \
             case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 32, 64>), grid, dim3(512), 0, st, a); break;  \
             case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 64, 32>), grid, dim3(256), 0, st, a); break;  \
             default: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 32, 32>), grid, dim3(256), 0, st, a); break; \
         }
         if (d->stride == 1) {
-            YM_WG3(1)
+            WG3_LAUNCH(1)
         } else {
-            YM_WG3(2)
+            WG3_LAUNCH(2)
         }
-#undef YM_WG3
+#undef WG3_LAUNCH
     } else if (p.kind == 1) {
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         if (p.T == 128)

@@ -27,13 +27,6 @@ class ConvDesc(ctypes.Structure):
                 ("y_ld", I64), ("out_f32", I32), ("accumulate", I32)]
 
 
-class BnTrain(ctypes.Structure):
-    """ym_bn_train (include/yolomi.h): BatchNorm state + outputs of the fused statistics finalize."""
-    _fields_ = [("gamma", P), ("beta", P), ("running_mean", P), ("running_var", P), ("num_batches_tracked", P),
-                ("momentum", F32), ("eps", F32), ("scale", P), ("shift", P), ("mean", P), ("rstd", P),
-                ("workspace", P)]
-
-
 class AdamWEntry(ctypes.Structure):
     """ym_adamw_entry (include/yolomi.h)."""
     _fields_ = [("p", P), ("g", P), ("m", P), ("v", P), ("offset", I64), ("n", I64)]
@@ -67,22 +60,15 @@ SIGNATURES = {
     "ym_conv_set_pipe": (R, [INT]),
     "ym_conv_set_direct": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
-    "ym_conv_fwd_bn": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_stem_stats": (R, [P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_stem_apply": (R, [P, P, P, P, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_stem_bwd_reduce": (R, [P, I64, I64, P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_stem_bwd_wgrad_workspace_size": (SZ, [INT]),
-    "ym_stem_bwd_wgrad": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_stem_bwd_wgrad_stored": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_conv_first_fwd_bn": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P, P]),
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
-    "ym_dw3x3_fwd_bn": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P, P]),
     "ym_dw3x3_bwd_workspace_size": (SZ, [INT]),
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
@@ -94,7 +80,6 @@ SIGNATURES = {
     "ym_bn_bwd_blocks": (R, [I64, INT]),
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P, P]),
-    "ym_bn_bwd_reduce_finalize": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply_res": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, I64, I64, INT, P]),
     "ym_sppf_supported": (R, [INT, INT, INT]),
@@ -130,7 +115,6 @@ SIGNATURES = {
     "ym_eval_detections": (R, [P, P, P, P, P, I64, I64, I64, I64, P, INT, INT, INT, F32, P, SZ, P, P]),
     "ym_eval_ap": (R, [P, P, I64, I64, P, SZ, P, P]),
     "ym_iou_matrix": (R, [P, P, I64, I64, P, P]),
-    "ym_debug_nms_stamps": (R, [P]),
     "ym_resize_linear_u8": (R, [P, P, INT, INT, P, P]),
     "ym_grad_norm_blocks": (R, [I64]),
     "ym_grad_norm": (R, [P, INT, I64, P, P, P]),

@@ -23,7 +23,7 @@ import os
 import numpy as np
 import torch
 
-from ._lib import BnEvalEntry, BnTrain, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
+from ._lib import BnEvalEntry, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
 
 BF16 = torch.bfloat16
 F16 = torch.float16
@@ -164,22 +164,6 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
-def bn_fold_on():
-    """YM_BN_FOLD=1: training BatchNorm statistics finalized inside the kernel that produces them
-    (ym_conv_fwd_bn, ym_bn_bwd_reduce_finalize, ...) instead of a separate ym_bn_finalize /
-    ym_bn_bwd_finalize launch.  Off by default: measured 2678 vs 2798 img/s (s@640 bs64) — every
-    workgroup's ticket (write-through stores, vmcnt(0), barrier, agent atomic) plus the elected
-    workgroups' two-level fold cost the conv forward family +1.5 ms/step, more than the 154 finalize
-    launches it removes."""
-    return os.environ.get("YM_BN_FOLD", "0") == "1"
-
-
-def bn_bwd_fold_on():
-    """YM_BN_BWD_FOLD=1: the backward statistics pass finalizes dgamma / dbeta / the apply coefficients
-    itself (ym_bn_bwd_reduce_finalize) instead of a separate ym_bn_bwd_finalize launch."""
-    return os.environ.get("YM_BN_BWD_FOLD", "0") == "1"
-
-
 # buffer-range keys for the stream scheduler: ('a' activation | 'g' gradient, Act id, c0, c1)
 def _ka(v):
     return ("a", id(v.act), v.c0, v.c0 + v.c)
@@ -255,18 +239,6 @@ class ConvBN:
             if kind != "bn" and self.k == 3 and f"{kind}3" in fam:     # the dense 3x3 convs on their own
                 fam[f"{kind}3"].append(ent)
 
-    def _bn_train(self, plan):
-        """ym_bn_train for the fused finalize (pointers only; the workspace is the current stream's)."""
-        bn = self.m.bn
-        t = BnTrain()
-        t.gamma, t.beta = _p(bn.weight), _p(bn.bias)
-        t.running_mean, t.running_var = _p(bn.running_mean), _p(bn.running_var)
-        t.num_batches_tracked = _p(bn.num_batches_tracked)
-        t.momentum, t.eps = float(bn.momentum), float(bn.eps)
-        t.scale, t.shift, t.mean, t.rstd = (self.bnv[i].data_ptr() for i in range(4))
-        t.workspace = plan.bn_ws.data_ptr()
-        return t
-
     def _static_args(self, plan):
         """Pointer arguments of this op's forward launches that never change for its plan (the plan's
         own buffers), converted once: at bs1 the eval forward is host-bound and re-deriving them per
@@ -283,19 +255,17 @@ class ConvBN:
             a = self._sa = (bnv, ss, sq, apply)
         return a
 
-    def _bn_fwd(self, plan, st, ss, sq, finalized=False):
+    def _bn_fwd(self, plan, st, ss, sq):
         """BatchNorm finalize + apply (+ SiLU, + residual) of the forward: 'bn' family, algorithmic bytes
         = the partial rows read + z read + y written (+ residual read)."""
         bn = self.m.bn
         (sc, sh, mu, rs), ssp, sqp, apply = self._static_args(plan)
         r = self.res
         e = self.M * self.co * 2
-        work = 8 * self.G * self.co * (1 if plan.training and not finalized else 0) + 2 * e + (e if r else 0)
+        work = 8 * self.G * self.co * (1 if plan.training else 0) + 2 * e + (e if r else 0)
 
         def run():
-            if finalized:
-                pass
-            elif plan.training:
+            if plan.training:
                 call("ym_bn_finalize", ssp, sqp, self.G, self.co, float(self.M), _p(bn.weight),
                      _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
                      float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
@@ -307,13 +277,6 @@ class ConvBN:
 
     def forward(self, plan, st):
         ss, sq = self.ps[0], self.ps[1]
-        if plan.training and bn_fold_on():
-            bt = self._bn_train(plan)
-            self._timed(plan, "fwd", plan._cur_stream, lambda: call(
-                "ym_conv_fwd_bn", ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(),
-                ss.data_ptr(), sq.data_ptr(), ctypes.byref(bt), st))
-            self._bn_fwd(plan, st, ss, sq, finalized=True)
-            return
         conv = self.__dict__.get("_sc")
         if conv is None:
             conv = self._sc = (ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
@@ -332,20 +295,14 @@ class ConvBN:
         r = self.res
         racc = r.grad_for_write(st) if r is not None else 0
         e = self.M * self.co * 2
-        fold = bn_bwd_fold_on()
         work = 5 * e + 16 * Gb * self.co + ((2 + racc) * e if r is not None else 0)
 
         def run():
-            if fold:
-                call("ym_bn_bwd_reduce_finalize", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co,
-                     self.HW, sc, sh, mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), _p(bn.weight),
-                     plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-            else:
-                call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
-                     mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-                call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-                     _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
-                     plan.bn_ws.data_ptr(), st)
+            call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                 mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+            call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+                 _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
+                 plan.bn_ws.data_ptr(), st)
             if r is not None:
                 call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc,
                      sh, mu, rs, self.act, self.coef.data_ptr(), self.z.data_ptr(), r.gptr(), r.bs, r.ld, racc, st)
@@ -376,21 +333,6 @@ class ConvBN:
             self.x.mark()
 
 
-def stem_recompute_on():
-    """YM_STEM_RECOMPUTE=1: the stem's pre-BatchNorm z recomputed from the image (ym_stem_stats /
-    _apply / _bwd_reduce / _bwd_wgrad) instead of stored — 2.5 GB less HBM traffic and 420 MB less
-    memory per s@640 bs64 step, but its VALU passes (9-tap conv + SiLU derivative + weight-gradient
-    outer product per element) run 0.16-0.41 ms each, so the step measured the same (2938 vs 2931
-    img/s): off by default until those passes move to MFMA."""
-    return os.environ.get("YM_STEM_RECOMPUTE", "0") == "1"
-
-
-def stem_fused_bwd_on():
-    """The stored-z stem backward's BatchNorm apply fused with its weight gradient
-    (ym_stem_bwd_wgrad_stored; YM_STEM_FUSED_BWD=0: ym_bn_bwd_apply + ym_conv_first_wgrad)."""
-    return os.environ.get("YM_STEM_FUSED_BWD", "1") != "0"
-
-
 class StemConvBN(ConvBN):
     """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
 
@@ -407,12 +349,9 @@ class StemConvBN(ConvBN):
         oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
         assert (oh, ow) == (y.H, y.W)
         self.M, self.HW, self.oh, self.ow = B * oh * ow, oh * ow, oh, ow
-        self.recompute = stem_recompute_on()
-        # z only when it is stored (the recompute path never materialises it)
-        self.z = None if self.recompute else torch.empty(self.M, co, dtype=BF16, device=plan.dev)
+        self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
         self.G = 1024
-        self.Gb = 1024
-        self.ps = torch.empty(2, max(self.G, self.Gb, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
+        self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
         self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)
         self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
 
@@ -421,84 +360,38 @@ class StemConvBN(ConvBN):
 
     def forward(self, plan, st):
         ss, sq = self.ps[0], self.ps[1]
-        if not self.recompute:
-            self._forward_stored(plan, st, ss, sq)
-            return
-        bn = self.m.bn
-        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-        if plan.training:
-            call("ym_stem_stats", plan.img.data_ptr(), _p(self.m.conv.weight), ss.data_ptr(), sq.data_ptr(), self.G,
-                 *self._geo(plan), st)
-        e = self.M * self.co * 2
-
-        def run():
-            if plan.training:
-                call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), self.G, self.co, float(self.M), _p(bn.weight),
-                     _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
-                     float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
-            elif not plan.eval_coeff_batched:
-                call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
-                     _p(bn.running_var), float(bn.eps), sc, sh, st)
-            call("ym_stem_apply", plan.img.data_ptr(), _p(self.m.conv.weight), sc, sh, self.y.ptr(), self.y.bs,
-                 self.y.ld, *self._geo(plan), st)
-        self._timed(plan, "bn", plan._cur_stream, run, e + 4 * plan.B * self.H * self.W)
-
-    def _forward_stored(self, plan, st, ss, sq):
-        B = plan.B
-        if plan.training and bn_fold_on():
-            bt = self._bn_train(plan)
-            call("ym_conv_first_fwd_bn", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(),
-                 ss.data_ptr(), sq.data_ptr(), B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G,
-                 ctypes.byref(bt), st)
-            self._bn_fwd(plan, st, ss, sq, finalized=True)
-            return
         call("ym_conv_first_fwd", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(), ss.data_ptr(),
-             sq.data_ptr(), B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
+             sq.data_ptr(), plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
         self._bn_fwd(plan, st, ss, sq)
 
     def backward(self, plan, st):
+        """Statistics pass + finalize as every Conv block, then the BatchNorm apply and the weight gradient in
+        ONE pass over dy and the stored z (ym_stem_bwd_wgrad_stored: dz is never written and re-read; the
+        kernel covers 16 / 32 / 64 channels — the n / s / m-l stems; other widths: BN backward + a separate
+        weight gradient over the written dz)."""
         dy = self.y.grad_for_read(st)
-        if not self.recompute and stem_fused_bwd_on() and self.co in (16, 32, 64):
-            # statistics pass + finalize as every Conv block, then the apply and the weight gradient in
-            # ONE pass over dy and the stored z (ym_stem_bwd_wgrad_stored: dz never written / re-read)
-            bn = self.m.bn
-            sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
-            Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
-            ws = plan.private_ws(self, lib().ym_stem_bwd_wgrad_workspace_size(self.co))
-            e = self.M * self.co * 2
-
-            def run():
-                call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
-                     mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-                call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-                     _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
-                     plan.bn_ws.data_ptr(), st)
-                call("ym_stem_bwd_wgrad_stored", dy, self.y.bs, self.y.ld, self.z.data_ptr(), plan.img.data_ptr(),
-                     self.bnv.data_ptr(), self.coef.data_ptr(), plan.gptr(self.m.conv.weight), ws.data_ptr(),
-                     ws.numel() * 4, *self._geo(plan), st)
-            self._timed(plan, "bn", plan._cur_stream, run, 4 * e + 16 * Gb * self.co + 4 * plan.B * self.H * self.W)
-            return
-        if not self.recompute:
+        if self.co not in (16, 32, 64):
             self._bn_bwd(plan, st, dy)
             ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
             call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight),
                  plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
             return
         bn = self.m.bn
-        rs = self.bnv[3].data_ptr()
-        ps, pd = self.ps[0], self.ps[1]
+        sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+        Gb = lib().ym_bn_bwd_blocks(self.M, self.co)
         ws = plan.private_ws(self, lib().ym_stem_bwd_wgrad_workspace_size(self.co))
         e = self.M * self.co * 2
 
         def run():
-            call("ym_stem_bwd_reduce", dy, self.y.bs, self.y.ld, plan.img.data_ptr(), _p(self.m.conv.weight),
-                 self.bnv.data_ptr(), ps.data_ptr(), pd.data_ptr(), self.Gb, *self._geo(plan), st)
-            call("ym_bn_bwd_finalize", ps.data_ptr(), pd.data_ptr(), self.Gb, self.co, float(self.M), _p(bn.weight), rs,
-                 plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
-            call("ym_stem_bwd_wgrad", dy, self.y.bs, self.y.ld, plan.img.data_ptr(), _p(self.m.conv.weight),
+            call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
+                 mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+            call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+                 _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
+                 plan.bn_ws.data_ptr(), st)
+            call("ym_stem_bwd_wgrad_stored", dy, self.y.bs, self.y.ld, self.z.data_ptr(), plan.img.data_ptr(),
                  self.bnv.data_ptr(), self.coef.data_ptr(), plan.gptr(self.m.conv.weight), ws.data_ptr(),
                  ws.numel() * 4, *self._geo(plan), st)
-        self._timed(plan, "bn", plan._cur_stream, run, 2 * e + 8 * plan.B * self.H * self.W)
+        self._timed(plan, "bn", plan._cur_stream, run, 4 * e + 16 * Gb * self.co + 4 * plan.B * self.H * self.W)
 
 
 class DWConvBN(ConvBN):
@@ -524,13 +417,6 @@ class DWConvBN(ConvBN):
     def forward(self, plan, st):
         ss, sq = self.ps[0], self.ps[1]
         gsz, gstr, goff = self.map
-        if plan.training and bn_fold_on():
-            bt = self._bn_train(plan)
-            call("ym_dw3x3_fwd_bn", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
-                 self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G,
-                 ctypes.byref(bt), st)
-            self._bn_fwd(plan, st, ss, sq, finalized=True)
-            return
         call("ym_dw3x3_fwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
              self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G, st)
         self._bn_fwd(plan, st, ss, sq)
@@ -614,9 +500,9 @@ class SPPFPools:
 
     def fused(self, plan):
         """The whole chain in one launch per direction (ym_sppf_fwd / _bwd, chain kept in LDS) when
-        the map fits; YM_SPPF_FUSED=0: one launch per pool."""
+        the map fits in LDS (ym_sppf_supported); otherwise one launch per pool."""
         sl = self.slices
-        return (os.environ.get("YM_SPPF_FUSED", "1") != "0" and lib().ym_sppf_supported(self.H, self.W, self.C)
+        return (lib().ym_sppf_supported(self.H, self.W, self.C)
                 and sl[1].bs == sl[2].bs == sl[3].bs and sl[1].ld == sl[2].ld == sl[3].ld)
 
     def forward(self, plan, st):
@@ -1008,25 +894,11 @@ class Plan:
     # s@640 bs64 step, replay is 1.5-2 ms SLOWER than eager launches (26.3-26.7 vs 24.7 ms/step at
     # 1 and 2 streams): the eager host enqueue already runs ahead of the GPU, and the replayed
     # graph runs its kernels with less overlap than the streams do.
-    # Eval-mode model plans can replay their forward as a HIP graph (YM_EVAL_GRAPH=1; training:
-    # YM_GRAPH=1).  Measured SLOWER, so off by default: s@640 inference bs1 2.66 vs 1.80 ms eager,
-    # bs128 13.7 vs 13.1 ms — the replay of ~175 multi-stream nodes costs more than the eager
-    # ctypes enqueue it removes.  The captured launches read weights, BatchNorm buffers and the
-    # image at fixed addresses: parameters updated in place (optimizer steps, load_state_dict) are
-    # seen by the replay; a parameter or buffer REPLACED by a new tensor changes the address key
-    # checked before every eval replay, which drops the graph (eager run, then a new capture).
     def _graph_ok(self):
         if not (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
                 and self.family_events is None):
             return False
-        if not self.training:
-            return os.environ.get("YM_EVAL_GRAPH", "0") == "1"
-        return os.environ.get("YM_GRAPH", "0") == "1"
-
-    def _address_key(self):
-        return (tuple(w.data_ptr() for w, *_ in self.weights.items),
-                tuple((op.m.bn.weight.data_ptr(), op.m.bn.running_mean.data_ptr(), op.m.bn.running_var.data_ptr())
-                      for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m")))
+        return self.training and os.environ.get("YM_GRAPH", "0") == "1"
 
     @property
     def graph_active(self):
@@ -1040,12 +912,6 @@ class Plan:
         if not self._graph_ok():
             body()
             return
-        if not self.training:
-            key = self._address_key()
-            if key != self.__dict__.get("_graph_key"):
-                graphs.clear()
-                runs.clear()
-                self._graph_key = key
         if runs.get(phase, 0) < 1:
             runs[phase] = runs.get(phase, 0) + 1
             body()
@@ -1075,9 +941,12 @@ class Plan:
         """Eval: every BatchNorm layer's scale / shift from its running statistics in ONE launch
         (ym_bn_eval_coeff_batch over a pointer table built once per plan; the parameters and buffers
         are read at launch time, so later weight / statistics updates are picked up)."""
-        key = tuple(op.m.bn.weight.data_ptr() for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m"))
+        ents = [op for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m")]
+        # keyed on EVERY pointer the table holds: a parameter or buffer replaced by a new tensor
+        # (load_state_dict(assign=True), bn.running_var = ...) rebuilds it instead of leaving a dangling one
+        key = tuple((_p(op.m.bn.weight), _p(op.m.bn.bias), _p(op.m.bn.running_mean), _p(op.m.bn.running_var),
+                     op.bnv.data_ptr()) for op in ents)
         if getattr(self, "_eval_key", None) != key:
-            ents = [op for op in self.ops if hasattr(op, "bnv") and hasattr(op, "m")]
             arr = (BnEvalEntry * len(ents))()
             for e, op in zip(arr, ents):
                 bn = op.m.bn
