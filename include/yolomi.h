@@ -156,6 +156,10 @@ int ym_conv_set_pipe(int mode);
  * layers) for later calls: -1 YM_CONV_DIRECT / default, 0 never, 1 maps of >= 1 M output pixels
  * (default), 2 any size.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_direct(int mode);
+/* Selection policy of the halo-staged pipelined 3x3 stride-1 kernel (conv_hpipe.hip: 16x16-pixel tiles,
+ * each 64-channel chunk of the 18x18 input halo staged once for all nine taps): -1 default, 0 never,
+ * 1 eligible layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
+int ym_conv_set_hpipe(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
  * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,

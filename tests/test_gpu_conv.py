@@ -168,7 +168,8 @@ def test_dgrad_accumulate_stride2():
     base = torch.randn(n, h, w, cin, generator=g).bfloat16()
     dx = base.to(dev)
     w_t = wbf.permute(1, 2, 3, 0).contiguous().to(dev)
-    call("ym_conv_dgrad", ctypes.byref(d), dz.to(dev).data_ptr(), w_t.data_ptr(), dx.data_ptr(),
+    dzd = dz.to(dev)
+    call("ym_conv_dgrad", ctypes.byref(d), dzd.data_ptr(), w_t.data_ptr(), dx.data_ptr(),
          torch.cuda.current_stream().cuda_stream)
     ref = base.float() + torch.nn.grad.conv2d_input((n, cin, h, w), wbf.float(), dz.float().permute(0, 3, 1, 2),
                                                     stride=s, padding=p).permute(0, 2, 3, 1)
@@ -198,6 +199,46 @@ def test_pipe_kernel_vs_torch(shape):
     """fp16 forward (+ BN statistic partials), bf16 data gradient (overwrite, then accumulate)."""
     from yolomi._lib import lib
     _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
+
+
+# halo-staged PIPELINED 3x3 stride-1 kernel (conv_hpipe.hip), forced on with ym_conv_set_hpipe(2): 16x16-pixel
+# tiles on maps whose sides are multiples of 16, 128-channel tiles (a partial second channel tile at 192),
+# 2-4 input chunks of 64 channels, channel-slice views in and out, fp16 z + BN statistic partials,
+# bf16 data gradient overwrite and accumulate
+HPIPE = [
+    (2, 16, 16, 128, 128, 3, 1, 1, 0, 0),
+    (1, 32, 48, 128, 128, 3, 1, 1, 64, 0),
+    (2, 16, 32, 128, 192, 3, 1, 1, 0, 8),
+    (3, 32, 32, 256, 128, 3, 1, 1, 0, 0),
+    (2, 48, 16, 192, 256, 3, 1, 1, 32, 64),
+    (9, 80, 80, 128, 128, 3, 1, 1, 0, 0),
+]
+
+
+@pytest.mark.parametrize("shape", HPIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}x{s[8]}y{s[9]}" for s in HPIPE])
+def test_hpipe_kernel_vs_torch(shape):
+    from yolomi._lib import lib
+    _views_fwd_dgrad_check(shape, lib().ym_conv_set_hpipe, 2, 4)
+
+
+def test_hpipe_selection():
+    """By default the halo-pipelined kernel takes the 3x3 stride-1 convs on 16-multiple maps with >= 512 tiles
+    (the 80x80 / 160x160 layers at bs64) and >= 128 output channels, in either direction; never stride 2 or
+    other maps."""
+    from yolomi._lib import lib
+
+    def desc(*shape):
+        d, _, _ = _desc(*shape)
+        d.out_f32 = 2                    # a Conv block's fp16 z
+        return d
+    d = desc(64, 80, 80, 128, 128, 3, 1, 1)
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) == 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
+    d = desc(64, 80, 80, 128, 64, 3, 1, 1)          # 64 output channels: forward elsewhere, dgrad (128) here
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
+    for shape in [(64, 40, 40, 128, 128, 3, 1, 1), (64, 160, 160, 64, 64, 3, 2, 1), (2, 80, 80, 128, 128, 3, 1, 1),
+                  (64, 80, 80, 64, 64, 3, 1, 1)]:
+        d = desc(*shape)
+        assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4, shape
 
 
 # halo-staged 3x3 kernel forced on (ym_conv_set_halo(1)) through the same training-path outputs the

@@ -85,5 +85,9 @@ def test_loss_curve_20_steps_vs_reference(golden):
     print("gpu rel err", np.round(err, 4).tolist())
     print("emu rel err", np.round(err_emu, 4).tolist())
     bound = np.maximum(np.maximum(2 * err_emu, 1.5 * err_emu.max()), 2e-2)
+    print("per-step bound", np.round(bound, 4).tolist())
     assert (err <= bound).all(), (err, bound)
+    # absolute caps independent of the rounding model: no step more than 6 % off the reference's loss, and
+    # the 20-step mean within 2 % (a change of the jitter model cannot widen what passes beyond these)
+    assert (err <= 6e-2).all(), err
     assert err.mean() <= 2e-2, err.mean()

@@ -100,7 +100,7 @@ def teacher_forced(scale, imgsz, bs, seed):
     from yolomi import graph as G
 
     m = _seeded_model(scale).train()
-    state0 = {k: v.clone() for k, v in m.state_dict().items()}
+    state0 = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
     b = {k: v.cuda() for k, v in synth_batch(bs, imgsz, seed=seed).items()}
     heads = m(b["img"])
     plan = m.__dict__["_ym_last_plan"]
@@ -252,9 +252,16 @@ def teacher_forced(scale, imgsz, bs, seed):
     return R
 
 
-@pytest.mark.parametrize("scale,imgsz,bs", [("s", 640, 2), ("m", 256, 1)])
-def test_teacher_forced_every_layer(scale, imgsz, bs):
+@pytest.mark.parametrize("scale,imgsz,bs,hpipe", [("s", 640, 2, 2), ("m", 256, 1, -1)])
+def test_teacher_forced_every_layer(scale, imgsz, bs, hpipe):
+    """hpipe = 2 forces the halo-pipelined 3x3 kernel on every eligible layer (at bs2 the default policy
+    leaves the 80x80 / 160x160 layers below its tile threshold), so the s@640 run pins it in the network."""
+    from yolomi._lib import lib
     torch.set_num_threads(min(16, torch.get_num_threads()))
-    R = teacher_forced(scale, imgsz, bs, seed=31)
+    prev = lib().ym_conv_set_hpipe(hpipe)
+    try:
+        R = teacher_forced(scale, imgsz, bs, seed=31)
+    finally:
+        lib().ym_conv_set_hpipe(prev)
     kinds = {w.split(" ")[0].split(":")[1] for _, w, _ in R.rows}
     assert any("model.0" in k for k in kinds)                   # the stem was checked

@@ -379,11 +379,11 @@ def test_loss_with_host_max_gt_matches_synced_count():
         assert torch.equal(a, c)
 
 
-@pytest.mark.parametrize("c,shape", [(32, (2, 64, 64)), (32, (3, 47, 61)), (24, (2, 40, 36))])
+@pytest.mark.parametrize("c,shape", [(32, (2, 64, 64)), (32, (3, 47, 61)), (128, (2, 40, 36))])
 def test_stem_block_vs_torch_fp32(c, shape):
     """The stem Conv(1, c, 3, 2) block on its own vs PyTorch fp32 (CPU) on the same input / output gradient:
     c = 32 runs the fused stored-z backward (ym_stem_bwd_wgrad_stored, BN apply inside the weight gradient;
-    odd map sizes give partial 8x32 tiles), c = 24 the generic one (ym_bn_bwd_apply + ym_conv_first_wgrad).
+    odd map sizes give partial 8x32 tiles), c = 128 the generic one (ym_bn_bwd_apply + ym_conv_first_wgrad).
     y within 1e-2, parameter gradients within 2e-2, running statistics within 1e-2 (relative L2)."""
     import models as M
     g = torch.Generator().manual_seed(sum(shape) + c)
@@ -412,3 +412,66 @@ def test_stem_block_vs_torch_fp32(c, shape):
         p = dict(mod.named_parameters())[k]
         assert rel(p.grad, r) < 2e-2, (k, rel(p.grad, r))
     assert rel(mod.bn.running_mean, rm) < 1e-2 and rel(mod.bn.running_var, rv) < 1e-2
+
+
+def test_sppf_block_tie_free_vs_torch_fp32():
+    """SPPF (yolo11_modules.py:92-105) as a block on inputs whose 5x5 pool maxima are tie-free: every pixel of an
+    image carries a distinct value of a random permutation (spacing 1/256), the same for all channels up to a
+    positive gain, and cv1 (positive weights, BN beta 3) keeps that order through SiLU — so every window's
+    maximum leads the next DISTINCT value by >= 4x the fp16 rounding of the GPU path, and the 16-bit path routes
+    every pooled gradient where fp32 does (copies of one source value, which the chained pools create, are exact
+    ties on both paths and resolve to the same first maximum).  The margin is asserted on the fp32 reference's
+    own windows.  Bounds: y within 1e-2, dx and parameter gradients within 2e-2 (relative L2) against PyTorch
+    fp32 on the CPU; the fixture test above keeps random inputs at 1e-1 (near-tied windows there)."""
+    import models as M
+    F = torch.nn.functional
+    g = torch.Generator().manual_seed(11)
+    B, C, H, W = 2, 64, 16, 16
+    base = torch.stack([torch.randperm(H * W, generator=g).view(H, W).float() / (H * W) for _ in range(B)])
+    x = base.view(B, 1, H, W) * (torch.rand(1, C, 1, 1, generator=g) + 0.5)
+    mod = M.SPPF(C, C, 5)
+    for m_ in mod.modules():
+        if isinstance(m_, torch.nn.BatchNorm2d):
+            m_.eps, m_.momentum = 1e-3, 0.03
+    with torch.no_grad():
+        mod.cv1.conv.weight.copy_(torch.rand(mod.cv1.conv.weight.shape, generator=g) + 0.1)
+        mod.cv1.bn.bias.fill_(3.0)
+    ref_sd = {k: v.clone() for k, v in mod.state_dict().items()}
+    xr = x.clone().requires_grad_(True)
+    P = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in ref_sd.items()
+         if "num_batches" not in k}
+
+    def cbs(t, pre):
+        z = F.conv2d(t, P[pre + ".conv.weight"])
+        u = F.batch_norm(z, P[pre + ".bn.running_mean"].detach().clone(), P[pre + ".bn.running_var"].detach().clone(),
+                         P[pre + ".bn.weight"], P[pre + ".bn.bias"], True, 0.03, 1e-3)
+        return F.silu(u)
+    a = cbs(xr, "cv1")
+    p1 = F.max_pool2d(a, 5, 1, 2)
+    p2 = F.max_pool2d(p1, 5, 1, 2)
+    p3 = F.max_pool2d(p2, 5, 1, 2)
+    yr = cbs(torch.cat((a, p1, p2, p3), 1), "cv2")
+    for t in (a, p1, p2):      # margin of every window's maximum over its next distinct value
+        win = F.unfold(F.pad(t.detach(), (2, 2, 2, 2), value=-1e9), 5).view(B, t.shape[1], 25, H * W)
+        mx = win.max(2, keepdim=True).values
+        second = torch.where(win < mx, win, torch.full_like(win, -1e9)).max(2).values
+        gap = ((mx[:, :, 0] - second) / mx[:, :, 0].abs()).min()
+        assert float(gap) > 4 * 2.0 ** -11, float(gap)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    mod.load_state_dict(ref_sd)
+    mod = mod.cuda().train()
+    xg = x.cuda().requires_grad_(True)
+    y = mod(xg)
+    y.backward(dy.cuda())
+    assert rel(y.detach(), yr.detach()) < 1e-2, rel(y.detach(), yr.detach())
+    assert rel(xg.grad, xr.grad) < 2e-2, rel(xg.grad, xr.grad)
+    # cv1's weight gradient is exactly 0 here: every input channel is the same spatial pattern up to a gain, so
+    # cv1's conv only scales that pattern per output channel and its training-mode BN removes the scale; it is
+    # held on the block's gradient scale instead (as the network tests do for BN-invariant parameters)
+    scale = max(float(P[k].grad.norm()) for k in P if P[k].grad is not None)
+    for k, p in mod.named_parameters():
+        if float(P[k].grad.norm()) < 1e-4 * scale:
+            assert float(p.grad.norm()) < 2e-2 * scale, (k, float(p.grad.norm()), scale)
+            continue
+        assert rel(p.grad, P[k].grad) < 2e-2, (k, rel(p.grad, P[k].grad))

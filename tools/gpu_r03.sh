@@ -30,3 +30,6 @@ F=$(find $OUT/pmc_FETCH_SIZE -name "*counter_collection.csv" | head -1)
 W=$(find $OUT/pmc_WRITE_SIZE -name "*counter_collection.csv" | head -1)
 python3 $R/tools/pmc_layers.py $F $W $OUT/seq.json profiles/r03 > $OUT/pmc_layers.txt && tail -3 $OUT/pmc_layers.txt
 cp $R/profiles/traffic.json $OUT/traffic.json
+timeout -k 10 300 python3 $R/tools/miopen_ref.py > $OUT/miopen_ref.txt 2> $OUT/miopen_ref.err || { echo "miopen ref failed"; tail -5 $OUT/miopen_ref.err; }
+cat $OUT/miopen_ref.txt
+bash $R/tools/pmc_conv.sh $OUT/pmc73 73 && python3 $R/tools/pmc_summary.py $OUT/pmc73 > $OUT/pmc73_summary.txt; cat $OUT/pmc73_summary.txt

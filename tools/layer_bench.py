@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=int, nargs="*", help="plan op indices to time (default: every ConvBN)")
+    ap.add_argument("--hpipe", type=int, default=-1, help="ym_conv_set_hpipe policy for this run (A/B)")
     ap.add_argument("--seq-out", help="counter-pass mode: write the (op, kind, k, flops, launches) order of the "
                                       "timed groups here and separate the groups with a marker kernel "
                                       "(tools/pmc_layers.py splits a rocprofv3 --pmc pass on the markers)")
@@ -35,6 +36,8 @@ def main():
     from yolomi._lib import call, stream_ptr
     from yolomi.graph import ConvBN
 
+    from yolomi._lib import lib
+    lib().ym_conv_set_hpipe(args.hpipe)
     dev = torch.device("cuda", 0)
     cfg = yaml.safe_load((ROOT / "yolo-scratch_amd" / "configs" / "yolo11n_crater.yaml").read_text())
     cfg["scale"] = args.scale

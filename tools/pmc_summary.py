@@ -31,7 +31,7 @@ def main():
         per = collections.defaultdict(lambda: collections.defaultdict(list))   # fam -> dispatch -> rows
         for r in rows:
             fam = family(r["Kernel_Name"])
-            if not any(k in fam for k in ("conv_gemm", "wgrad3", "wgrad1", "conv_halo")):
+            if not any(k in fam for k in ("conv_gemm", "wgrad3", "wgrad1", "conv_halo", "conv_pipe", "conv_hpipe")):
                 continue
             per[fam][int(r["Dispatch_Id"])].append(r)
         for fam, disp in per.items():

@@ -31,6 +31,7 @@
 #include "conv_direct.h"
 #include "conv_epi.h"
 #include "conv_halo.h"
+#include "conv_hpipe.h"
 #include "conv_pipe.h"
 #include "reduce.h"
 #include "tile.h"
@@ -795,10 +796,20 @@ extern "C" int ym_conv_set_direct(int mode) {
     return prev;
 }
 
+extern "C" int ym_conv_set_hpipe(int mode) {
+    // selection policy of the halo-staged pipelined 3x3 kernel: -1 default, 0 never, 1 eligible layers of
+    // >= 512 tiles (default), 2 every eligible layer; returns the previous setting
+    const int prev = g_hpipe_force;
+    g_hpipe_force = mode < -1 || mode > 2 ? -1 : mode;
+    return prev;
+}
+
 extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
-    // 3: direct register-weight kernel (conv_direct.hip), 2: persistent pipelined implicit GEMM
-    // (conv_pipe.hip), 1: halo-staged 3x3 kernel (conv_halo.hip), 0: 2-stage implicit GEMM
+    // 4: halo-staged pipelined 3x3 kernel (conv_hpipe.hip), 3: direct register-weight kernel
+    // (conv_direct.hip), 2: persistent pipelined implicit GEMM (conv_pipe.hip), 1: halo-staged 3x3 kernel
+    // (conv_halo.hip), 0: 2-stage implicit GEMM
     if (d && direct_plan(d, dgrad ? 1 : 0).ok) return 3;
+    if (d && hpipe_plan(d, dgrad ? 1 : 0).ok) return 4;
     if (d && pipe_plan(d, dgrad ? 1 : 0).ok) return 2;
     return d && halo_plan(d, dgrad ? 1 : 0).ok ? 1 : 0;
 }
@@ -808,6 +819,8 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     if (!d) return 0;
     const DirectPlan dp = direct_plan(d, 0);
     if (dp.ok) return dp.grid;
+    const HPipePlan hq = hpipe_plan(d, 0);
+    if (hq.ok) return hq.rows;
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) return pp.rows;
     const HaloPlan hp = halo_plan(d, 0);
@@ -844,6 +857,12 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
         return YM_OK;
     }
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
+    const HPipePlan hq = hpipe_plan(d, 0);
+    if (hq.ok) {
+        hpipe_launch(hq, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_fwd (hpipe)");
+        return YM_OK;
+    }
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) {
@@ -897,6 +916,12 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     if (dp.ok) {
         direct_launch(dp, d, 1, dz, wt, dx, nullptr, nullptr, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_dgrad (direct)");
+        return YM_OK;
+    }
+    const HPipePlan hq = hpipe_plan(d, 1);
+    if (hq.ok) {
+        hpipe_launch(hq, d, 1, dz, wt, dx, nullptr, nullptr, as_stream(stream));
+        YM_LAUNCH_CHECK("ym_conv_dgrad (hpipe)");
         return YM_OK;
     }
     const PipePlan pp = pipe_plan(d, 1);

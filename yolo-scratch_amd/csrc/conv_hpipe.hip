@@ -1,0 +1,441 @@
+// Halo-staged persistent pipelined 3x3 stride-1 convolution for gfx950 (fp16 forward, bf16 data
+// gradient, fp32 accumulate) — the 3x3 layers on maps whose sides are multiples of 16 (80x80, 160x160
+// at s@640; 160x160 / 320x320 at m@1280).
+//
+// Replaces nn.Conv2d (k=3, s=1, p=1) forward / input-gradient inside Conv and Bottleneck
+// (/root/reference/yolo_scratch_cuda/models/yolo11_modules.py:21-47, Detect :221-234).
+//
+// Why: conv_pipe.hip's implicit GEMM stages the input once PER TAP — a 256 x 128 tile's K step moves
+// 48 KB (32 KB of it gathered input) for 4.2 MFLOP, and that L2 -> LDS stream, not the MFMA, bounds it
+// (~0.3 of the MFMA peak).  Here the output tile is a 16 x 16 pixel RECTANGLE of one
+// image, and each 64-channel chunk of its 18 x 18 input halo is staged ONCE and read by all nine taps
+// (shifted LDS windows); only the 16 KB weight slice of a tap is staged per K step.  Per 9 K steps:
+// 41.5 KB of halo + 9 x 16 KB of weights = 186 KB instead of 432 KB (2.3x fewer staged bytes per FLOP).
+// Everything else is conv_pipe's structure:
+//  * 256 pixels x 128 (or 64) channels per tile on 8 waves of 64 x 64 (64 x 32);
+//  * K step = one tap of one 64-channel chunk (two 32-deep halves); weights through a 3-slot LDS ring
+//    with two slots in flight (LDS-DMA, counted vmcnt waits, raw s_barrier); the halo double-buffered,
+//    the next chunk's halo issued at the first K step of the current chunk (9 steps of cover);
+//  * the barrier in the middle of a K step: every LDS read has 16 MFMAs to hide behind;
+//  * persistent workgroups (one per CU), tiles grouped per XCD, the channel tiles of one pixel tile on
+//    one XCD; BatchNorm statistics in registers across a workgroup's tiles, one partial row each;
+//  * LDS-transposed epilogue with 16-B row stores.
+// Halo LDS rows are 128 B (64 channels); row r stores logical 16-B chunk c at slot c ^ (r & 7), which is
+// conflict-free for ds_read_b128 at EVERY starting row (the tap shifts start fragments at arbitrary rows;
+// conv_pipe's (r >> 1) & 7 swizzle conflicts 2-way there — checked with a bank model of the four
+// ds_read_b128 lane groups).
+#include <algorithm>
+
+#include "common.h"
+#include "conv_hpipe.h"
+#include "tile.h"
+
+namespace ym {
+
+int g_hpipe_force = -1;
+
+namespace {
+
+constexpr int HF = 0;   // forward: fp16 x fp16
+constexpr int HD = 1;   // data gradient (of a stride-1 conv): bf16 x bf16, taps flipped
+
+constexpr int TS = 16;                    // output tile side (pixels)
+constexpr int HS = TS + 2;                // halo side
+constexpr int HROWS = HS * HS;            // 324 halo pixels
+constexpr int HPIECES = (HROWS + 7) / 8;  // 41 DMA pieces of 8 pixel rows (the last half out of range)
+constexpr int HBUF = HPIECES * 1024;      // bytes per halo buffer
+constexpr int RB = 128;                   // 64 channels x 2 B per LDS row
+
+struct HArgs {
+    const bf16_t* x; int64_t x_bs, x_ld;     // input view (forward: x; data gradient: dz)
+    const bf16_t* w;                          // [Nout][3][3][Kin]
+    void* y; int64_t y_bs, y_ld;              // output view
+    float* st_sum; float* st_sq;              // [rows][Nout] or null
+    int H, W, Kin, Nout, N;
+    int out_f32, accumulate;
+    int ntiles;                               // channel tiles
+    int tpr, tpi;                             // tiles per tile-row (W / 16), per image
+    int mt_total;                             // pixel tiles: N * tpi
+};
+
+__device__ __forceinline__ int fsw128(int r) { return (r >> 1) & 7; }   // weight rows (aligned reads)
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+    asm volatile("" ::: "memory");
+}
+
+// runtime (wave-uniform) vmcnt: the pending-DMA count after the stage a step needs depends on whether
+// a halo was issued in between
+__device__ __forceinline__ void vm_wait_n(int n) {
+    switch (n) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<1>(); break;
+        case 2: vm_wait<2>(); break;
+        case 3: vm_wait<3>(); break;
+        case 4: vm_wait<4>(); break;
+        case 5: vm_wait<5>(); break;
+        case 6: vm_wait<6>(); break;
+        case 7: vm_wait<7>(); break;
+        case 8: vm_wait<8>(); break;
+        case 9: vm_wait<9>(); break;
+        case 10: vm_wait<10>(); break;
+        case 11: vm_wait<11>(); break;
+        default: vm_wait<12>(); break;
+    }
+}
+
+__device__ __forceinline__ void step_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int BN, int WM, int WN, int MODE>
+__global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
+    constexpr int NS = 4;                     // weight ring: slot of step g computing, g+1..g+3 in flight
+    constexpr int NW = WM * WN;
+    static_assert(NW == 8, "8 waves");
+    constexpr int AI = BN / 8 / NW;           // weight DMA pieces per wave per step
+    constexpr int TM = BN / WM / 16;          // 16-channel subtiles per wave
+    constexpr int TN = TS / WN;               // tile rows (16-pixel subtiles) per wave
+    constexpr int WSLOT = BN * RB;
+    constexpr int WCH = BN / WM;              // channels per wave
+    constexpr int EPW = 16 * WCH * 2;         // epilogue transpose area per wave
+    constexpr int HI_MAX = (HPIECES + NW - 1) / NW;   // halo pieces of wave 0 (others one fewer or equal)
+    static_assert(AI >= 1 && TM >= 1 && TN >= 1, "tile");
+    // the epilogue's transpose area is the halo buffer of the tile's last chunk: after the middle barrier of
+    // the tile's last K step no wave reads it, and the next halo DMA into it is issued a K step later
+    static_assert(NW * EPW <= HBUF, "epilogue area inside a halo buffer");
+    static_assert(2 * HBUF + NS * WSLOT <= 160 * 1024, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char smem[2 * HBUF + NS * WSLOT];
+    char* const hbuf0 = smem;
+    char* const wring = smem + 2 * HBUF;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave / WN, wc = wave % WN;
+    const int fc = lane >> 4, fr = lane & 15;
+    const int CC = a.Kin >> 6;                // 64-channel chunks
+    const int hi_w = (HPIECES - wave + NW - 1) / NW;   // this wave's halo pieces (wave-uniform)
+
+    // ---- this workgroup's tiles: channel tile fixed, pixel tiles of its XCD's range (as conv_pipe)
+    const int G8 = int(gridDim.x) >> 3;
+    const int xcd = int(blockIdx.x) & 7, q = int(blockIdx.x) >> 3;
+    const int nt = q % a.ntiles, qq = q / a.ntiles, qstride = G8 / a.ntiles;
+    const int per = (a.mt_total + 7) >> 3;
+    const int mt_lo = xcd * per + qq, mt_hi = min(xcd * per + per, a.mt_total);
+    const int ntile = mt_lo < mt_hi ? (mt_hi - mt_lo + qstride - 1) / qstride : 0;
+    const int n0 = nt * BN;
+    const int spt = 9 * CC;                   // K steps per tile
+    const int total = ntile * spt;
+
+    // weight DMA rows (fixed): row r of the A image = output channel n0 + r
+    const uint32_t wrow_b = uint32_t(9 * a.Kin) * 2u;
+    const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
+    uint32_t a_off[AI];
+#pragma unroll
+    for (int j = 0; j < AI; ++j) {
+        const int r = (wave * AI + j) * 8 + (lane >> 3);
+        const int ch = n0 + r;
+        a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t((lane & 7) ^ fsw128(r)) * 16u : OOB;
+    }
+    const __amdgpu_buffer_rsrc_t xres = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
+
+    // ---- issue side: weight stage s -> (chunk, tap); halo of global chunk h -> (tile, chunk)
+    auto issue_w = [&](int s) {
+        const int within = s % spt;
+        const int cc = within / 9, tap = within - cc * 9;
+        const uint32_t soff = uint32_t(tap * a.Kin + cc * 64) * 2u;
+        char* st = wring + (s % NS) * WSLOT;
+#pragma unroll
+        for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, a_off[j], soff);
+    };
+    uint32_t hoff[HI_MAX];                    // per-lane halo offsets of the tile being staged
+    int h_tile = -1;
+    auto issue_h = [&](int h) {
+        const int t = h / CC, cc = h - t * CC;
+        if (t != h_tile) {
+            h_tile = t;
+            const int mt = mt_lo + t * qstride;
+            const int n = mt / a.tpi, rem = mt - n * a.tpi;
+            const int ty = rem / a.tpr, tx = rem - ty * a.tpr;
+#pragma unroll
+            for (int j = 0; j < HI_MAX; ++j) {
+                const int hr = (wave + NW * j) * 8 + (lane >> 3);
+                const int iy = ty * TS - 1 + hr / HS, ix = tx * TS - 1 + hr % HS;
+                const bool ok = hr < HROWS && uint32_t(iy) < uint32_t(a.H) && uint32_t(ix) < uint32_t(a.W);
+                hoff[j] = ok ? uint32_t((int64_t(n) * a.x_bs + (int64_t(iy) * a.W + ix) * a.x_ld) * 2) +
+                                   uint32_t((lane & 7) ^ (hr & 7)) * 16u
+                             : OOB;
+            }
+        }
+        char* hb = hbuf0 + (h & 1) * HBUF;
+#pragma unroll
+        for (int j = 0; j < HI_MAX; ++j)
+            if (j < hi_w) dma16(xres, hb + (wave + NW * j) * 1024, hoff[j], uint32_t(cc * 64) * 2u);
+    };
+
+    // per-lane fragment offsets: A as conv_pipe; B = halo rows of this wave's tile rows
+    uint32_t offA[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        const int ra = wr * (BN / WM) + fr;
+        offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
+    }
+    bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
+    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int g, int kk) {
+        const int within = g % spt;
+        const int cc = within / 9, tap = within - cc * 9;
+        const int kh = tap / 3, kw = tap - kh * 3;
+        const int dh = MODE == HF ? kh : 2 - kh, dw = MODE == HF ? kw : 2 - kw;
+        const char* As = wring + (g % NS) * WSLOT + offA[kk];
+        const char* Hs = hbuf0 + ((g / spt * CC + cc) & 1) * HBUF;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int hr = (wc * TN + j + dh) * HS + fr + dw;
+            fb[j] = *reinterpret_cast<const bf16x8*>(Hs + hr * RB + (((kk * 4 + fc) ^ (hr & 7)) << 4));
+        }
+    };
+    f32x4 acc[TM][TN];
+    auto mma = [&](const bf16x8* fa, const bf16x8* fb) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (MODE == HF)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
+                                                                        __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0,
+                                                                        0, 0);
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+    };
+
+    float ssum[TM][4], ssq[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
+
+    // ---- prologue: halo of chunk 0, weight stages 0..3; stage 0 and the halo landed everywhere
+    const int nchunks = ntile * CC;
+    if (total > 0) issue_h(0);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+        if (s < total) issue_w(s);
+    vm_wait_n(AI * (min(total, NS) - 1));
+    step_barrier();
+    if (total > 0) read_frags(f0a, f0b, 0, 0);
+
+    int ct = 0, ck = 0;
+    for (int g = 0; g < total; ++g) {
+        if (ck == 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        read_frags(f1a, f1b, g, 1);
+        mma(f0a, f0b);
+        // stage g+1 must have landed (own DMAs); stages g+2 and g+3 may stay in flight, and so may halos
+        // issued in steps g-2 and g-1 (after stage g+1, when those steps began a chunk with a successor)
+        if (g + 1 < total) {
+            int pend = (g + 2 < total ? AI : 0) + (g + 3 < total ? AI : 0);
+#pragma unroll
+            for (int b = 1; b <= 2; ++b) {
+                const int gs = g - b;
+                if (gs >= 0 && gs % 9 == 0 && gs / 9 + 1 < nchunks) pend += hi_w;
+            }
+            vm_wait_n(pend);
+        }
+        step_barrier();
+        // the halo buffer of chunk h-1 and the weight slot of step g are free (their reads returned before
+        // the barrier): the next chunk's halo at its predecessor's first step, then weight stage g+4
+        if (g % 9 == 0 && g / 9 + 1 < nchunks) issue_h(g / 9 + 1);
+        if (g + NS < total) issue_w(g + NS);
+        if (g + 1 < total) read_frags(f0a, f0b, g + 1, 0);
+        mma(f1a, f1b);
+        if (++ck < spt) continue;
+        ck = 0;
+
+        // ---- epilogue of tile ct (conv_pipe's LDS-transposed 16-B row stores)
+        const int mt = mt_lo + ct * qstride;
+        ++ct;
+        const int n = mt / a.tpi, rem = mt - n * a.tpi;
+        const int ty = rem / a.tpr, tx = rem - ty * a.tpr;
+        char* ep = hbuf0 + ((ct * CC - 1) & 1) * HBUF + wave * EPW;     // (ct already advanced)
+        const int wch0 = n0 + wr * WCH;
+        const bool half = a.out_f32 == 2;
+        const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.H) * a.W * a.y_ld) * 2;
+        const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
+        constexpr int CPR = WCH * 2 / 16;
+        constexpr int RPS = 64 / CPR;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int cb = wch0 + i * 16 + fc * 4;
+                if (a.st_sum) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (cb + r < a.Nout) {
+                            const float v = acc[i][j][r];
+                            ssum[i][r] += v;
+                            ssq[i][r] += v * v;
+                        }
+                }
+                uint2 o;
+                if (half) {
+                    o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
+                    o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
+                } else {
+                    o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
+                    o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
+                }
+                const int byte = (i * 16 + fc * 4) * 2;
+                const int chunk = (byte >> 4) ^ (fr & (CPR - 1));
+                *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            const int oy = ty * TS + wc * TN + j;
+#pragma unroll
+            for (int h = 0; h < 16 / RPS; ++h) {
+                const int p = h * RPS + lane / CPR, c = lane % CPR;
+                const uint4 v = *reinterpret_cast<const uint4*>(ep + p * (WCH * 2) + ((c ^ (p & (CPR - 1))) * 16));
+                const int ox = tx * TS + p;
+                const uint32_t off = wch0 + c * 8 < a.Nout
+                                         ? uint32_t((int64_t(n) * a.y_bs + (int64_t(oy) * a.W + ox) * a.y_ld + wch0 +
+                                                     c * 8) * 2)
+                                         : OOB;
+                uint4 wv = v;
+                if (a.accumulate) {
+                    const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
+                    uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
+                                      bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
+                    wv = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, wv),
+                                                       yres, off, 0, 0);
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+        }
+    }
+
+    if (a.st_sum) {
+        vm_wait<0>();
+        __syncthreads();
+        float (*red)[WN][BN] = reinterpret_cast<float (*)[WN][BN]>(smem);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float s = ssum[i][r], sq = ssq[i][r];
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) {
+                    s += __shfl_xor(s, o, 64);
+                    sq += __shfl_xor(sq, o, 64);
+                }
+                if (fr == 0) {
+                    const int cl = wr * (BN / WM) + i * 16 + fc * 4 + r;
+                    red[0][wc][cl] = s;
+                    red[1][wc][cl] = sq;
+                }
+            }
+        __syncthreads();
+        const int row = xcd + 8 * qq;
+        for (int cl = tid; cl < BN; cl += NW * 64) {
+            const int ch = n0 + cl;
+            if (ch < a.Nout) {
+                float ps = 0.f, pq = 0.f;
+#pragma unroll
+                for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
+                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
+                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad) {
+    HPipePlan p{};
+    const int mode = g_hpipe_force >= 0 ? g_hpipe_force : 1;
+    if (!d || mode == 0) return p;
+    if (d->k != 3 || d->stride != 1 || d->pad != 1) return p;
+    if (d->h != d->oh || d->w != d->ow || d->h % TS || d->w % TS) return p;
+    const int kin = dgrad ? d->cout : d->cin, nout = dgrad ? d->cin : d->cout;
+    // >= 128 output channels: the 64-channel tile (8 MFMAs per half step and wave) measured slower than
+    // conv_halo.hip on the 64-channel 80x80 layers (0.080 vs 0.070 ms fwd, s@640 bs64)
+    if (kin % 64 != 0 || nout % 8 != 0 || nout < 128) return p;
+    const int64_t in_ld = dgrad ? d->y_ld : d->x_ld, in_bs = dgrad ? d->y_bs : d->x_bs;
+    const int64_t out_ld = dgrad ? d->x_ld : d->y_ld, out_bs = dgrad ? d->x_bs : d->y_bs;
+    if (in_ld % 8 || in_bs % 8 || out_ld % 8 || out_bs % 8) return p;
+    if (!dgrad && d->out_f32 == 1) return p;                     // Detect's fp32 bias convs: conv.hip
+    if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31) || int64_t(d->n) * out_bs * 2 >= (int64_t(1) << 31)) return p;
+    p.cfg = nout >= 128 ? 0 : 1;
+    const int bn = p.cfg == 0 ? 128 : 64;
+    const int ntiles = (nout + bn - 1) / bn;
+    const int64_t tiles = int64_t(d->n) * (d->h / TS) * (d->w / TS);
+    if (mode == 1 && tiles * ntiles < 512) return p;          // several tiles per CU (tail imbalance)
+    int grid = 256;
+    const int unit = 8 * ntiles;
+    grid = (grid / unit) * unit;
+    if (grid < unit) return p;
+    p.grid = grid;
+    p.rows = grid / ntiles;
+    p.ok = 1;
+    return p;
+}
+
+int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
+                 float* st_sum, float* st_sq, hipStream_t st) {
+    HArgs a{};
+    a.x = x;
+    a.w = w;
+    a.y = y;
+    a.N = d->n;
+    a.H = d->h;
+    a.W = d->w;
+    if (!dgrad) {
+        a.x_bs = d->x_bs; a.x_ld = d->x_ld; a.y_bs = d->y_bs; a.y_ld = d->y_ld;
+        a.Kin = d->cin; a.Nout = d->cout;
+        a.out_f32 = d->out_f32;
+        a.st_sum = st_sum; a.st_sq = st_sq;
+    } else {
+        a.x_bs = d->y_bs; a.x_ld = d->y_ld; a.y_bs = d->x_bs; a.y_ld = d->x_ld;
+        a.Kin = d->cout; a.Nout = d->cin;
+        a.out_f32 = 0;
+    }
+    a.accumulate = d->accumulate;
+    const int bn = p.cfg == 0 ? 128 : 64;
+    a.ntiles = (a.Nout + bn - 1) / bn;
+    a.tpr = a.W / TS;
+    a.tpi = (a.H / TS) * a.tpr;
+    a.mt_total = a.N * a.tpi;
+    if (!dgrad) {
+        if (p.cfg == 0) conv_hpipe_kernel<128, 2, 4, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+        else conv_hpipe_kernel<64, 1, 8, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+    } else {
+        if (p.cfg == 0) conv_hpipe_kernel<128, 2, 4, HD><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+        else conv_hpipe_kernel<64, 1, 8, HD><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+    }
+    return 0;
+}
+
+}  // namespace ym

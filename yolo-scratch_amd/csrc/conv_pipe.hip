@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         offB[kk] = uint32_t(BN * RB + rb * RB + (((kk * 4 + fc) ^ fsw128(rb)) << 4));
     }
     bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
-    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) __device__ {
+    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) {
         const char* As = smem + buf * STAGE + offA[kk];
         const char* Bs = smem + buf * STAGE + offB[kk];
 #pragma unroll
@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * RB);
     };
     f32x4 acc[TM][TN];
-    auto mma = [&](const bf16x8* fa, const bf16x8* fb) __device__ {
+    auto mma = [&](const bf16x8* fa, const bf16x8* fb) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -59,6 +59,7 @@ SIGNATURES = {
     "ym_conv_set_halo": (R, [INT]),
     "ym_conv_set_pipe": (R, [INT]),
     "ym_conv_set_direct": (R, [INT]),
+    "ym_conv_set_hpipe": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
