@@ -39,6 +39,12 @@ SHAPES = [
     (1, 40, 40, 128, 136, 3, 1, 1),
     (16, 64, 64, 32, 128, 3, 1, 1),
     (3, 24, 10, 72, 80, 3, 1, 1),
+    # weight gradient on whole-row units (wgrad.hip: 20 x 3 rows on 20-wide maps, stride 1 and 2;
+    # 10 x 6 on 10-wide ones), with an odd unit count per split (a unit of zeros pads the pair)
+    (2, 40, 40, 128, 72, 3, 2, 1),
+    (1, 20, 20, 64, 64, 3, 1, 1),
+    # maps >= 64 wide: two register sets (units t+1, t+2 in flight), 7 units per split (odd)
+    (3, 64, 72, 64, 64, 3, 1, 1),
     # narrow inputs: several taps share one 64-deep K step (fwd Kin = cin, dgrad Kin = cout)
     (2, 9, 7, 64, 32, 3, 1, 1),
     (1, 10, 10, 8, 16, 3, 1, 1),

@@ -417,12 +417,19 @@ def test_stem_block_vs_torch_fp32(c, shape):
 def test_sppf_block_tie_free_vs_torch_fp32():
     """SPPF (yolo11_modules.py:92-105) as a block on inputs whose 5x5 pool maxima are tie-free: every pixel of an
     image carries a distinct value of a random permutation (spacing 1/256), the same for all channels up to a
-    positive gain, and cv1 (positive weights, BN beta 3) keeps that order through SiLU — so every window's
+    positive gain, and cv1 (positive weights, BN beta 1: u = xhat + 1 >= -0.73, where SiLU is still increasing)
+    keeps that order through SiLU — so every window's
     maximum leads the next DISTINCT value by >= 4x the fp16 rounding of the GPU path, and the 16-bit path routes
     every pooled gradient where fp32 does (copies of one source value, which the chained pools create, are exact
     ties on both paths and resolve to the same first maximum).  The margin is asserted on the fp32 reference's
-    own windows.  Bounds: y within 1e-2, dx and parameter gradients within 2e-2 (relative L2) against PyTorch
-    fp32 on the CPU; the fixture test above keeps random inputs at 1e-1 (near-tied windows there)."""
+    own windows.  Bounds: y within 1e-2 and dx within 2e-2 (relative L2) against PyTorch fp32 on the CPU;
+    parameter gradients within max(2e-2, 2 x the 16-bit storage model's own distance), never above 5e-2 (the
+    model measures 1.6 / 2.3 % on cv1's BN weight / bias here); the fixture test above keeps random inputs at
+    1e-1 (near-tied windows there).
+    (cv1's BN bias gradient is sum(dy_a * silu'(u)) where sum(dy_a) = 0 exactly — cv2's BN backward makes
+    every concat channel's gradient zero-mean and the pools only move it — so with beta 3, where silu' is
+    nearly constant, it was a cancellation residue (0.18 relative error from bf16 gradient storage);
+    beta 1 spreads silu' over 0.3-1.1.)"""
     import models as M
     F = torch.nn.functional
     g = torch.Generator().manual_seed(11)
@@ -435,23 +442,31 @@ def test_sppf_block_tie_free_vs_torch_fp32():
             m_.eps, m_.momentum = 1e-3, 0.03
     with torch.no_grad():
         mod.cv1.conv.weight.copy_(torch.rand(mod.cv1.conv.weight.shape, generator=g) + 0.1)
-        mod.cv1.bn.bias.fill_(3.0)
+        mod.cv1.bn.bias.fill_(1.0)
     ref_sd = {k: v.clone() for k, v in mod.state_dict().items()}
     xr = x.clone().requires_grad_(True)
     P = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k) for k, v in ref_sd.items()
          if "num_batches" not in k}
 
-    def cbs(t, pre):
-        z = F.conv2d(t, P[pre + ".conv.weight"])
-        u = F.batch_norm(z, P[pre + ".bn.running_mean"].detach().clone(), P[pre + ".bn.running_var"].detach().clone(),
-                         P[pre + ".bn.weight"], P[pre + ".bn.bias"], True, 0.03, 1e-3)
-        return F.silu(u)
-    a = cbs(xr, "cv1")
-    p1 = F.max_pool2d(a, 5, 1, 2)
-    p2 = F.max_pool2d(p1, 5, 1, 2)
-    p3 = F.max_pool2d(p2, 5, 1, 2)
-    yr = cbs(torch.cat((a, p1, p2, p3), 1), "cv2")
-    for t in (a, p1, p2):      # margin of every window's maximum over its next distinct value
+    from oracle.precision import _ConvQ, _Round
+
+    def block(P, xin, rounded):
+        def cbs(t, pre):
+            if rounded:        # the HIP path's storage points (oracle/precision.py): fp16 in / z, bf16 grads
+                z = _Round.apply(_ConvQ.apply(_Round.apply(t), P[pre + ".conv.weight"], 1, 1))
+            else:
+                z = F.conv2d(t, P[pre + ".conv.weight"])
+            u = F.batch_norm(z, P[pre + ".bn.running_mean"].detach().clone(),
+                             P[pre + ".bn.running_var"].detach().clone(), P[pre + ".bn.weight"], P[pre + ".bn.bias"],
+                             True, 0.03, 1e-3)
+            return F.silu(u)
+        a = cbs(xin, "cv1")
+        p1 = F.max_pool2d(a, 5, 1, 2)
+        p2 = F.max_pool2d(p1, 5, 1, 2)
+        p3 = F.max_pool2d(p2, 5, 1, 2)
+        return cbs(torch.cat((a, p1, p2, p3), 1), "cv2"), (a, p1, p2)
+    yr, pooled = block(P, xr, False)
+    for t in pooled:           # margin of every window's maximum over its next distinct value
         win = F.unfold(F.pad(t.detach(), (2, 2, 2, 2), value=-1e9), 5).view(B, t.shape[1], 25, H * W)
         mx = win.max(2, keepdim=True).values
         second = torch.where(win < mx, win, torch.full_like(win, -1e9)).max(2).values
@@ -459,6 +474,10 @@ def test_sppf_block_tie_free_vs_torch_fp32():
         assert float(gap) > 4 * 2.0 ** -11, float(gap)
     dy = torch.randn(yr.shape, generator=g)
     yr.backward(dy)
+    # the same block under the 16-bit storage model: its parameter-gradient distance from fp32 is the floor a
+    # correct 16-bit path sits at (cv1's BN gradients are 512-pixel sums of bf16-stored, pool-routed gradients)
+    Pe = {k: v.detach().clone().requires_grad_(v.requires_grad) for k, v in P.items()}
+    block(Pe, x.clone(), True)[0].backward(dy)
     mod.load_state_dict(ref_sd)
     mod = mod.cuda().train()
     xg = x.cuda().requires_grad_(True)
@@ -474,4 +493,5 @@ def test_sppf_block_tie_free_vs_torch_fp32():
         if float(P[k].grad.norm()) < 1e-4 * scale:
             assert float(p.grad.norm()) < 2e-2 * scale, (k, float(p.grad.norm()), scale)
             continue
-        assert rel(p.grad, P[k].grad) < 2e-2, (k, rel(p.grad, P[k].grad))
+        tol = min(5e-2, max(2e-2, 2.0 * rel(Pe[k].grad, P[k].grad)))
+        assert rel(p.grad, P[k].grad) < tol, (k, rel(p.grad, P[k].grad), tol)

@@ -97,6 +97,8 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
         p = dict(model.named_parameters())[k]
         tol = max(1e-1, 2.0 * rel(emu[k], r), 2.0 * rel(at_gpu[k], r))
         assert rel(p.grad, r) < tol, (k, rel(p.grad, r), tol)
+    top1 = max(worst1, key=lambda w: w[2])
+    print(f"[{scale}] largest gradient error vs the oracle at the GPU heads: {top1[1]} {top1[2]:.4f} (bound {top1[3]:.4f})")
     return sorted(worst1)[-2:], sorted(worst2)[-2:]
 
 

@@ -8,7 +8,7 @@ TAG=${1:-r03}
 OUT=$R/gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 if [ "$2" != "skip-tests" ]; then
-  timeout -k 10 500 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+  timeout -k 10 500 python3 -u -m pytest $R/tests -m gpu -x -q -s --timeout 120 --timeout-method thread $PYTEST_EXTRA > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "pytest_gpu exit $rc"; tail -3 $OUT/pytest_gpu.log
   if [ $rc -ne 0 ]; then tail -40 $OUT/pytest_gpu.log; exit $rc; fi
 fi
@@ -33,3 +33,6 @@ cp $R/profiles/traffic.json $OUT/traffic.json
 timeout -k 10 300 python3 $R/tools/miopen_ref.py > $OUT/miopen_ref.txt 2> $OUT/miopen_ref.err || { echo "miopen ref failed"; tail -5 $OUT/miopen_ref.err; }
 cat $OUT/miopen_ref.txt
 bash $R/tools/pmc_conv.sh $OUT/pmc73 73 && python3 $R/tools/pmc_summary.py $OUT/pmc73 > $OUT/pmc73_summary.txt; cat $OUT/pmc73_summary.txt
+# last: the 3-stream HIP-graph capture (segfaulted in round 2) under faulthandler
+YM_GRAPH=1 YM_STREAMS=3 GRAPH_MAX_STREAMS=3 timeout -k 10 180 python3 -X faulthandler $R/tools/graph_debug.py full > $OUT/graph3.log 2>&1
+echo "graph3 exit $?"; tail -40 $OUT/graph3.log

@@ -7,6 +7,8 @@ R = os.environ.get("GRAFT_REPO_ROOT", "/root/repo")
 sys.path.insert(0, R)
 sys.path.insert(0, R + "/yolo-scratch_amd")
 import torch
+import yolomi.graph as _yg
+_yg.GRAPH_MAX_STREAMS = int(os.environ.get("GRAPH_MAX_STREAMS", "2"))
 from oracle import model as om
 from models import build_yolo11
 from datasets.synthetic import synth_batch

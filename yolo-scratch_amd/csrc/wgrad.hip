@@ -9,8 +9,9 @@
 // no zero-fill by the caller.
 //
 // wgrad3_kernel<S>  3x3, pad 1, stride S in {1, 2}: one workgroup owns a 64co x 64ci tile for
-//   ALL nine taps (144 fp32 accumulators per lane).  Per 8x8 block of output pixels it stages
-//   dz (64 pixels x 64 co) and the input halo ((7S+3)^2 pixels x 64 ci) once — fp16
+//   ALL nine taps (144 fp32 accumulators per lane).  Per unit of <= 64 output pixels (an 8x8 block,
+//   or whole rows of a narrow map) it stages dz (64 pixels x 64 co) and the input halo ((7S+3)^2
+//   pixels x 64 ci for 8x8) once — fp16
 //   activations converted to bf16 once — and every tap reads its shifted window out of the same
 //   halo with transposed LDS reads (ds_read_b64_tr_b16) whose tap offsets are immediates.
 // wgrad1_kernel<T>  1x1 stride 1 over whole-image views: pixels are a flat axis, so each lane's
@@ -33,7 +34,7 @@ struct WgArgs {
     float* part;                              // [splits][Cout][taps][Cin] fp32
     int N, IH, IW, Cin, OH, OW, Cout, KH, KW, stride, pad;
     int64_t M;                                // N*OH*OW
-    int64_t units;                            // K units: 64-pixel stages (1x1), 8x8 tiles (3x3), 32-pixel steps
+    int64_t units;                            // K units: 64-pixel stages (1x1), tw x th rectangles (3x3), 32-pixel steps
     int64_t chunk;                            // units per split
     int ci_tiles;                             // generic kernel: channel tiles per tap column
     int co_t, ci_t, splits;                   // wgrad3 / wgrad1: tile grid (1-D launch, see wg_tile)
@@ -70,15 +71,22 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
 }
 
 // ------------------------------------------------------------------ 3x3
-// TCO x TCI (64 or 32) channel tiles.  NWV = 4: waves own (co half, ci half), all 9 taps;
-// NWV = 8: waves own (co half, ci quarter) of a 64-ci tile, two waves per SIMD sharing the same
-// staged dz / halo.  32-channel tiles serve the 32-channel layers of the stem stage, which a 64x64
-// tile ran three-quarters empty (zero-filled channels through every MFMA).
-template <int S, int NWV, int TCO, int TCI>
-__global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
+// TCO x TCI (64 or 32) channel tiles; a wave owns WCO co x WCI ci of the tile for all 9 taps
+// ((TCO/WCO) x (TCI/WCI) waves).  Per 32-pixel k step a wave reads its co fragments once and every
+// tap's ci fragments once, so LDS bytes per MFMA = 1 KB / (WCO/16) + (WCO/16) KB / (9 WCI/16): the
+// 64 x 16 waves of the stride-1 64x64 tiles (4 waves) read 0.36 KB per MFMA where 32 x 16 waves
+// (8 waves) read 0.61 — 152 B/clk per CU against LDS's 128, which bounded the kernel.  32-channel
+// tiles serve the 32-channel layers of the stem stage, which a 64x64 tile ran three-quarters empty.
+// A K unit is a tw x th rectangle of output pixels (tw * th <= 64; the plan picks 8x8, or whole
+// rows — 20 x 3 — on the 20-wide maps, where 8x8 tiles cover 24x24 = 1.44x the pixels).  The units
+// of a split are staged through two register sets: while unit t is multiplied, the loads of units
+// t + 1 and t + 2 are in flight.
+template <int S, int TCO, int TCI, int WCO, int WCI, int TW, int TH, bool DEEP>
+__global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(WgArgs a) {
+    constexpr int NWC = TCI / WCI;            // waves along ci
+    constexpr int NWV = (TCO / WCO) * NWC;
     constexpr int NT = NWV * 64;
-    constexpr int TI = TCO / 32;              // 16-co subtiles per wave (waves split co in halves)
-    constexpr int WCI = TCI / (NWV / 2);      // ci per wave
+    constexpr int TI = WCO / 16;              // 16-co subtiles per wave
     constexpr int TJ = WCI / 16;              // 16-ci subtiles per wave
     static_assert(TI >= 1 && TJ >= 1, "wgrad3 tile geometry");
     constexpr int CPD = TCO / 8, CPX = TCI / 8;       // 16-B chunks per dz / halo row
@@ -86,39 +94,47 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
     constexpr int DI = (64 + RPD - 1) / RPD;  // dz chunks per thread (threads past row 63 idle)
     constexpr int RSD = TCO * 2 + 32;         // dz rows: consecutive-row tr reads conflict free
     constexpr int RSX = TCI * 2 + (S == 1 ? 32 : 16);   // halo rows: reads step S rows
-    constexpr int HD = 7 * S + 3;             // halo side
-    constexpr int HR = HD * HD;
+    constexpr int TP = TW * TH;               // pixels of a unit (<= 64)
+    constexpr int HW = (TW - 1) * S + 3, HR = ((TH - 1) * S + 3) * HW;   // halo width / rows
     constexpr int XI = (HR + RPX - 1) / RPX;  // 16-B halo chunks per thread
+    static_assert(TP <= 64, "wgrad3 unit");
     __shared__ __attribute__((aligned(16))) char Dz[64 * RSD];
     __shared__ __attribute__((aligned(16))) char Xh[HR * RSX];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wr = wave / (NWV / 2), wc = wave % (NWV / 2);
+    const int wr = wave / NWC, wc = wave % NWC;
     int cot, cit, split;
     wg_tile(a, cot, cit, split);
     const int co0 = cot * TCO, ci0 = cit * TCI;
     const int dsc = tid % CPD, dsrow = tid / CPD;     // staging: chunk of rows row + RP*it
     const int xsc = tid % CPX, xsrow = tid / CPX;
     const bool co_ok = co0 + dsc * 8 < a.Cout, ci_ok = ci0 + xsc * 8 < a.Cin;
-    int x_hy[XI], x_hx[XI];
+    int d_py[DI], d_px[DI], x_hy[XI], x_hx[XI];
+#pragma unroll
+    for (int it = 0; it < DI; ++it) {
+        const int p = dsrow + RPD * it;
+        d_py[it] = p < TP ? p / TW : 1 << 20;         // pixel slots past the unit stage zeros
+        d_px[it] = p < TP ? p - (p / TW) * TW : 0;
+    }
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
         const int r = xsrow + RPX * it;
-        x_hy[it] = r / HD;
-        x_hx[it] = r - x_hy[it] * HD;
+        x_hy[it] = r / HW;
+        x_hx[it] = r - x_hy[it] * HW;
     }
-    const int ntw = (a.OW + 7) >> 3, nth = (a.OH + 7) >> 3;
+    const int ntw = (a.OW + TW - 1) / TW, nth = (a.OH + TH - 1) / TH;
     const int64_t t_begin = int64_t(split) * a.chunk;
     const int64_t t_end = std::min<int64_t>(a.units, t_begin + a.chunk);
 
-    // fragment-read geometry: lane's k rows (pixels of the 8x8 tile) for the two 32-pixel halves
+    // fragment-read geometry: lane's k rows (pixels of the unit) for the two 32-pixel halves; pixel
+    // slots past the unit read halo row 0 (always staged, finite) against their zero dz rows
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     int hb_lo[2], hb_hi[2];                   // halo row of (pixel, tap 0,0)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
         const int plo = kk * 32 + 4 * g + q, phi = plo + 16;
-        hb_lo[kk] = (plo >> 3) * S * HD + (plo & 7) * S;
-        hb_hi[kk] = (phi >> 3) * S * HD + (phi & 7) * S;
+        hb_lo[kk] = plo < TP ? (plo / TW) * S * HW + (plo % TW) * S : 0;
+        hb_hi[kk] = phi < TP ? (phi / TW) * S * HW + (phi % TW) * S : 0;
     }
 
     f32x4 acc[9][TI][TJ];
@@ -129,30 +145,30 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
 #pragma unroll
             for (int j = 0; j < TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 rdz[DI], rx[XI];
-    auto load = [&](int64_t t) {
-        const int tw = int(t % ntw);
-        const int64_t r = t / ntw;
-        const int th = int(r % nth), n = int(r / nth);
-        const int oh0 = th * 8, ow0 = tw * 8;
+    uint4 da[DI], xa[XI], db[DI], xb[XI];
+    auto load = [&](int64_t t, uint4 (&rdz)[DI], uint4 (&rx)[XI]) {
+        const bool live = t < t_end;              // past the split: zeros, no branch around the loads
+        const int u = int(live ? t : t_begin);     // units < 2^31 (M < 2^31, checked on the host)
+        const int tw = u % ntw, r = u / ntw;
+        const int th = r % nth, n = r / nth;
+        const int oh0 = th * TH, ow0 = tw * TW;
         const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + int64_t(n) * a.dz_bs, a.dz_bs * 2);
         const __amdgpu_buffer_rsrc_t rxs = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
 #pragma unroll
         for (int it = 0; it < DI; ++it) {
-            const int p = dsrow + RPD * it;
-            const int oh = oh0 + (p >> 3), ow = ow0 + (p & 7);
-            const bool ok = co_ok && p < 64 && oh < a.OH && ow < a.OW;
+            const int oh = oh0 + d_py[it], ow = ow0 + d_px[it];
+            const bool ok = live && co_ok && dsrow + RPD * it < 64 && oh < a.OH && ow < a.OW;
             rdz[it] = buf_load16(rd, ok ? uint32_t(((oh * a.OW + ow) * int(a.dz_ld) + co0 + dsc * 8) * 2) : OOB);
         }
         const int ih0 = oh0 * S - 1, iw0 = ow0 * S - 1;
 #pragma unroll
         for (int it = 0; it < XI; ++it) {
             const int ih = ih0 + x_hy[it], iw = iw0 + x_hx[it];
-            const bool ok = ci_ok && xsrow + RPX * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
+            const bool ok = live && ci_ok && xsrow + RPX * it < HR && unsigned(ih) < unsigned(a.IH) && unsigned(iw) < unsigned(a.IW);
             rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + xsc * 8) * 2) : OOB);
         }
     };
-    auto store = [&]() {
+    auto store = [&](const uint4 (&rdz)[DI], const uint4 (&rx)[XI]) {
 #pragma unroll
         for (int it = 0; it < DI; ++it)
             if (dsrow + RPD * it < 64) *reinterpret_cast<uint4*>(Dz + (dsrow + RPD * it) * RSD + dsc * 16) = rdz[it];
@@ -161,33 +177,27 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
             if (xsrow + RPX * it < HR)
                 *reinterpret_cast<uint4*>(Xh + (xsrow + RPX * it) * RSX + xsc * 16) = h8_to_bf8(rx[it]);
     };
-
-    if (t_begin < t_end) {
-        load(t_begin);
-        store();
-        __syncthreads();
-    }
-    for (int64_t t = t_begin; t < t_end; ++t) {
-        const bool more = t + 1 < t_end;
-        if (more) load(t + 1);
+    auto compute = [&]() {
+        int hl[2] = {hb_lo[0], hb_lo[1]}, hh[2] = {hb_hi[0], hb_hi[1]};
+        asm volatile("" : "+v"(hl[0]), "+v"(hl[1]), "+v"(hh[0]), "+v"(hh[1]));
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             bf16x8 af[TI];
 #pragma unroll
             for (int i = 0; i < TI; ++i) {
-                const int col = (wr * (TCO / 2) + i * 16 + 4 * pp) * 2;
+                const int col = (wr * WCO + i * 16 + 4 * pp) * 2;
                 af[i] = tr_frag(Dz + (kk * 32 + 4 * g + q) * RSD + col, Dz + (kk * 32 + 16 + 4 * g + q) * RSD + col);
             }
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
                 for (int kw = 0; kw < 3; ++kw) {
-                    const int toff = kh * HD + kw;
+                    const int toff = kh * HW + kw;
                     bf16x8 bfr[TJ];
 #pragma unroll
                     for (int j = 0; j < TJ; ++j) {
                         const int col = (wc * WCI + j * 16 + 4 * pp) * 2;
-                        bfr[j] = tr_frag(Xh + (hb_lo[kk] + toff) * RSX + col, Xh + (hb_hi[kk] + toff) * RSX + col);
+                        bfr[j] = tr_frag(Xh + (hl[kk] + toff) * RSX + col, Xh + (hh[kk] + toff) * RSX + col);
                     }
 #pragma unroll
                     for (int i = 0; i < TI; ++i)
@@ -197,10 +207,46 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
                                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[kh * 3 + kw][i][j], 0, 0, 0);
                 }
         }
-        __syncthreads();
-        if (more) {
-            store();
+    };
+
+    if constexpr (DEEP) {
+        // units go in pairs, one per register set (static indexing; a split with an odd count multiplies
+        // one unit of zeros at its end): the loop has one exit, so the accumulators are not copied
+        // between the two bodies' register assignments
+        if (t_begin < t_end) {
+            load(t_begin, da, xa);
+            load(t_begin + 1, db, xb);
+            store(da, xa);
             __syncthreads();
+            load(t_begin + 2, da, xa);
+        }
+        for (int64_t t = t_begin; t < t_end; t += 2) {
+            compute();                        // unit t (set a's, staged)
+            __syncthreads();
+            store(db, xb);
+            __syncthreads();
+            load(t + 3, db, xb);
+            compute();                        // unit t + 1
+            __syncthreads();
+            store(da, xa);
+            __syncthreads();
+            load(t + 4, da, xa);
+        }
+    } else {
+        // one register set: unit t + 1 in flight while unit t is multiplied
+        if (t_begin < t_end) {
+            load(t_begin, da, xa);
+            store(da, xa);
+            __syncthreads();
+            load(t_begin + 1, da, xa);
+        }
+        for (int64_t t = t_begin; t < t_end; ++t) {
+            compute();
+            __syncthreads();
+            if (t + 1 >= t_end) break;
+            store(da, xa);
+            __syncthreads();
+            load(t + 2, da, xa);
         }
     }
 
@@ -216,7 +262,7 @@ __global__ void __launch_bounds__(NWV * 64) wgrad3_kernel(WgArgs a) {
                 if (ci >= a.Cin) continue;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int co = co0 + wr * (TCO / 2) + i * 16 + (lane >> 4) * 4 + r;
+                    const int co = co0 + wr * WCO + i * 16 + (lane >> 4) * 4 + r;
                     if (co < a.Cout) base[(int64_t(co) * 9 + t) * a.Cin + ci] = acc[t][i][j][r];
                 }
             }
@@ -465,6 +511,8 @@ struct WgPlan {
     int T2;
     int co_t, ci_t;
     int64_t units, chunk, splits;
+    int tw, th;        // wgrad3 unit rectangle
+    bool deep;         // wgrad3: two register sets (units t + 1, t + 2 in flight)
 };
 
 WgPlan wg_plan(const ym_conv_desc* d) {
@@ -475,7 +523,14 @@ WgPlan wg_plan(const ym_conv_desc* d) {
         p.kind = 3;
         p.T = d->cout <= 32 ? 32 : 64;
         p.T2 = d->cin <= 32 ? 32 : 64;
+        p.tw = p.th = 8;
         p.units = int64_t(d->n) * ((d->oh + 7) / 8) * ((d->ow + 7) / 8);
+        // whole-row units on the narrow maps 8x8 tiles pad (a 20-wide map: 20 x 3 rows, 448 units per
+        // 64 images instead of 576 covering 24x24; 10 wide: 10 x 6) — 64x64 channel tiles only
+        if ((d->ow == 20 || d->ow == 10) && p.T == 64 && p.T2 == 64) {
+            p.tw = d->ow; p.th = 64 / d->ow;
+            p.units = int64_t(d->n) * ((d->oh + p.th - 1) / p.th);
+        }
     } else if (d->k == 1 && d->stride == 1 && d->pad == 0 && whole) {
         p.kind = 1;
         // 128-wide tiles once both channel counts reach 96: fewer tiles re-read dz and x fewer times, at
@@ -493,11 +548,19 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     const int64_t cols = int64_t(p.co_t) * p.ci_t * (p.kind == 0 ? d->k * d->k : 1);
     // enough K units per workgroup to amortise writing its fp32 partial tile (64x64x9 floats for
     // 3x3: 147 KB, about the input an 8x8-pixel unit moves 12 times)
-    const int64_t min_units = p.kind == 3 ? 12 : 8;
+    int64_t min_units = p.kind == 3 ? 12 : 8;
     // workgroups per launch: 256 measured best in the training step (2800 img/s vs 2767 at 512 and
     // 2725 at 1024): the weight gradients run on the side stream beside the data gradients, and
     // fewer, longer split-K blocks leave the main stream room and halve the partials to reduce
-    constexpr int64_t target = 256;
+    int64_t target = 256;
+    // stride-1 3x3 layers with few units per channel tile (20x20 maps, 256-channel 40x40): 512 workgroups of
+    // >= 6 units — the larger partials cost less than half the CUs idling (s@640 bs64, same-process A/B:
+    // 128->128 20x20 34.7 -> 30.2 us, 256->128 40x40 84.8 -> 76.1 us; the stride-2 20x20 layers and
+    // 128-channel 40x40 ones measured slower, so they keep 256)
+    if (p.kind == 3 && d->stride == 1 && p.units / cols < 256) { target = 512; min_units = 6; }
+    // the second register set pays where a split runs many units (maps >= 64 wide: 80x80 128->128
+    // 152.8 -> 147.6 us); below that the extra VGPRs (120 -> 166: one workgroup per CU) cost as much
+    p.deep = p.kind == 3 && d->ow >= 64;
     int64_t splits = std::max<int64_t>(1, std::min<int64_t>(target / cols, p.units / min_units));
     splits = std::min<int64_t>(splits, p.kind == 0 ? 65535 : 256);
     if (p.kind != 0 && splits >= 8) splits &= ~int64_t(7);      // whole XCD groups (wg_tile)
@@ -552,17 +615,23 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
         YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
-#define WG3_LAUNCH(S_)                                                                                        \
-        switch (tc) {                                                                                     \
-            case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 64, 64>), grid, dim3(512), 0, st, a); break;  \
-            case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 8, 32, 64>), grid, dim3(512), 0, st, a); break;  \
-            case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 64, 32>), grid, dim3(256), 0, st, a); break;  \
-            default: hipLaunchKernelGGL((wgrad3_kernel<S_, 4, 32, 32>), grid, dim3(256), 0, st, a); break; \
+#define WG3_LAUNCH(S_, D_)                                                                                        \
+        if (p.tw == 20) {                                                                                   \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 20, 3, false>), grid, dim3(512), 0, st, a); \
+        } else if (p.tw == 10) {                                                                            \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 10, 6, false>), grid, dim3(512), 0, st, a); \
+        } else {                                                                                            \
+            switch (tc) {                                                                                   \
+                case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 8, 8, D_>), grid, dim3(512), 0, st, a); break; \
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 64, 16, 16, 8, 8, D_>), grid, dim3(512), 0, st, a); break; \
+                case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 32, 32, 16, 8, 8, D_>), grid, dim3(256), 0, st, a); break; \
+                default: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 32, 16, 16, 8, 8, D_>), grid, dim3(256), 0, st, a); break; \
+            }                                                                                               \
         }
         if (d->stride == 1) {
-            WG3_LAUNCH(1)
+            if (p.deep) { WG3_LAUNCH(1, true) } else { WG3_LAUNCH(1, false) }
         } else {
-            WG3_LAUNCH(2)
+            if (p.deep) { WG3_LAUNCH(2, true) } else { WG3_LAUNCH(2, false) }
         }
 #undef WG3_LAUNCH
     } else if (p.kind == 1) {
@@ -597,3 +666,4 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     YM_LAUNCH_CHECK("ym_conv_wgrad(reduce)");
     return YM_OK;
 }
+

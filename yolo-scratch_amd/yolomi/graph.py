@@ -30,6 +30,9 @@ F16 = torch.float16
 F32 = torch.float32
 ACT_DTYPE, GRAD_DTYPE = F16, BF16      # activations fp16 (precision), gradients bf16 (range)
 BN_EPS, BN_MOM = 1e-3, 0.03
+# HIP graph capture of the 3-stream schedule segfaulted in round 2 (forward capture; 1 and 2 streams
+# captured and replayed correctly): graphs use at most this many scheduler streams (tools/graph_debug.py)
+GRAPH_MAX_STREAMS = 2
 
 
 # ----------------------------------------------------------------------------- buffers
@@ -780,9 +783,7 @@ class Plan:
         if self.dev.type != "cuda":
             return 1
         k = max(1, int(os.environ.get("YM_STREAMS", "3")))
-        # HIP graph capture of the 3-stream schedule segfaults in the ROCm 7.2 runtime (forward
-        # capture, reproducible; 1 and 2 streams capture and replay correctly): graphs use 2
-        return min(k, 2) if self._graph_ok() else k
+        return min(k, GRAPH_MAX_STREAMS) if self._graph_ok() else k
 
     def _schedule(self, ops, phase, K):
         key = (phase, K, len(ops))
