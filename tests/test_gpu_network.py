@@ -38,6 +38,13 @@ def _oracle_grads(scale, img, seed, rounding=False, jitter=0):
     return {k: v.grad for k, v in leaf.items()}
 
 
+# absolute cap on (1), independent of the rounding model.  Not the 0.1 a per-layer bound would give: the
+# largest whole-network errors measured in round 3 are 0.10 (n@320), 0.15 (m@256), 0.22 (s@640 bs2) and
+# 0.24 (s@128, model.0.bn.bias), each within 0.73 of its rounding-model bound — backbone BatchNorm
+# parameters behind SPPF's argmax routing.  Per-layer parity at 1e-2 is tests/test_gpu_layers.py.
+NET_CAP = 0.3
+
+
 def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_items, ref_grad_norm, ref_full, img,
                   batch_cpu, emu_samples=5):
     """Head maps, loss / items and EVERY parameter gradient of one training step against the
@@ -46,10 +53,10 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
     (1) element-wise against the fp32 oracle's network backward of d loss / d heads evaluated at
         the GPU's own head maps — the loss is a discrete function of the heads (assignment, and
         IoU^4-weighted target scores amplify head rounding), so this isolates the network backward:
-        relative L2 <= max(3e-2, 2 x the storage-rounding model's error on the same head gradients,
+        relative L2 <= min(NET_CAP, max(3e-2, 2 x the storage-rounding model's error on the same head gradients,
         worst of `emu_samples` samples of that model: oracle/precision.py, the network is chaotic in
         last-bit differences, e.g. a 1-ulp change in one layer's fp32 BN statistics moves the s@128
-        stem-weight gradient error from 0.10 to 0.16 with every kernel output still correct);
+        stem-weight gradient error from 0.10 to 0.16 with every kernel output still correct));
     (2) in norm against the reference's gradients: <= max(0.1, 2 x the rounding model's error,
         2 x the change the GPU's head values alone cause in the fp32 oracle's gradient)."""
     from oracle import loss as ol
@@ -80,7 +87,7 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
         r = at_gpu[k].double()
         sc = max(float(r.norm()), 1e-4 * gmax_at)
         err1 = float((g - r).norm()) / sc
-        tol1 = max(3e-2, 2.0 * max(float((e[k].double() - r).norm()) for e in at_gpu_emu) / sc)
+        tol1 = min(NET_CAP, max(3e-2, 2.0 * max(float((e[k].double() - r).norm()) for e in at_gpu_emu) / sc))
         worst1.append((err1 / tol1, k, err1, tol1))
         assert err1 <= tol1, ("vs oracle at GPU heads", k, err1, tol1)
         # (2) against the reference's gradient norm

@@ -107,7 +107,10 @@ __device__ __forceinline__ void vm_wait() {
 // sched_barriers keep the compiler from moving MFMAs / LDS reads across it
 __device__ __forceinline__ void step_barrier() {
     __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // the builtin, not inline asm: the compiler's wait-count pass sees this wait, so the MFMAs after the
+    // barrier do not wait again for the fragments read before it (with an asm wait they stalled on the
+    // next stage's freshly issued reads: lgkmcnt(3..0) ahead of the first four MFMAs of every step)
+    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
