@@ -34,5 +34,5 @@ timeout -k 10 300 python3 $R/tools/miopen_ref.py > $OUT/miopen_ref.txt 2> $OUT/m
 cat $OUT/miopen_ref.txt
 bash $R/tools/pmc_conv.sh $OUT/pmc73 73 && python3 $R/tools/pmc_summary.py $OUT/pmc73 > $OUT/pmc73_summary.txt; cat $OUT/pmc73_summary.txt
 # last: the 3-stream HIP-graph capture (segfaulted in round 2) under faulthandler
-YM_GRAPH=1 YM_STREAMS=3 GRAPH_MAX_STREAMS=3 timeout -k 10 180 python3 -X faulthandler $R/tools/graph_debug.py full > $OUT/graph3.log 2>&1
+YM_GRAPH=1 YM_STREAMS=3 timeout -k 10 180 python3 -X faulthandler $R/tools/graph_debug.py full > $OUT/graph3.log 2>&1
 echo "graph3 exit $?"; tail -40 $OUT/graph3.log

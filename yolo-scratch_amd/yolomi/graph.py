@@ -30,9 +30,6 @@ F16 = torch.float16
 F32 = torch.float32
 ACT_DTYPE, GRAD_DTYPE = F16, BF16      # activations fp16 (precision), gradients bf16 (range)
 BN_EPS, BN_MOM = 1e-3, 0.03
-# HIP graph capture of the 3-stream schedule segfaulted in round 2 (forward capture; 1 and 2 streams
-# captured and replayed correctly): graphs use at most this many scheduler streams (tools/graph_debug.py)
-GRAPH_MAX_STREAMS = 2
 
 
 # ----------------------------------------------------------------------------- buffers
@@ -706,8 +703,20 @@ class Plan:
         s = self.side_stream
         if s is None:
             return st
-        s.wait_stream(self._cur_stream or torch.cuda.current_stream(self.dev))
+        self._link(s, self._cur_stream or torch.cuda.current_stream(self.dev))
         return s.cuda_stream
+
+    def _link(self, dst, src):
+        """dst waits for everything issued so far on src, through ONE persistent event per source stream
+        (re-recorded each time).  torch's wait_stream records a temporary event that is destroyed right
+        after the wait; inside a HIP graph capture the runtime still refers to it at hipStreamEndCapture,
+        which then crashed once the capture held several such joins (the 3-stream forward capture)."""
+        evs = self.__dict__.setdefault("_link_events", {})
+        ev = evs.get(src.cuda_stream)
+        if ev is None:
+            ev = evs[src.cuda_stream] = torch.cuda.Event()
+        ev.record(src)
+        dst.wait_event(ev)
 
     def _begin_side(self):
         use = self.dev.type == "cuda" and os.environ.get("YM_SIDE_STREAM", "1") != "0"
@@ -718,7 +727,7 @@ class Plan:
 
     def _join_side(self):
         if self.side_stream is not None:
-            torch.cuda.current_stream(self.dev).wait_stream(self.side_stream)
+            self._link(torch.cuda.current_stream(self.dev), self.side_stream)
 
     def act(self, C, H, W, name=""):
         return View(Act(self, C, H, W, name=name))
@@ -783,7 +792,7 @@ class Plan:
         if self.dev.type != "cuda":
             return 1
         k = max(1, int(os.environ.get("YM_STREAMS", "3")))
-        return min(k, GRAPH_MAX_STREAMS) if self._graph_ok() else k
+        return k
 
     def _schedule(self, ops, phase, K):
         key = (phase, K, len(ops))
@@ -857,16 +866,26 @@ class Plan:
         evs = self.__dict__.setdefault("_events", {}).setdefault(phase, {})
         main = streams[0]
         for s in streams[1:]:
-            s.wait_stream(main)
+            self._link(s, main)
         ptrs = [s.cuda_stream for s in streams]
         fwd = phase == "fwd"
+        # HIP graph capture (ROCm 7.2 runtime) segfaults in hipStreamEndCapture once two non-origin streams
+        # have waited on each other's events (tools/hip_graph_repro.py `cycle`: s2 waits on s1, later s1 on
+        # s2 — four torch calls, no yolomi code).  While capturing, such a wait is relayed through the origin
+        # stream (main waits on the producer's event, the consumer on main's), which captures and replays
+        # correctly (`sched46_relay`); eager runs keep the direct wait.
+        relay = torch.cuda.is_current_stream_capturing()
         # ops launch on explicit stream handles (no torch stream context per op: it is host time the
         # GPU waits for); the few torch-side launches (side-stream joins, probe events) use _cur_stream
         for i, op in enumerate(ops):
             k, waits = sched[i]
             s = streams[k]
             for j in waits:
-                s.wait_event(evs[j])
+                if relay and k != 0 and sched[j][0] != 0:
+                    main.wait_event(evs[j])
+                    self._link(s, main)
+                else:
+                    s.wait_event(evs[j])
             self._cur, self._cur_stream = k, s
             if fwd:
                 op.forward(self, ptrs[k])
@@ -880,7 +899,7 @@ class Plan:
                     ev = evs[i] = torch.cuda.Event()
                 ev.record(s)
         for s in streams[1:]:
-            main.wait_stream(s)
+            self._link(main, s)
         self._cur, self._cur_stream = 0, None
 
     # --------------------------------------------------------------- HIP graphs
@@ -891,10 +910,8 @@ class Plan:
     # launches point at fixed buffers: the input image and the head gradient are copied into the
     # plan's own static tensors when the caller's differ.  Not used while the bench probe times a
     # kernel with events, or for block plans.  Data parallelism in graph mode all-reduces the flat
-    # gradient once after the backward (yolomi/dist.py).  Opt-in (YM_GRAPH=1): measured on the
-    # s@640 bs64 step, replay is 1.5-2 ms SLOWER than eager launches (26.3-26.7 vs 24.7 ms/step at
-    # 1 and 2 streams): the eager host enqueue already runs ahead of the GPU, and the replayed
-    # graph runs its kernels with less overlap than the streams do.
+    # gradient once after the backward (yolomi/dist.py).  Opt-in (YM_GRAPH=1): the step is GPU-bound
+    # (host enqueue ~8 ms of a ~20 ms step), so replay has no host time to win back.
     def _graph_ok(self):
         if not (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
                 and self.family_events is None):
