@@ -308,7 +308,7 @@ def main():
     step_tf = value / world * per_img / 1e12
     import ctypes
     from yolomi._lib import lib as _yl
-    probe_kernel = {2: "conv_pipe_kernel", 1: "conv_halo_kernel"}.get(
+    probe_kernel = {4: "conv_hpipe_kernel", 3: "conv_direct_kernel", 2: "conv_pipe_kernel", 1: "conv_halo_kernel"}.get(
         _yl().ym_conv_algo(ctypes.byref(dom.desc), 0), "conv_gemm_kernel")
     def fam_rate(kind):
         ms, work, _ = fams[kind]
@@ -331,7 +331,8 @@ def main():
                "traffic": t3["bytes_per_launch"] if t3 else None,
                "traffic_unit": "HBM bytes per training step, summed over the family's launches",
                "traffic_source": t3["source"] if t3 else None,
-               "kernel": f"dense 3x3 conv kernels (conv_pipe / conv_halo / conv_gemm / conv_direct fwd + dgrad, "
+               "kernel": f"dense 3x3 conv kernels (conv_pipe / conv_hpipe / conv_halo / conv_gemm / conv_direct "
+                         f"fwd + dgrad, "
                          f"wgrad3 + split-K reduce): {c3_n} launches per step, {c3_flop / 1e9:.0f} GFLOP algorithmic "
                          f"in {c3_ms:.3f} ms summed launch time (HIP events on the launch stream, all launches on "
                          f"one stream, {PROBE_STEPS} steps)",

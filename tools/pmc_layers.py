@@ -30,17 +30,14 @@ def dispatches(path, counter):
     return [rows[k] for k in sorted(rows)]
 
 
-def groups(disp):
-    is_sep = ["elementwise" in n for n, _ in disp]
-    start = next(i for i in range(len(disp) - 2) if is_sep[i] and is_sep[i + 1] and is_sep[i + 2]) + 3
-    out, cur = [], 0.0
-    for (n, v), sp in zip(disp[start:], is_sep[start:]):
-        if sp:
-            out.append(cur)
-            cur = 0.0
-        else:
-            cur += v
-    return out
+def groups(disp, ngroups):
+    """Counter sums of the last `ngroups` groups: each group ENDS with one separator, so the groups are the
+    runs between the last ngroups + 1 separators (the warm-up training step before them launches torch
+    elementwise kernels of its own, three in a row among them, so the start is anchored at the end)."""
+    sep = [i for i, (n, _) in enumerate(disp) if "elementwise" in n]
+    bounds = sep[-(ngroups + 1):]
+    assert len(bounds) == ngroups + 1, (len(sep), ngroups)
+    return [sum(v for _, v in disp[a + 1:b]) for a, b in zip(bounds[:-1], bounds[1:])]
 
 
 def main():
@@ -49,9 +46,9 @@ def main():
     commit = sys.argv[5] if len(sys.argv) > 5 else None
     seq = json.loads(Path(seq_json).read_text())
     B = seq["batch"]
-    fetch = groups(dispatches(fetch_csv, "FETCH_SIZE"))
-    write = groups(dispatches(write_csv, "WRITE_SIZE"))
     G = seq["groups"]
+    fetch = groups(dispatches(fetch_csv, "FETCH_SIZE"), len(G))
+    write = groups(dispatches(write_csv, "WRITE_SIZE"), len(G))
     assert len(fetch) >= len(G) and len(write) >= len(G), (len(fetch), len(write), len(G))
     fam = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     alg3 = 0.0

@@ -12,7 +12,7 @@ struct DirectPlan {
     int classes;     // output-parity classes (4: stride-2 data gradient, else 1)
 };
 
-// -1: YM_CONV_DIRECT / default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size
+// -1: default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size
 extern int g_direct_force;
 
 DirectPlan direct_plan(const ym_conv_desc* d, int dgrad);

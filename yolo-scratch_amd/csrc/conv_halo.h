@@ -14,7 +14,7 @@ struct HaloPlan {
     int gx;              // grid x (= rows of the BN statistics partials)
 };
 
-// -1: YM_CONV_HALO / default policy (3); 0 never; 1 wherever it applies; 2 maps <= 24 wide; 3 maps <= 48
+// -1: default policy (3); 0 never; 1 wherever it applies; 2 maps <= 24 wide; 3 maps <= 48
 // wide or <= 64 output channels (ym_conv_set_halo)
 extern int g_halo_force;
 

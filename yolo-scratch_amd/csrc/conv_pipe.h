@@ -14,7 +14,7 @@ struct PipePlan {
     int rows;        // rows of the BN statistics partials (= grid / channel tiles)
 };
 
-// -1: YM_CONV_PIPE / default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
+// -1: default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
 // tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
 extern int g_pipe_force;
 
