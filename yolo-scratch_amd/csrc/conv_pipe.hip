@@ -193,22 +193,32 @@ struct Issuer {
         a_tap = uint32_t(((kh0 + ti * ost) * a.KW + (kw0 + tj * ost)) * a.Kin) * 2u;
     }
 
-    // one stage into `st`, then advance the stream position
-    __device__ __forceinline__ void issue(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off) {
-        if (kci == 0) tap_setup();
-        const uint32_t kb = uint32_t(kci) * 128u;
-        {
-            // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
-            const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
-            const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
-            const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
-            const __amdgpu_buffer_rsrc_t xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
-                                                          __builtin_amdgcn_readfirstlane(x_bytes));
-#pragma unroll
-            for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, a_off[j], a_tap + kb);
-#pragma unroll
-            for (int j = 0; j < BI; ++j) dma16(xres, st + BN * RB + (wave * BI + j) * 1024, b_off[j], kb);
+    __device__ __forceinline__ void start() {
+        if (ntile > 0) {
+            tile_setup();
+            tap_setup();
         }
+    }
+
+    // the DMAs of the stage at the stream position into `st` (straight-line code: the caller interleaves
+    // them with MFMAs); `live` false = past the stream's end: out-of-range offsets, nothing is fetched and
+    // every step keeps the same DMA count (the counted vmcnt waits stay constant)
+    __device__ __forceinline__ void issue_dma(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off, bool live) {
+        const uint32_t kb = uint32_t(kci) * 128u;
+        // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
+        const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
+        const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
+        const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
+        const __amdgpu_buffer_rsrc_t xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
+                                                      __builtin_amdgcn_readfirstlane(x_bytes));
+#pragma unroll
+        for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, live ? a_off[j] : OOB, a_tap + kb);
+#pragma unroll
+        for (int j = 0; j < BI; ++j) dma16(xres, st + BN * RB + (wave * BI + j) * 1024, live ? b_off[j] : OOB, kb);
+    }
+
+    // advance the stream position by one stage (new tap: its gather offsets; new tile: its pixels)
+    __device__ __forceinline__ void advance() {
         if (++kci == kc) {
             kci = 0;
             if (++tj == nkw) {
@@ -218,6 +228,7 @@ struct Issuer {
                     if (++i < ntile) tile_setup();
                 }
             }
+            tap_setup();
         }
     }
 };
@@ -310,15 +321,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
 
     Issuer<BM, BN, NW, MODE> is(a, wave, lane, mt_lo, qstride, ntile);
-    if (ntile > 0) is.tile_setup();
+    is.start();
 
-    // prologue: stages 0..2 in flight; stage 0 landed everywhere; its first-half fragments read
+    // prologue: stages 0..2 in flight (stages past the stream's end fetch nothing); stage 0 landed
+    // everywhere; its first-half fragments read
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-        if (s < total) is.issue(smem + s * STAGE, wres, a_off);
-    if (total >= 3) vm_wait<2 * DPS>();
-    else if (total == 2) vm_wait<DPS>();
-    else vm_wait<0>();
+    for (int s = 0; s < NS; ++s) {
+        is.issue_dma(smem + s * STAGE, wres, a_off, s < total);
+        is.advance();
+    }
+    vm_wait<2 * DPS>();
     step_barrier();
     if (total > 0) read_frags(f0a, f0b, 0, 0);
 
@@ -340,17 +352,25 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         }
         read_frags(f1a, f1b, buf, 1);
         mma(f0a, f0b);
-        // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight
-        if (g + 1 < total) {
-            if (g + 2 < total) vm_wait<DPS>();
-            else vm_wait<0>();
-        }
+        // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight (every step issues DPS DMAs,
+        // live or not, so the count is constant)
+        vm_wait<DPS>();
         step_barrier();
-        // the slot of stage g is free again (every wave's reads of it returned before the barrier)
-        if (g + 3 < total) is.issue(smem + buf * STAGE, wres, a_off);
+        // the slot of stage g is free again (every wave's reads of it returned before the barrier): stage
+        // g+3's DMAs go out one at a time between the second half's MFMAs (issued in a burst they held both
+        // waves of a SIMD off the MFMA pipe for the whole burst), then the next stage's first-half reads
         const int nbuf = buf == NS - 1 ? 0 : buf + 1;
-        if (g + 1 < total) read_frags(f0a, f0b, nbuf, 0);
+        is.issue_dma(smem + buf * STAGE, wres, a_off, g + 3 < total);
+        read_frags(f0a, f0b, nbuf, 0);
         mma(f1a, f1b);
+#pragma unroll
+        for (int d = 0; d < DPS; ++d) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                     // one DMA
+            __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (DPS + 1), 0);  // MFMAs
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);                   // next-stage reads
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - DPS * ((TM * TN) / (DPS + 1)), 0);
+        is.advance();
         buf = nbuf;
         if (++ck < cnk) continue;
         ck = 0;
