@@ -155,13 +155,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     const __amdgpu_buffer_rsrc_t xres = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
 
     // ---- issue side: weight stage s -> (chunk, tap); halo of global chunk h -> (tile, chunk)
-    auto issue_w = [&](int s) {
+    // weight stage s into its ring slot; past the stream's end (live false) the DMAs fetch nothing but still
+    // count, so every step issues AI of them and the counted waits stay constant
+    auto issue_w = [&](int s, bool live) {
         const int within = s % spt;
         const int cc = within / 9, tap = within - cc * 9;
         const uint32_t soff = uint32_t(tap * a.Kin + cc * 64) * 2u;
         char* st = wring + (s % NS) * WSLOT;
 #pragma unroll
-        for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, a_off[j], soff);
+        for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, live ? a_off[j] : OOB, soff);
     };
     uint32_t hoff[HI_MAX];                    // per-lane halo offsets of the tile being staged
     int h_tile = -1;
@@ -237,8 +239,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     if (total > 0) issue_h(0);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-        if (s < total) issue_w(s);
-    vm_wait_n(AI * (min(total, NS) - 1));
+        issue_w(s, s < total);
+    vm_wait_n(AI * (NS - 1));
     step_barrier();
     if (total > 0) read_frags(f0a, f0b, 0, 0);
 
@@ -255,7 +257,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         // stage g+1 must have landed (own DMAs); stages g+2 and g+3 may stay in flight, and so may halos
         // issued in steps g-2 and g-1 (after stage g+1, when those steps began a chunk with a successor)
         if (g + 1 < total) {
-            int pend = (g + 2 < total ? AI : 0) + (g + 3 < total ? AI : 0);
+            int pend = 2 * AI;
 #pragma unroll
             for (int b = 1; b <= 2; ++b) {
                 const int gs = g - b;
@@ -267,9 +269,18 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         // the halo buffer of chunk h-1 and the weight slot of step g are free (their reads returned before
         // the barrier): the next chunk's halo at its predecessor's first step, then weight stage g+4
         if (g % 9 == 0 && g / 9 + 1 < nchunks) issue_h(g / 9 + 1);
-        if (g + NS < total) issue_w(g + NS);
-        if (g + 1 < total) read_frags(f0a, f0b, g + 1, 0);
+        // the weight DMAs one at a time between the second half's MFMAs (a burst held both waves of a SIMD
+        // off the MFMA pipe), then the next step's first-half reads (harmless past the end)
+        issue_w(g + NS, g + NS < total);
+        read_frags(f0a, f0b, g + 1, 0);
         mma(f1a, f1b);
+#pragma unroll
+        for (int d = 0; d < AI; ++d) {
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // one weight DMA
+            __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (AI + 1), 0);  // MFMAs
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);                  // next-step reads
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - AI * ((TM * TN) / (AI + 1)), 0);
         if (++ck < spt) continue;
         ck = 0;
 
