@@ -8,7 +8,8 @@
 // 128 x 128 tiles, one K stage in flight and one barrier + read burst per K step leave the MFMA
 // pipes 77 % idle (profiles/r01/pmc_op6): every K step opens with the LDS latency of its fragment
 // reads, and 64 B/cycle of staging per CU at peak is more than the TA delivers.  Here:
-//  * 256 pixels x 128 channels per tile, 8 waves of 64 x 64, K steps of 64 (two 32-deep halves):
+//  * 256 pixels x 128 channels per tile, 16 waves of 32 x 64 (64-channel tiles: 8 waves of 64 x 32),
+//    K steps of 64 (two 32-deep halves):
 //    a third fewer staged bytes per FLOP than 128 x 128;
 //  * a 3-stage LDS ring filled by LDS-DMA (buffer_load ... lds) with TWO stages in flight, counted
 //    vmcnt waits and raw s_barrier (no vmcnt(0) drain in the loop);
@@ -489,12 +490,16 @@ struct Cfg {
 };
 constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
 
+// 256 x 128 tiles run on 16 waves of 32 x 64 (four per SIMD, 127 VGPRs): same staging and LDS as 8 waves
+// of 64 x 64, 1.5x the fragment reads, but while some waves of a SIMD issue their DMA pieces or wait at
+// the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
+// layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     if (mode == PF) {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
+        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PF><<<dim3(grid), dim3(1024), 0, st>>>(a);
         else conv_pipe_kernel<256, 64, 1, 8, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
     } else {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 2, 4, PD><<<dim3(grid), dim3(512), 0, st>>>(a);
+        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PD><<<dim3(grid), dim3(1024), 0, st>>>(a);
         else conv_pipe_kernel<256, 64, 1, 8, PD><<<dim3(grid), dim3(512), 0, st>>>(a);
     }
 }
@@ -579,3 +584,4 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
 }
 
 }  // namespace ym
+
