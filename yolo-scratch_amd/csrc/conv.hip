@@ -772,7 +772,7 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
 }
 
 extern "C" int ym_conv_set_halo(int mode) {
-    // selection policy of the halo-staged 3x3 kernel: -1 env/default, 0 never, 1 wherever it applies,
+    // selection policy of the halo-staged 3x3 kernel: -1 default, 0 never, 1 wherever it applies,
     // 2 where it measured faster in the step (the default), 3 the wider per-layer rule; returns the
     // previous setting
     const int prev = g_halo_force;
@@ -781,7 +781,7 @@ extern "C" int ym_conv_set_halo(int mode) {
 }
 
 extern "C" int ym_conv_set_pipe(int mode) {
-    // selection policy of the pipelined implicit GEMM: -1 env/default, 0 never, 1 layers of >= 1024
+    // selection policy of the pipelined implicit GEMM: -1 default, 0 never, 1 layers of >= 1024
     // tiles (default), 2 >= 256 tiles; returns the previous setting
     const int prev = g_pipe_force;
     g_pipe_force = mode < -1 || mode > 3 ? -1 : mode;
@@ -789,7 +789,7 @@ extern "C" int ym_conv_set_pipe(int mode) {
 }
 
 extern "C" int ym_conv_set_direct(int mode) {
-    // selection policy of the direct register-weight kernel: -1 env/default, 0 never, 1 maps of
+    // selection policy of the direct register-weight kernel: -1 default, 0 never, 1 maps of
     // >= 1 M output pixels (default), 2 any size; returns the previous setting
     const int prev = g_direct_force;
     g_direct_force = mode < -1 || mode > 2 ? -1 : mode;
