@@ -301,18 +301,22 @@ __global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
 #pragma unroll
         for (int j = 0; j < TS; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    uint4 ra[ITEMS], rb[ITEMS];
-    auto load = [&](int64_t p0) {
-        // records end at p_end: rows past it read as zero
-        const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + p0 * a.dz_ld, (p_end - p0) * a.dz_ld * 2);
-        const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + p0 * a.x_ld, (p_end - p0) * a.x_ld * 2);
+    // two register sets (units t + 1 and t + 2 in flight while unit t is multiplied; one unit of
+    // look-ahead left the kernel waiting on its loads two thirds of its cycles — SQ_WAIT_ANY 66 %,
+    // profiles/r03/pmc73_summary.txt); units go in pairs, a split with an odd count multiplies zeros
+    uint4 ra0[ITEMS], rb0[ITEMS], ra1[ITEMS], rb1[ITEMS];
+    auto load = [&](int64_t p0, uint4 (&ra)[ITEMS], uint4 (&rb)[ITEMS]) {
+        // records end at p_end: rows past it (and whole units past it) read as zero
+        const int64_t left = std::max<int64_t>(0, p_end - p0);
+        const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + p0 * a.dz_ld, left * a.dz_ld * 2);
+        const __amdgpu_buffer_rsrc_t rx = make_rsrc(a.x + p0 * a.x_ld, left * a.x_ld * 2);
 #pragma unroll
         for (int it = 0; it < ITEMS; ++it) {
             ra[it] = buf_load16(rd, dz_off[it]);
             rb[it] = buf_load16(rx, x_off[it]);
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const uint4 (&ra)[ITEMS], const uint4 (&rb)[ITEMS]) {
 #pragma unroll
         for (int it = 0; it < ITEMS; ++it) {
             const int r = srow + RPP * it;
@@ -321,16 +325,7 @@ __global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
         }
     };
     const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-
-    int buf = 0;
-    if (p_begin < p_end) {
-        load(p_begin);
-        store(0);
-        __syncthreads();
-    }
-    for (int64_t p0 = p_begin; p0 < p_end; p0 += KP) {
-        const bool more = p0 + KP < p_end;
-        if (more) load(p0 + KP);
+    auto compute = [&](int buf) {
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             const char* A0 = As[buf] + (kk * 32 + 4 * g + q) * RS;
@@ -352,9 +347,24 @@ __global__ void __launch_bounds__(256, 2) wgrad1_kernel(WgArgs a) {
                 for (int j = 0; j < TS; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        if (more) store(buf ^ 1);
+    };
+
+    if (p_begin < p_end) {
+        load(p_begin, ra0, rb0);
+        load(p_begin + KP, ra1, rb1);
+        store(0, ra0, rb0);
         __syncthreads();
-        buf ^= 1;
+        load(p_begin + 2 * KP, ra0, rb0);
+    }
+    for (int64_t p0 = p_begin; p0 < p_end; p0 += 2 * KP) {
+        compute(0);                           // unit at p0
+        store(1, ra1, rb1);
+        __syncthreads();
+        load(p0 + 3 * KP, ra1, rb1);
+        compute(1);                           // unit at p0 + KP (zeros past the split)
+        store(0, ra0, rb0);
+        __syncthreads();
+        load(p0 + 4 * KP, ra0, rb0);
     }
     float* base = a.part + int64_t(split) * a.Cout * a.Cin;
 #pragma unroll
