@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--variants", type=int, nargs="+", default=[0, 1])
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--also", nargs="*", default=[], help="other setters applied first, NAME=VALUE")
     args = ap.parse_args()
     import torch
     import yaml
@@ -39,6 +40,9 @@ def main():
     plan = model.__dict__["_ym_last_plan"]
     st = stream_ptr(dev)
     setter = getattr(lib(), args.setter)
+    for kv in args.also:
+        name, val = kv.split("=")
+        getattr(lib(), name)(int(val))
     res = {}
     for _ in range(args.rounds):
         for i in args.only:

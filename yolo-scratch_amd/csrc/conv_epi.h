@@ -19,7 +19,11 @@ namespace ym {
 // WCH = 16 * TM channels of this wave; ep: this wave's LDS area (16 * WCH * 2 bytes).
 // pix_off(q) -> byte offset of wave-local pixel q's channel wch0 in the output (OOB when the pixel
 // is outside the map / tile).  half: fp16 (1) or bf16 (0) output; accumulate: add into the bf16 output.
-template <int TM, int TN, class PixOff>
+// ASMW: the LDS writes as inline asm — the compiler's wait-count pass then does not treat them as possibly
+// aliasing in-flight LDS-DMA stages and drain every DMA (vmcnt(0)) in front of them (the pipelined kernels
+// keep stages in flight through the epilogue); this wave's LDS operations execute in order, so the reads
+// that follow see the data.
+template <int TM, int TN, bool ASMW = false, class PixOff>
 __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
                                                bool stats, char* ep, int lane, int wch0, int nout,
                                                __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
@@ -54,7 +58,13 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
             }
             const int byte = (i * 16 + fc * 4) * 2;                    // within the pixel row
             const int chunk = (byte >> 4) ^ (fr & (CPR - 1));          // swizzled 16-B chunk
-            *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
+            char* dst = ep + fr * (WCH * 2) + chunk * 16 + (byte & 15);
+            if constexpr (ASMW) {
+                const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>(dst));
+                asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o) : "memory");
+            } else {
+                *reinterpret_cast<uint2*>(dst) = o;
+            }
         }
 #pragma unroll
         for (int h = 0; h < 16 / RPS; ++h) {
