@@ -207,18 +207,6 @@ def test_pipe_kernel_vs_torch(shape):
     _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
 
 
-# the ping-pong form of the 256 x 128 tile (conv_pipe.hip conv_pp_kernel: two wave groups one barrier apart),
-# on the same shapes (the 64-channel-tile shape stays on the 16-wave kernel's 256 x 64 form)
-@pytest.mark.parametrize("shape", PIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in PIPE])
-def test_pipe_pingpong_kernel_vs_torch(shape):
-    from yolomi._lib import lib
-    prev = lib().ym_conv_set_pipe_pp(1)
-    try:
-        _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
-    finally:
-        lib().ym_conv_set_pipe_pp(prev)
-
-
 # halo-staged PIPELINED 3x3 stride-1 kernel (conv_hpipe.hip), forced on with ym_conv_set_hpipe(2): 16x16-pixel
 # tiles on maps whose sides are multiples of 16, 128-channel tiles (a partial second channel tile at 192),
 # 2-4 input chunks of 64 channels, channel-slice views in and out, fp16 z + BN statistic partials,
@@ -237,17 +225,6 @@ HPIPE = [
 def test_hpipe_kernel_vs_torch(shape):
     from yolomi._lib import lib
     _views_fwd_dgrad_check(shape, lib().ym_conv_set_hpipe, 2, 4)
-
-
-# the ping-pong form of the halo-pipelined 128-channel tile (conv_hpipe.hip conv_hpp_kernel)
-@pytest.mark.parametrize("shape", HPIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}x{s[8]}y{s[9]}" for s in HPIPE])
-def test_hpipe_pingpong_kernel_vs_torch(shape):
-    from yolomi._lib import lib
-    prev = lib().ym_conv_set_hpipe_pp(1)
-    try:
-        _views_fwd_dgrad_check(shape, lib().ym_conv_set_hpipe, 2, 4)
-    finally:
-        lib().ym_conv_set_hpipe_pp(prev)
 
 
 def test_hpipe_selection():

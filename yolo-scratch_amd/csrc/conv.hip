@@ -788,22 +788,6 @@ extern "C" int ym_conv_set_pipe(int mode) {
     return prev;
 }
 
-extern "C" int ym_conv_set_pipe_pp(int mode) {
-    // experimental (not in the header): 256 x 128 pipelined tiles on the ping-pong kernel (1) or the
-    // 16-wave kernel (0); returns the previous setting
-    const int prev = g_pipe_pp;
-    g_pipe_pp = mode < 0 || mode > 6 ? 0 : mode;
-    return prev;
-}
-
-extern "C" int ym_conv_set_hpipe_pp(int mode) {
-    // experimental (not in the header): 128-channel halo-pipelined tiles on the ping-pong kernel (1) or the
-    // 8-wave kernel (0); returns the previous setting
-    const int prev = g_hpipe_pp;
-    g_hpipe_pp = mode ? 1 : 0;
-    return prev;
-}
-
 extern "C" int ym_conv_set_direct(int mode) {
     // selection policy of the direct register-weight kernel: -1 default, 0 never, 1 maps of
     // >= 1 M output pixels (default), 2 any size; returns the previous setting

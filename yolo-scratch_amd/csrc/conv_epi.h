@@ -19,11 +19,7 @@ namespace ym {
 // WCH = 16 * TM channels of this wave; ep: this wave's LDS area (16 * WCH * 2 bytes).
 // pix_off(q) -> byte offset of wave-local pixel q's channel wch0 in the output (OOB when the pixel
 // is outside the map / tile).  half: fp16 (1) or bf16 (0) output; accumulate: add into the bf16 output.
-// ASMW: the LDS writes as inline asm — the compiler's wait-count pass then does not treat them as possibly
-// aliasing in-flight LDS-DMA stages and drain every DMA (vmcnt(0)) in front of them (the pipelined kernels
-// keep stages in flight through the epilogue); this wave's LDS operations execute in order, so the reads
-// that follow see the data.
-template <int TM, int TN, bool ASMW = false, class PixOff>
+template <int TM, int TN, class PixOff>
 __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
                                                bool stats, char* ep, int lane, int wch0, int nout,
                                                __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
@@ -58,13 +54,7 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
             }
             const int byte = (i * 16 + fc * 4) * 2;                    // within the pixel row
             const int chunk = (byte >> 4) ^ (fr & (CPR - 1));          // swizzled 16-B chunk
-            char* dst = ep + fr * (WCH * 2) + chunk * 16 + (byte & 15);
-            if constexpr (ASMW) {
-                const uint32_t la = uint32_t(reinterpret_cast<uintptr_t>(dst));
-                asm volatile("ds_write_b64 %0, %1" ::"v"(la), "v"(o) : "memory");
-            } else {
-                *reinterpret_cast<uint2*>(dst) = o;
-            }
+            *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
         }
 #pragma unroll
         for (int h = 0; h < 16 / RPS; ++h) {
@@ -75,6 +65,68 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
                 if (wch0 + c * 8 < nout) off += uint32_t(c) * 16u;
                 else off = OOB;
             }
+            if (accumulate) {                                          // gradient fan-in (bf16)
+                const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
+                uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
+                                  bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
+                v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                   yres, off, 0, 0);
+        }
+    }
+}
+
+// Register-only form (round 3; the pipelined kernel's data gradient): each pair of 16-pixel subtiles (ja, jb) is exchanged
+// between lane rows with v_permlane16_swap (rows 1 / 3 of ja's packed values <-> rows 0 / 2 of jb's), after which
+// lane (fc, fr) holds 8 consecutive channels (i*16 + (fc >> 1)*8 ..) of ONE pixel (subtile fc odd ? jb : ja, row
+// fr): one 16-B store per lane and channel subtile, 32 pixels x 32 B per instruction, TM * TN / 2 stores per lane.
+// No LDS: an LDS transpose makes hipcc drain every in-flight LDS-DMA stage (vmcnt(0)) in front of it.
+// pix_off(q) as above (byte offset of wave-local pixel q's channel wch0, OOB outside); nout % 8 == 0.
+template <int TM, int TN, class PixOff>
+__device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
+                                              bool stats, int lane, int wch0, int nout,
+                                              __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
+                                              PixOff pix_off) {
+    static_assert(TN % 2 == 0, "subtile pairs");
+    const int fc = lane >> 4, fr = lane & 15;
+    if (stats) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if (pix_off(j * 16 + fr) == OOB) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int cb = wch0 + i * 16 + fc * 4;
+                if (cb < nout) {                                       // nout % 8 == 0: all four or none
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float v = acc[i][j][r];
+                        ssum[i][r] += v;
+                        ssq[i][r] = fmaf(v, v, ssq[i][r]);
+                    }
+                }
+            }
+        }
+    }
+    auto pack = [&](float lo, float hi) -> uint32_t {
+        return half ? (uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16)) : pk2bf(lo, hi);
+    };
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp) {
+        const int ja = 2 * jp, jb = ja + 1;
+        const uint32_t base = pix_off((fc & 1 ? jb : ja) * 16 + fr);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const uint32_t x0 = pack(acc[i][ja][0], acc[i][ja][1]), x1 = pack(acc[i][ja][2], acc[i][ja][3]);
+            const uint32_t y0 = pack(acc[i][jb][0], acc[i][jb][1]), y1 = pack(acc[i][jb][2], acc[i][jb][3]);
+            const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+            const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+            uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            const int co = i * 16 + (fc >> 1) * 8;                     // channel offset within the wave
+            const uint32_t off = base != OOB && wch0 + co < nout ? base + uint32_t(co) * 2u : OOB;
             if (accumulate) {                                          // gradient fan-in (bf16)
                 const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
                 uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};

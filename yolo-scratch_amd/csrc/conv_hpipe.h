@@ -15,8 +15,6 @@ struct HPipePlan {
 // selection policy (ym_conv_set_hpipe): -1 default (1); 0 never; 1 eligible layers with >= 512 tiles;
 // 2 every eligible layer
 extern int g_hpipe_force;
-// 128-channel tiles on the ping-pong kernel (1) or the 8-wave one (0)
-extern int g_hpipe_pp;
 
 HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad);
 int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,

@@ -27,14 +27,12 @@
 #include <algorithm>
 
 #include "common.h"
-#include "conv_epi.h"
 #include "conv_hpipe.h"
 #include "tile.h"
 
 namespace ym {
 
 int g_hpipe_force = -1;
-int g_hpipe_pp = 0;
 
 namespace {
 
@@ -387,257 +385,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     }
 }
 
-// barrier first, then this wave's fragment reads retired: the reads' latency overlaps the wait for the
-// other group (used where no DMA is issued into the buffers just read before the next barrier)
-__device__ __forceinline__ void bar_then_wait() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_waitcnt(0xC07F);       // lgkmcnt(0)
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// Ping-pong schedule of the halo-staged tile (round 3).  The 16 x 16-pixel x 128-channel tile, the halo
-// staged once per 64-channel chunk and the per-tap 16 KB weight slices are conv_hpipe_kernel's; the K loop
-// is conv_pipe.hip's conv_pp_kernel: two groups of four waves (one of each per SIMD, wave w: channel half
-// w >> 2, tile rows 4 (w & 3) .. +3), the second group one barrier behind, so in every interval between two
-// barriers one group runs a 16-MFMA cluster (a 32-deep half of a K step) while the other reads the next
-// half's fragments and issues its DMA share.  The point: a K step here stages ~21 one-KiB DMA pieces
-// (16 weight + 41 / 9 halo) instead of the implicit GEMM's 48, which at the measured per-CU LDS-DMA rate
-// (~15-20 cycles a piece, tools/dma_bench.hip) fits under the MFMA clusters.
-// Per wave and K step g (tap t of chunk c):
-//   phase 0: A/B fragments (kk 0); weight piece 0 of stage g+2; halo piece (pos-1)*2 of chunk c+1 at chunk
-//            positions 1..3; barrier; lgkmcnt(0); 16 MFMAs; barrier
-//   phase 1: fragments (kk 1); weight piece 1 of stage g+2; halo piece (pos-1)*2+1; vmcnt(stage g+1 landed);
-//            lgkmcnt(0); barrier; 16 MFMAs; barrier
-// RAW: stage g+1 / the halo of chunk c+1 are retired by every wave's vmcnt in its phase-1 load part of step g
-// (resp. earlier), before the barrier that precedes their first read.  WAR: stage g+2 overwrites the slot of
-// stage g-1, last read in group 1's phase-1 load part of step g-1, which retires its reads before its barrier;
-// a halo buffer is re-filled from position 1 of the chunk after the next, and the epilogue (which borrows the
-// last chunk's halo buffer as its transpose area) runs in the load slot right after the tile's last MFMAs.
-template <int MODE>
-__global__ void __launch_bounds__(512, 1) conv_hpp_kernel(HArgs a) {
-    constexpr int BN = 128, WM = 2, WN = 4, NW = 8;
-    constexpr int D = 2, NS = D + 1;          // weight ring: stages g (reading), g+1 (landed), g+2 (issuing)
-    constexpr int AI = BN / 8 / NW;           // 2 weight pieces per wave per step: one per phase
-    constexpr int TM = BN / WM / 16, TN = TS / WN;
-    constexpr int WSLOT = BN * RB;
-    constexpr int WCH = BN / WM, EPW = 16 * WCH * 2;
-    constexpr int HI_MAX = (HPIECES + NW - 1) / NW;
-    static_assert(AI == 2 && TM == 4 && TN == 4, "geometry");
-    static_assert(HI_MAX <= 6, "halo pieces fit positions 1..3 x two phases");
-    static_assert(NW * EPW <= HBUF, "epilogue area inside a halo buffer");
-    static_assert(2 * HBUF + NS * WSLOT <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char smem[2 * HBUF + NS * WSLOT];
-    char* const hbuf0 = smem;
-    char* const wring = smem + 2 * HBUF;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2;
-    const int wr = grp, wc = wave & 3;
-    const int fc = lane >> 4, fr = lane & 15;
-    const int CC = a.Kin >> 6;
-    const int hi_w = (HPIECES - wave + NW - 1) / NW;
-
-    const int G8 = int(gridDim.x) >> 3;
-    const int xcd = int(blockIdx.x) & 7, q = int(blockIdx.x) >> 3;
-    const int nt = q % a.ntiles, qq = q / a.ntiles, qstride = G8 / a.ntiles;
-    const int per = (a.mt_total + 7) >> 3;
-    const int mt_lo = xcd * per + qq, mt_hi = min(xcd * per + per, a.mt_total);
-    const int ntile = mt_lo < mt_hi ? (mt_hi - mt_lo + qstride - 1) / qstride : 0;
-    const int n0 = nt * BN;
-    const int spt = 9 * CC;
-    const int total = ntile * spt;
-    const int nchunks = ntile * CC;
-
-    const uint32_t wrow_b = uint32_t(9 * a.Kin) * 2u;
-    const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
-    uint32_t a_off[AI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int r = (wave * AI + j) * 8 + (lane >> 3);
-        const int ch = n0 + r;
-        a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t((lane & 7) ^ fsw128(r)) * 16u : OOB;
-    }
-    const __amdgpu_buffer_rsrc_t xres = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
-
-    // weight piece p of stage s (past the stream's end: out of range, still counted)
-    auto issue_w = [&](int s, int p) {
-        const bool live = s < total;
-        const int within = s % spt;
-        const int cc = within / 9, tap = within - cc * 9;
-        const uint32_t soff = uint32_t(tap * a.Kin + cc * 64) * 2u;
-        dma16(wres, wring + (s % NS) * WSLOT + (wave * AI + p) * 1024, live ? a_off[p] : OOB, soff);
-    };
-    // halo piece j of global chunk h (tile h / CC): the per-lane offsets of the tile are set up once
-    uint32_t hoff[HI_MAX];
-    int h_tile = -1;
-    auto halo_setup = [&](int t) {
-        h_tile = t;
-        const int mt = mt_lo + t * qstride;
-        const int n = mt / a.tpi, rem = mt - n * a.tpi;
-        const int ty = rem / a.tpr, tx = rem - ty * a.tpr;
-#pragma unroll
-        for (int j = 0; j < HI_MAX; ++j) {
-            const int hr = (wave + NW * j) * 8 + (lane >> 3);
-            const int iy = ty * TS - 1 + hr / HS, ix = tx * TS - 1 + hr % HS;
-            const bool ok = j < hi_w && hr < HROWS && uint32_t(iy) < uint32_t(a.H) && uint32_t(ix) < uint32_t(a.W);
-            hoff[j] = ok ? uint32_t((int64_t(n) * a.x_bs + (int64_t(iy) * a.W + ix) * a.x_ld) * 2) +
-                               uint32_t((lane & 7) ^ (hr & 7)) * 16u
-                         : OOB;
-        }
-    };
-    auto issue_h = [&](int h, int j) {
-        const int t = h / CC, cc = h - t * CC;
-        if (t != h_tile) halo_setup(t);
-        dma16(xres, hbuf0 + (h & 1) * HBUF + (wave + NW * j) * 1024, hoff[j], uint32_t(cc * 64) * 2u);
-    };
-    // does step g, phase p issue a halo piece (chunk g / 9 + 1's piece (pos - 1) * 2 + p at positions 1..3)?
-    auto hflag = [&](int g, int p) -> int {
-        if (g < 0) return 0;
-        const int pos = g % 9, j = (pos - 1) * 2 + p;
-        return pos >= 1 && pos <= 3 && j < hi_w && g / 9 + 1 < nchunks ? 1 : 0;
-    };
-
-    uint32_t offA[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-        const int ra = wr * WCH + fr;
-        offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
-    }
-    bf16x8 fa[TM], fb[TN];
-    f32x4 acc[TM][TN];
-    auto read_frags = [&](const char* As, const char* Hs, int dh, int dw, int kk) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + offA[kk] + i * 16 * RB);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int hr = (wc * TN + j + dh) * HS + fr + dw;
-            fb[j] = *reinterpret_cast<const bf16x8*>(Hs + hr * RB + (((kk * 4 + fc) ^ (hr & 7)) << 4));
-        }
-    };
-    auto mma = [&]() {
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if constexpr (MODE == HF)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
-                                                                        __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0, 0, 0);
-                else
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-            }
-        __builtin_amdgcn_s_setprio(0);
-    };
-
-    float ssum[TM][4], ssq[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
-    const bool half = a.out_f32 == 2;
-    const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.H) * a.W * a.y_ld) * 2;
-    const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
-    const int wch0 = n0 + wr * WCH;
-
-    // ---- prologue: halo of chunk 0, weight stages 0 and 1; stage 0 and the halo landed everywhere; group 1
-    // falls one barrier behind
-    if (total > 0) {
-#pragma unroll
-        for (int j = 0; j < HI_MAX; ++j)
-            if (j < hi_w) issue_h(0, j);
-    }
-#pragma unroll
-    for (int s = 0; s < D; ++s)
-#pragma unroll
-        for (int p = 0; p < AI; ++p) issue_w(s, p);
-    vm_wait<AI>();
-    step_barrier();
-    if (grp == 1) step_barrier();
-
-    int g = 0, wslot = 0;
-    for (int ct = 0; ct < ntile; ++ct) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int cc = 0; cc < CC; ++cc) {
-            const char* Hs = hbuf0 + ((ct * CC + cc) & 1) * HBUF;
-            for (int tap = 0; tap < 9; ++tap, ++g) {
-                const int kh = tap / 3, kw = tap - kh * 3;
-                const int dh = MODE == HF ? kh : 2 - kh, dw = MODE == HF ? kw : 2 - kw;
-                const char* As = wring + wslot * WSLOT;
-                // phase (g, 0)
-                read_frags(As, Hs, dh, dw, 0);
-                issue_w(g + D, 0);
-                if (hflag(g, 0)) issue_h(g / 9 + 1, (tap - 1) * 2);
-                bar_then_wait();
-                mma();
-                step_barrier();
-                // phase (g, 1): stage g+1 (and any halo issued before it) retired by this wave
-                read_frags(As, Hs, dh, dw, 1);
-                issue_w(g + D, 1);
-                if (hflag(g, 1)) issue_h(g / 9 + 1, (tap - 1) * 2 + 1);
-                vm_wait_n(AI + hflag(g - 1, 1) + hflag(g, 0) + hflag(g, 1));
-                step_barrier();
-                mma();
-                step_barrier();
-                wslot = wslot == NS - 1 ? 0 : wslot + 1;
-            }
-        }
-        // ---- epilogue of tile ct in the load slot after its last MFMAs; transpose area = the halo buffer of the
-        // tile's last chunk (group 1 read it in the interval before; it is re-filled from position 1 of the
-        // chunk after next)
-        const int mt = mt_lo + ct * qstride;
-        const int n = mt / a.tpi, rem = mt - n * a.tpi;
-        const int ty = rem / a.tpr, tx = rem - ty * a.tpr;
-        char* ep = hbuf0 + (((ct + 1) * CC - 1) & 1) * HBUF + wave * EPW;
-        auto pix_off = [&](int qp) -> uint32_t {
-            const int oy = ty * TS + wc * TN + (qp >> 4), ox = tx * TS + (qp & 15);
-            return uint32_t((int64_t(n) * a.y_bs + (int64_t(oy) * a.W + ox) * a.y_ld + wch0) * 2);
-        };
-        epilogue_store<TM, TN, true>(acc, ssum, ssq, a.st_sum != nullptr, ep, lane, wch0, a.Nout, yres, half,
-                                     a.accumulate != 0, pix_off);
-    }
-    if (grp == 0) step_barrier();
-
-    if (a.st_sum) {
-        vm_wait<0>();
-        __syncthreads();
-        float (*red)[WN][BN] = reinterpret_cast<float (*)[WN][BN]>(smem);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = ssum[i][r], sq = ssq[i][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    s += __shfl_xor(s, o, 64);
-                    sq += __shfl_xor(sq, o, 64);
-                }
-                if (fr == 0) {
-                    const int cl = wr * WCH + i * 16 + fc * 4 + r;
-                    red[0][wc][cl] = s;
-                    red[1][wc][cl] = sq;
-                }
-            }
-        __syncthreads();
-        const int row = xcd + 8 * qq;
-        for (int cl = tid; cl < BN; cl += NW * 64) {
-            const int ch = n0 + cl;
-            if (ch < a.Nout) {
-                float ps = 0.f, pq = 0.f;
-#pragma unroll
-                for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
-                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
-            }
-        }
-    }
-}
-
 }  // namespace
 
 HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad) {
@@ -695,11 +442,6 @@ int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uin
     a.tpr = a.W / TS;
     a.tpi = (a.H / TS) * a.tpr;
     a.mt_total = a.N * a.tpi;
-    if (p.cfg == 0 && g_hpipe_pp) {
-        if (!dgrad) conv_hpp_kernel<HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
-        else conv_hpp_kernel<HD><<<dim3(p.grid), dim3(512), 0, st>>>(a);
-        return 0;
-    }
     if (!dgrad) {
         if (p.cfg == 0) conv_hpipe_kernel<128, 2, 4, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
         else conv_hpipe_kernel<64, 1, 8, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);

@@ -17,8 +17,6 @@ struct PipePlan {
 // -1: default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
 // tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
 extern int g_pipe_force;
-// 256 x 128 tiles on the ping-pong kernel (1) or the 16-wave kernel (0)
-extern int g_pipe_pp;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);

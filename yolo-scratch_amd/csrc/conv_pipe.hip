@@ -40,9 +40,6 @@ namespace ym {
 // output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
 // wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
 int g_pipe_force = -1;
-// 256 x 128 tiles: 1 the ping-pong kernel (conv_pp_kernel), 0 the 16-wave one (ym_conv_set_pipe_pp)
-int g_pipe_pp = 0;
-long long* g_pp_dbg = nullptr;
 
 namespace {
 
@@ -63,7 +60,6 @@ struct PipeArgs {
     int ntiles;                               // channel tiles
     int mt_pre[5];                            // first m-tile of each class (prefix), mt_pre[ncls] = total
     int ncls;
-    long long* dbg;                           // diagnostic timestamps (ping-pong ablation 3 only)
 };
 
 struct Cls {
@@ -223,23 +219,6 @@ struct Issuer {
         for (int j = 0; j < BI; ++j) dma16(xres, st + BN * RB + (wave * BI + j) * 1024, live ? b_off[j] : OOB, kb);
     }
 
-    // pieces [P0, P0 + NP) of the stage (weight pieces first, then activation pieces): the ping-pong kernel
-    // issues a stage in two halves, one per load phase
-    template <int P0, int NP>
-    __device__ __forceinline__ void issue_part(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off, bool live) {
-        const uint32_t kb = uint32_t(kci) * 128u;
-        const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
-        const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
-        const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
-        const __amdgpu_buffer_rsrc_t xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
-                                                      __builtin_amdgcn_readfirstlane(x_bytes));
-#pragma unroll
-        for (int d = P0; d < P0 + NP; ++d) {
-            if (d < AI) dma16(wres, st + (wave * AI + d) * 1024, live ? a_off[d] : OOB, a_tap + kb);
-            else dma16(xres, st + BN * RB + (wave * BI + (d - AI)) * 1024, live ? b_off[d - AI] : OOB, kb);
-        }
-    }
-
     // advance the stream position by one stage (new tap: its gather offsets; new tile: its pixels)
     __device__ __forceinline__ void advance() {
         if (++kci == kc) {
@@ -256,7 +235,9 @@ struct Issuer {
     }
 };
 
-template <int BM, int BN, int WM, int WN, int MODE>
+// EPI: 0 LDS-transposed epilogue (forward); 2 register-only epilogue (epilogue_regs: no LDS, so hipcc does not
+// drain the in-flight stages in front of it) whose stores the next step's wait leaves in flight (data gradient)
+template <int BM, int BN, int WM, int WN, int MODE, int EPI = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
     constexpr int NS = 3;                     // LDS ring: stage g computing, g+1 and g+2 in flight
     constexpr int RB = 128;                   // 64 K x 2 B per LDS row
@@ -271,6 +252,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     // epilogue transpose area: 16 pixels x (BN / WM) channels x 2 B per wave, after the ring
     constexpr int WCH = BN / WM;                          // channels per wave
     constexpr int EPW = 16 * WCH * 2;                     // bytes per wave
+    constexpr int EPS = EPI == 2 ? TM * TN / 2 : TN * (16 / (64 / (WCH * 2 / 16)));   // epilogue stores per lane
     static_assert(NS * STAGE + NW * EPW <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + NW * EPW];
 
@@ -376,8 +358,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         read_frags(f1a, f1b, buf, 1);
         mma(f0a, f0b);
         // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight (every step issues DPS DMAs,
-        // live or not, so the count is constant)
-        vm_wait<DPS>();
+        // live or not, so the count is constant); in a tile's first step the previous tile's epilogue stores,
+        // issued after stage g+2's pieces, may stay in flight too
+        if (EPI == 2 && ck == 0 && ct > 0) vm_wait<DPS + EPS>();
+        else vm_wait<DPS>();
         step_barrier();
         // the slot of stage g is free again (every wave's reads of it returned before the barrier): stage
         // g+3's DMAs go out one at a time between the second half's MFMAs (issued in a burst they held both
@@ -403,7 +387,21 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         // transposed through this wave's LDS area 16 pixels at a time, so every store is a 16-B piece of
         // a pixel's contiguous channel run (8 lanes = one 128-B segment), issued as buffer stores whose
         // out-of-tile pixels fall out of range (no branches, a fixed count per tile)
-        {
+        if constexpr (EPI == 2) {
+            const int wch0 = n0 + wr * WCH;
+            const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
+            const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
+            auto pix_off = [&](int qp) -> uint32_t {
+                const int64_t m = m0 + wc * (BM / WN) + qp;
+                if (m >= cc.Mc) return OOB;
+                const uint32_t n = uint32_t(m) / cc.OHW, pix = uint32_t(m) - n * cc.OHW;
+                const uint32_t ci_ = pix / uint32_t(cc.OWc);
+                const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW + int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
+                return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
+            };
+            epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_f32 == 2,
+                                  a.accumulate != 0, pix_off);
+        } else {
             char* ep = smem + NS * STAGE + wave * EPW;
             const int wch0 = n0 + wr * WCH;                   // first channel of this wave
             const bool half = a.out_f32 == 2;                  // fp16 z (forward) or bf16 (data gradient)
@@ -506,231 +504,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     }
 }
 
-// Ping-pong variant of the 256 x 128 tile (round 3): 8 waves of 64 channels x 64 pixels in two groups of
-// four (one wave of each group per SIMD), the second group one workgroup barrier behind the first.  Every
-// interval between two barriers, one group runs a 16-MFMA cluster (one 32-deep half of a K step) while the
-// other reads the next half's fragments and issues its share of the stage DMA, so each SIMD's MFMA pipe is
-// fed by alternate waves instead of all waves meeting at one barrier per K step with their loads and MFMAs
-// in series.  Per wave and phase (a 32-deep half of a K step):
-//   load part:    [tile epilogue] + 8 ds_read_b128 + 3 LDS-DMA pieces (half a stage, 2 stages ahead)
-//                 [+ counted vmcnt after the stage's second half] ; lgkmcnt(0) ; barrier
-//   compute part: 16 MFMAs ; barrier
-// Stages: 3-slot ring of 48 KB (stage g computing, g+1 landed or landing, g+2 being issued).  RAW: a wave's
-// stage g+1 pieces are retired by its vmcnt in its load part of (g, 1), before the barrier that precedes
-// the first read of stage g+1 (group 0's load part of (g+1, 0)); WAR: stage g+2 goes into the slot of stage
-// g-1, whose last reads (group 1, load part of (g-1, 1)) retired before the barrier in front of the first
-// issue (group 0, load part of (g, 0)).
-template <int MODE, int ABL = 0>
-__global__ void __launch_bounds__(512, 1) conv_pp_kernel(PipeArgs a) {
-    constexpr int BM = 256, BN = 128, WM = 2, WN = 4, NW = 8, NS = 3, RB = 128;
-    constexpr int AI = BN / 8 / NW, BI = BM / 8 / NW, DPS = AI + BI, HP = DPS / 2;
-    constexpr int TM = BN / WM / 16, TN = BM / WN / 16;          // 4 x 4 subtiles: 64 ch x 64 px per wave
-    constexpr int STAGE = (BM + BN) * RB;
-    constexpr int WCH = BN / WM, EPW = 16 * WCH * 2;
-    static_assert(DPS % 2 == 0 && NS * STAGE + NW * EPW <= 160 * 1024, "ping-pong geometry");
-    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + NW * EPW];
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wave >> 2;                                    // 0: leads, 1: one barrier behind
-    const int wr = grp, wc = wave & 3;                            // channel block, pixel block
-    const int fc = lane >> 4, fr = lane & 15;
-    const int kc = a.Kin >> 6;
-
-    const int G8 = int(gridDim.x) >> 3;
-    const int xcd = int(blockIdx.x) & 7, q = int(blockIdx.x) >> 3;
-    const int nt = q % a.ntiles, qq = q / a.ntiles, qstride = G8 / a.ntiles;
-    const int mt_total = a.mt_pre[a.ncls];
-    const int per = (mt_total + 7) >> 3;
-    const int mt_lo = xcd * per + qq, mt_hi = min(xcd * per + per, mt_total);
-    const int ntile = mt_lo < mt_hi ? (mt_hi - mt_lo + qstride - 1) / qstride : 0;
-    const int n0 = nt * BN;
-    int total = 0;
-    if (a.ncls == 1) total = ntile * cls_of(a, 0).ntap * kc;
-    else
-        for (int t = 0; t < ntile; ++t) total += cls_of(a, cls_find(a, mt_lo + t * qstride)).ntap * kc;
-
-    const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
-    const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
-    uint32_t a_off[AI];
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-        const int r = (wave * AI + j) * 8 + (lane >> 3);
-        const int ch = n0 + r;
-        a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t((lane & 7) ^ fsw128(r)) * 16u : OOB;
-    }
-    uint32_t offA[2], offB[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-        const int ra = wr * WCH + fr, rb = wc * (BM / WN) + fr;
-        offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
-        offB[kk] = uint32_t(BN * RB + rb * RB + (((kk * 4 + fc) ^ fsw128(rb)) << 4));
-    }
-    bf16x8 fa[TM], fb[TN];
-    f32x4 acc[TM][TN];
-    float ssum[TM][4], ssq[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
-
-    const bool half = a.out_f32 == 2;
-    const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
-    const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
-    const int wch0 = n0 + wr * WCH;
-    int64_t m0 = 0;
-    Cls cc{};
-    auto epilogue = [&]() {
-        char* ep = smem + NS * STAGE + wave * EPW;
-        const int64_t mb = m0 + wc * (BM / WN);
-        auto pix_off = [&](int qp) -> uint32_t {
-            const int64_t m = mb + qp;
-            if (m >= cc.Mc) return OOB;
-            const uint32_t n = uint32_t(m) / cc.OHW, pix = uint32_t(m) - n * cc.OHW;
-            const uint32_t ci_ = pix / uint32_t(cc.OWc);
-            const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW + int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
-            return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
-        };
-        epilogue_store<TM, TN, true>(acc, ssum, ssq, a.st_sum != nullptr, ep, lane, wch0, a.Nout, yres, half,
-                               a.accumulate != 0, pix_off);
-    };
-
-    Issuer<BM, BN, NW, MODE> is(a, wave, lane, mt_lo, qstride, ntile);
-    is.start();
-    // prologue: stages 0 and 1 in flight, stage 0 landed everywhere; group 1 falls one barrier behind
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        is.issue_dma(smem + s * STAGE, wres, a_off, s < total);
-        is.advance();
-    }
-    vm_wait<DPS>();
-    step_barrier();
-    if (grp == 1) step_barrier();
-
-    int buf = 0, g = 0;
-    for (int ct = 0; ct < ntile; ++ct) {
-        {
-            const int mt = mt_lo + ct * qstride;
-            const int c = cls_find(a, mt);
-            cc = cls_of(a, c);
-            m0 = int64_t(mt - a.mt_pre[c]) * BM;
-        }
-        const int cnk = cc.ntap * kc;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int ck = 0; ck < cnk; ++ck, ++g) {
-            auto stamp = [&](int k) {
-                if constexpr ((ABL & 4) != 0) {
-                    if (blockIdx.x == 0 && lane == 0 && g < 32) a.dbg[(wave * 32 + g) * 8 + k] = __builtin_amdgcn_s_memtime();
-                }
-            };
-            stamp(0);
-            const int ibuf = buf == 0 ? NS - 1 : buf - 1;             // slot of stage g + 2 (= g - 1)
-            const bool live = g + 2 < total;
-            // ---- phase (g, 0)
-            {
-                const char* As = smem + buf * STAGE + offA[0];
-                const char* Bs = smem + buf * STAGE + offB[0];
-                if (!(ABL & 2) || g == 0) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * RB);
-                }
-                if constexpr (!(ABL & 1)) is.template issue_part<0, HP>(smem + ibuf * STAGE, wres, a_off, live);
-                stamp(1);
-                step_barrier();
-                stamp(2);
-                __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        if constexpr (MODE == PF)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
-                                                                                __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0, 0, 0);
-                        else
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-                    }
-                __builtin_amdgcn_s_setprio(0);
-                stamp(3);
-                step_barrier();
-                stamp(4);
-            }
-            // ---- phase (g, 1): the stage's second half of DMA pieces, then stage g + 1 retired (own pieces)
-            {
-                const char* As = smem + buf * STAGE + offA[1];
-                const char* Bs = smem + buf * STAGE + offB[1];
-                if (!(ABL & 2)) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * RB);
-                }
-                if constexpr (!(ABL & 1)) is.template issue_part<HP, HP>(smem + ibuf * STAGE, wres, a_off, live);
-                is.advance();
-                vm_wait<DPS>();
-                stamp(5);
-                step_barrier();
-                stamp(6);
-                __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        if constexpr (MODE == PF)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
-                                                                                __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0, 0, 0);
-                        else
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-                    }
-                __builtin_amdgcn_s_setprio(0);
-                stamp(7);
-                step_barrier();
-            }
-            buf = buf == NS - 1 ? 0 : buf + 1;
-        }
-        epilogue();                                                // in the slot of the next load part
-    }
-    if (grp == 0) step_barrier();                                 // barrier counts even again
-
-    if (a.st_sum) {
-        vm_wait<0>();
-        __syncthreads();
-        float (*red)[WN][BN] = reinterpret_cast<float (*)[WN][BN]>(smem);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                float s = ssum[i][r], sq = ssq[i][r];
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
-                    s += __shfl_xor(s, o, 64);
-                    sq += __shfl_xor(sq, o, 64);
-                }
-                if (fr == 0) {
-                    const int cl = wr * WCH + i * 16 + fc * 4 + r;
-                    red[0][wc][cl] = s;
-                    red[1][wc][cl] = sq;
-                }
-            }
-        __syncthreads();
-        const int row = xcd + 8 * qq;
-        for (int cl = tid; cl < BN; cl += NW * 64) {
-            const int ch = n0 + cl;
-            if (ch < a.Nout) {
-                float ps = 0.f, pq = 0.f;
-#pragma unroll
-                for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
-                a.st_sum[int64_t(row) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(row) * a.Nout + ch] = pq;
-            }
-        }
-    }
-}
-
 // tile configurations
 struct Cfg {
     int bm, bn;
@@ -742,23 +515,13 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
-    if (cfg == 0 && g_pipe_pp) {
-        if (mode == PF) {
-            if (g_pipe_pp == 1) conv_pp_kernel<PF><<<dim3(grid), dim3(512), 0, st>>>(a);
-            if (g_pipe_pp == 2) conv_pp_kernel<PF, 1><<<dim3(grid), dim3(512), 0, st>>>(a);
-            if (g_pipe_pp == 3) conv_pp_kernel<PF, 2><<<dim3(grid), dim3(512), 0, st>>>(a);
-            if (g_pipe_pp == 4) conv_pp_kernel<PF, 4><<<dim3(grid), dim3(512), 0, st>>>(a);
-            if (g_pipe_pp == 5) conv_pp_kernel<PF, 5><<<dim3(grid), dim3(512), 0, st>>>(a);
-            if (g_pipe_pp == 6) conv_pp_kernel<PF, 6><<<dim3(grid), dim3(512), 0, st>>>(a);
-        } else conv_pp_kernel<PD><<<dim3(grid), dim3(512), 0, st>>>(a);
-        return;
-    }
     if (mode == PF) {
         if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PF><<<dim3(grid), dim3(1024), 0, st>>>(a);
         else conv_pipe_kernel<256, 64, 1, 8, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
     } else {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PD><<<dim3(grid), dim3(1024), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PD><<<dim3(grid), dim3(512), 0, st>>>(a);
+        // data gradient: register-only epilogue (same-process A/B, s@640 bs64: 1-8 % faster on 9 of 10 layers)
+        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PD, 2><<<dim3(grid), dim3(1024), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PD, 2><<<dim3(grid), dim3(512), 0, st>>>(a);
     }
 }
 
@@ -837,21 +600,8 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
         acc += int((int64_t(a.N) * ohc * owc + bm - 1) / bm);
     }
     a.mt_pre[a.ncls] = acc;
-    if (g_pipe_pp >= 4 && !g_pp_dbg) {
-        hipMalloc(&g_pp_dbg, 8 * 32 * 8 * sizeof(long long));
-        hipMemset(g_pp_dbg, 0, 8 * 32 * 8 * sizeof(long long));
-    }
-    a.dbg = g_pp_dbg;
     launch_cfg(dgrad ? PD : PF, p.cfg, a, p.grid, st);
     return YM_OK;
 }
 
 }  // namespace ym
-
-extern "C" int ym_pp_stamps(long long* host) {
-    // diagnostic: copy the ping-pong kernel's timestamps (8 waves x 32 K steps x 8 points) to the host
-    if (!ym::g_pp_dbg) return -1;
-    hipDeviceSynchronize();
-    hipMemcpy(host, ym::g_pp_dbg, 8 * 32 * 8 * sizeof(long long), hipMemcpyDeviceToHost);
-    return 0;
-}
