@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 GPU session: parity tests, the driver's exact bench command, its rocprofv3 kernel-trace summary,
 # and the per-layer counter passes behind the 3x3 family's traffic.  Outputs under gpurun_out/$1.
-# Usage (GPU box, repo root): bash tools/gpu_r03.sh TAG [skip-tests]
+# Usage (GPU box, repo root): bash tools/gpu_r03.sh TAG [skip-tests|tests] [short]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r03}
@@ -30,6 +30,7 @@ F=$(find $OUT/pmc_FETCH_SIZE -name "*counter_collection.csv" | head -1)
 W=$(find $OUT/pmc_WRITE_SIZE -name "*counter_collection.csv" | head -1)
 python3 $R/tools/pmc_layers.py $F $W $OUT/seq.json profiles/r03 > $OUT/pmc_layers.txt && tail -3 $OUT/pmc_layers.txt
 cp $R/profiles/traffic.json $OUT/traffic.json
+[ "$3" = "short" ] && exit 0
 timeout -k 10 300 python3 $R/tools/miopen_ref.py > $OUT/miopen_ref.txt 2> $OUT/miopen_ref.err || { echo "miopen ref failed"; tail -5 $OUT/miopen_ref.err; }
 cat $OUT/miopen_ref.txt
 bash $R/tools/pmc_conv.sh $OUT/pmc73 73 && python3 $R/tools/pmc_summary.py $OUT/pmc73 > $OUT/pmc73_summary.txt; cat $OUT/pmc73_summary.txt
