@@ -92,6 +92,21 @@ __device__ __forceinline__ int cls_find(const PipeArgs& a, int mt) {
 
 __device__ __forceinline__ int fsw128(int r) { return (r >> 1) & 7; }
 
+// (image, in-image index, row) of pixel m0 + r, r < 256, given the tile's (tn, tp) = divmod(m0, ohw) (computed
+// once per tile): one wrap for the image, the row by the float reciprocal of the row width with one
+// correction (x < 2^24) — the generic 32-bit divisions these replace cost ~30 VALU each and ran per pixel
+// in every tile's setup and epilogue (12 per lane and tile)
+__device__ __forceinline__ void split_pix(uint32_t tn, uint32_t tp, uint32_t r, uint32_t ohw, uint32_t w, float inv_w,
+                                          uint32_t& n, uint32_t& pix, uint32_t& row) {
+    pix = tp + r;
+    n = tn;
+    while (pix >= ohw) { pix -= ohw; ++n; }
+    uint32_t q = uint32_t(float(pix) * inv_w);
+    const int rem = int(pix) - int(q * w);
+    q = rem < 0 ? q - 1 : (rem >= int(w) ? q + 1 : q);
+    row = q;
+}
+
 // one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc + voff + soff land at lds + 16 l
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
@@ -152,7 +167,8 @@ struct Issuer {
         kh0 = k.kh0;
         kw0 = k.kw0;
         const int64_t m0 = int64_t(mt - a.mt_pre[c]) * BM;
-        const uint32_t nfirst = uint32_t(m0 / k.OHW);
+        const uint32_t nfirst = uint32_t(m0) / k.OHW, tp = uint32_t(m0) - nfirst * k.OHW;
+        const float inv_w = 1.0f / float(k.OWc);
         x_tile = a.x + int64_t(nfirst) * a.x_bs;
         const int64_t xb = (int64_t(a.N) - nfirst) * a.x_bs * 2;
         x_bytes = int(xb < 0x7fffffff ? xb : 0x7fffffff);
@@ -161,9 +177,8 @@ struct Issuer {
             const int r = (wave * BI + j) * 8 + lrow;
             const int64_t m = m0 + r;
             if (m < k.Mc) {
-                const uint32_t um = uint32_t(m);
-                const uint32_t n = um / k.OHW, pix = um - n * k.OHW;
-                const uint32_t ii = pix / uint32_t(k.OWc);
+                uint32_t n, pix, ii;
+                split_pix(nfirst, tp, uint32_t(r), k.OHW, uint32_t(k.OWc), inv_w, n, pix, ii);
                 const int oh = int(ii) * a.os + k.py, ow = int(pix - ii * uint32_t(k.OWc)) * a.os + k.px;
                 if (MODE == PF) {
                     bh[j] = oh * a.stride - a.pad;
@@ -343,12 +358,17 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     int ct = 0, ck = 0, cnk = 0, buf = 0;
     int64_t m0 = 0;
     Cls cc{};
+    uint32_t t_n = 0, t_p = 0;                // divmod(m0, OHW) of the computing tile
+    float inv_owc = 1.f;
     for (int g = 0; g < total; ++g) {
         if (ck == 0) {
             const int mt = mt_lo + ct * qstride;
             const int c = cls_find(a, mt);
             cc = cls_of(a, c);
             m0 = int64_t(mt - a.mt_pre[c]) * BM;
+            t_n = uint32_t(m0) / cc.OHW;
+            t_p = uint32_t(m0) - t_n * cc.OHW;
+            inv_owc = 1.0f / float(cc.OWc);
             cnk = cc.ntap * kc;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -394,8 +414,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
             auto pix_off = [&](int qp) -> uint32_t {
                 const int64_t m = m0 + wc * (BM / WN) + qp;
                 if (m >= cc.Mc) return OOB;
-                const uint32_t n = uint32_t(m) / cc.OHW, pix = uint32_t(m) - n * cc.OHW;
-                const uint32_t ci_ = pix / uint32_t(cc.OWc);
+                uint32_t n, pix, ci_;
+                split_pix(t_n, t_p, uint32_t(wc * (BM / WN) + qp), cc.OHW, uint32_t(cc.OWc), inv_owc, n, pix, ci_);
                 const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW + int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
                 return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
             };
@@ -444,8 +464,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                     const int64_t m = m0 + wc * (BM / WN) + j * 16 + p;
                     uint32_t off = OOB;
                     if (m < cc.Mc && wch0 + c * 8 < a.Nout) {
-                        const uint32_t n = uint32_t(m) / cc.OHW, pix = uint32_t(m) - n * cc.OHW;
-                        const uint32_t ci_ = pix / uint32_t(cc.OWc);
+                        uint32_t n, pix, ci_;
+                        split_pix(t_n, t_p, uint32_t(m - m0), cc.OHW, uint32_t(cc.OWc), inv_owc, n, pix, ci_);
                         const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW +
                                              int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
                         off = uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0 + c * 8) * 2);
