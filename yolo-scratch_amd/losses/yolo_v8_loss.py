@@ -10,8 +10,11 @@ is libyolomi's ym_loss_fwd / ym_loss_bwd on the (B, A, 64+nc) head buffer.
 The host synchronises once per call (the largest per-image box count sizes
 the GT table) instead of 2*B*M+4 times.
 
-The helper functions (bbox_iou, bbox2dist, make_anchors, dist2bbox) are the
-reference's tensor utilities with identical semantics.  TaskAlignedAssigner and
+The helper functions (bbox_iou, bbox2dist, make_anchors, dist2bbox) and the
+reference's helper methods (TaskAlignedAssigner.get_pos_mask / get_box_metrics /
+select_candidates_in_gts / select_highest_overlaps / get_targets, BboxLoss._df_loss,
+v8DetectionLoss.preprocess / bbox_decode) are the reference's tensor utilities with
+identical semantics (tests/test_loss_helpers_cpu.py); the HIP path does not call them.  TaskAlignedAssigner and
 BboxLoss are callable on their own with the reference's signatures and return
 conventions; they run the same HIP kernels on explicit tensors (ym_tal_assign,
 ym_bbox_loss_fwd / _bwd).
@@ -23,6 +26,7 @@ import math
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from yolomi._lib import YolomiError, call, lib, require_device, stream_ptr
 
@@ -133,6 +137,54 @@ class TaskAlignedAssigner(nn.Module):
              tgi.data_ptr(), stream_ptr(dev))
         return t_lab.to(gt_labels.dtype), t_box, t_sc, fg, tgi
 
+    # The reference's step helpers (:182-270), kept for code that calls them directly.  They are tensor
+    # utilities on whatever device their inputs live on — the HIP forward above computes the same quantities
+    # fused (ym_tal_assign) and does not call them.  get_targets reads self.bs / self.n_max_boxes, which
+    # forward sets, as in the reference.
+    def get_pos_mask(self, pd_scores, pd_bboxes, gt_labels, gt_bboxes, anc_points, mask_gt):
+        """-> (mask_pos (B,A,M) float, align_metric, overlaps), reference :182-194."""
+        align_metric, overlaps = self.get_box_metrics(pd_scores, pd_bboxes, gt_labels, gt_bboxes)
+        inside = self.select_candidates_in_gts(anc_points, gt_bboxes)
+        return inside * mask_gt[:, None, :], align_metric, overlaps
+
+    def get_box_metrics(self, pd_scores, pd_bboxes, gt_labels, gt_bboxes):
+        """-> (score^alpha * IoU^beta, IoU clamped at 0), both (B,A,M), reference :196-208."""
+        overlaps = bbox_iou(pd_bboxes[:, :, None, :], gt_bboxes[:, None, :, :], xywh=False).squeeze(-1).clamp_(0)
+        cls_idx = gt_labels.long()[:, None, :].expand(-1, pd_scores.shape[1], -1)
+        return torch.gather(pd_scores, 2, cls_idx).pow(self.alpha) * overlaps.pow(self.beta), overlaps
+
+    def select_candidates_in_gts(self, xy_centers, gt_bboxes, eps=1e-9):
+        """(B,A,M) 1.0 where the anchor centre lies strictly inside the box (min side distance > eps),
+        in the boxes' dtype, reference :210-224."""
+        x, y = xy_centers[None, :, None, 0], xy_centers[None, :, None, 1]
+        g = gt_bboxes[:, None, :, :]
+        sides = torch.stack((x - g[..., 0], y - g[..., 1], g[..., 2] - x, g[..., 3] - y), -1)
+        return (sides.amin(-1) > eps).to(gt_bboxes.dtype)
+
+    def select_highest_overlaps(self, mask_pos, overlaps, n_max_boxes):
+        """Anchors claimed by several boxes keep only their highest-IoU box; -> (target_gt_idx, fg_mask,
+        mask_pos), reference :226-244."""
+        fg_mask = mask_pos.sum(-1)
+        if fg_mask.max() > 1:
+            shared = (fg_mask[..., None] > 1).expand(-1, -1, n_max_boxes)
+            best = torch.zeros_like(mask_pos).scatter_(-1, overlaps.argmax(-1, keepdim=True), 1)
+            mask_pos = torch.where(shared, best, mask_pos).float()
+            fg_mask = mask_pos.sum(-1)
+        return mask_pos.argmax(-1), fg_mask, mask_pos
+
+    def get_targets(self, gt_labels, gt_bboxes, target_gt_idx, fg_mask):
+        """-> (labels (B,A), boxes (B,A,4), one-hot scores (B,A,nc) zero off the foreground), reference
+        :246-270."""
+        rows = target_gt_idx + self.n_max_boxes * torch.arange(self.bs, dtype=torch.int64,
+                                                               device=gt_labels.device)[:, None]
+        labels = gt_labels.flatten()[rows]
+        boxes = gt_bboxes.view(-1, 4)[rows]
+        labels.clamp_(0, self.num_classes)
+        scores = torch.zeros(*labels.shape, self.num_classes, dtype=torch.float32, device=labels.device)
+        scores.scatter_(2, labels[..., None].long(), 1)
+        scores = torch.where(fg_mask[..., None].repeat(1, 1, self.num_classes) > 0, scores, 0)
+        return labels, boxes, scores.float()
+
 
 class _BboxLossFn(torch.autograd.Function):
     @staticmethod
@@ -183,6 +235,18 @@ class BboxLoss(nn.Module):
         tss = torch.as_tensor(target_scores_sum, dtype=torch.float32, device=pred_dist.device).detach().reshape(1)
         return _BboxLossFn.apply(pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores,
                                  tss.contiguous(), fg_mask)
+
+    @staticmethod
+    def _df_loss(pred_dist, target):
+        """Distribution focal loss of (n, reg_max) logits against continuous targets (n, 4) -> (n, 1), reference
+        :312-324 (a tensor utility; the HIP box loss computes the same term fused).  Clamps `target` in place, as
+        the reference does."""
+        target = target.clamp_(0, pred_dist.shape[-1] - 1 - 0.01)
+        left = target.long()
+        w_left = (left + 1) - target
+        ce_l = F.cross_entropy(pred_dist, left.view(-1), reduction="none").view(left.shape)
+        ce_r = F.cross_entropy(pred_dist, (left + 1).view(-1), reduction="none").view(left.shape)
+        return (ce_l * w_left + ce_r * (1 - w_left)).mean(-1, keepdim=True)
 
 
 class _LossCtx:
@@ -299,6 +363,33 @@ class v8DetectionLoss:
             raise YolomiError("the fused loss runs on the MI355X only (got CPU tensors)")
         loss, items = _LossFn.apply(head, self, batch, level_hw)
         return loss, items
+
+    # The reference's helpers (:501-538), kept for code that calls them directly: tensor utilities on the
+    # inputs' device; __call__ does the same work inside ym_loss_fwd and does not call them.
+    def preprocess(self, targets_cls, targets_bbox, batch_idx, batch_size, img_size):
+        """Padded per-image target table (batch_size, max boxes, 6) = [class, x1, y1, x2, y2 (pixels), 1],
+        boxes in each image's original order, rows past an image's count zero; reference :501-527."""
+        if len(targets_cls) == 0:
+            return torch.zeros(batch_size, 0, 6, device=self.device)
+        owner = [batch_idx == i for i in range(batch_size)]
+        counts = [int(m.sum()) for m in owner]
+        out = torch.zeros(batch_size, max(counts), 6, device=self.device)
+        pix = targets_bbox * img_size.repeat(2)[:4]
+        for i, (m, n) in enumerate(zip(owner, counts)):
+            if n:
+                out[i, :n, 0] = targets_cls[m, 0]
+                out[i, :n, 1:5] = pix[m]
+                out[i, :n, 5] = 1.0
+        return out
+
+    def bbox_decode(self, anchor_points, pred_dist, stride_tensor):
+        """(B, A, 4*reg_max) side distributions -> xyxy boxes around the anchors (grid units): the softmax
+        expectation over the reg_max bins of each side, then dist2bbox; reference :529-538."""
+        if self.reg_max > 1:
+            b, a, c = pred_dist.shape
+            bins = torch.arange(c // 4, device=pred_dist.device, dtype=pred_dist.dtype)
+            pred_dist = pred_dist.view(b, a, 4, c // 4).softmax(3).matmul(bins.view(-1, 1)).view(b, a, 4)
+        return dist2bbox(pred_dist, anchor_points[None], xywh=False, dim=-1)
 
     def assignment(self):
         """(target_gt_idx, fg_mask, target-score magnitude) of the last call, as device tensors (for tests)."""
