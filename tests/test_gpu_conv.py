@@ -218,6 +218,10 @@ HPIPE = [
     (3, 32, 32, 256, 128, 3, 1, 1, 0, 0),
     (2, 48, 16, 192, 256, 3, 1, 1, 32, 64),
     (9, 80, 80, 128, 128, 3, 1, 1, 0, 0),
+    # 64 -> 64: the 72 KB weight tensor resident in LDS (cfg 2), a halo per tile
+    (2, 16, 16, 64, 64, 3, 1, 1, 0, 0),
+    (3, 32, 48, 64, 64, 3, 1, 1, 64, 32),
+    (9, 80, 80, 64, 64, 3, 1, 1, 0, 0),
 ]
 
 
@@ -229,8 +233,8 @@ def test_hpipe_kernel_vs_torch(shape):
 
 def test_hpipe_selection():
     """By default the halo-pipelined kernel takes the 3x3 stride-1 convs on 16-multiple maps with >= 512 tiles
-    (the 80x80 / 160x160 layers at bs64) and >= 128 output channels, in either direction; never stride 2 or
-    other maps."""
+    (the 80x80 / 160x160 layers at bs64) and >= 128 output channels or 64 -> 64 (weights resident), in either
+    direction; never stride 2 or other maps."""
     from yolomi._lib import lib
 
     def desc(*shape):
@@ -241,8 +245,10 @@ def test_hpipe_selection():
     assert lib().ym_conv_algo(ctypes.byref(d), 0) == 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
     d = desc(64, 80, 80, 128, 64, 3, 1, 1)          # 64 output channels: forward elsewhere, dgrad (128) here
     assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
+    d = desc(64, 80, 80, 64, 64, 3, 1, 1)
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) == 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
     for shape in [(64, 40, 40, 128, 128, 3, 1, 1), (64, 160, 160, 64, 64, 3, 2, 1), (2, 80, 80, 128, 128, 3, 1, 1),
-                  (64, 80, 80, 64, 64, 3, 1, 1)]:
+                  (64, 80, 80, 32, 64, 3, 1, 1)]:
         d = desc(*shape)
         assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4, shape
 

@@ -7,7 +7,7 @@ namespace ym {
 
 struct HPipePlan {
     int ok;          // the halo-pipelined kernel handles this conv
-    int cfg;         // 0: 128-channel tiles, 1: 64-channel tiles
+    int cfg;         // 0: 128-channel tiles, 1: 64-channel tiles, 2: 64 -> 64 with the weights resident in LDS
     int grid;        // workgroups (persistent; a multiple of 8 * channel tiles)
     int rows;        // rows of the BN statistics partials (= grid / channel tiles)
 };

@@ -103,9 +103,13 @@ __device__ __forceinline__ void step_barrier() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BN, int WM, int WN, int MODE>
+// WRES (64 -> 64 channels, one 64-channel chunk): the layer's whole weight tensor (9 taps x 64 x 64, 72 KB)
+// is staged into LDS once per workgroup and stays resident; the K loop then stages only the halo (41 pieces
+// per 9 K steps) and waits only before a chunk's first step for its halo
+template <int BN, int WM, int WN, int MODE, bool WRES = false>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
-    constexpr int NS = 4;                     // weight ring: slot of step g computing, g+1..g+3 in flight
+    constexpr int NS = WRES ? 9 : 4;          // weight ring: slot of step g computing, g+1..g+3 in flight (WRES:
+                                              // the 9 taps, resident)
     constexpr int NW = WM * WN;
     static_assert(NW == 8, "8 waves");
     constexpr int AI = BN / 8 / NW;           // weight DMA pieces per wave per step
@@ -158,6 +162,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     // weight stage s into its ring slot; past the stream's end (live false) the DMAs fetch nothing but still
     // count, so every step issues AI of them and the counted waits stay constant
     auto issue_w = [&](int s, bool live) {
+        if constexpr (WRES) return;
         const int within = s % spt;
         const int cc = within / 9, tap = within - cc * 9;
         const uint32_t soff = uint32_t(tap * a.Kin + cc * 64) * 2u;
@@ -237,10 +242,21 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     // ---- prologue: halo of chunk 0, weight stages 0..3; stage 0 and the halo landed everywhere
     const int nchunks = ntile * CC;
     if (total > 0) issue_h(0);
+    if constexpr (WRES) {
+        // every tap's weight slice, once (slot t = tap t; one 64-channel chunk)
 #pragma unroll
-    for (int s = 0; s < NS; ++s)
-        issue_w(s, s < total);
-    vm_wait_n(AI * (NS - 1));
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int j = 0; j < AI; ++j)
+                dma16(wres, wring + t * WSLOT + (wave * AI + j) * 1024, total > 0 ? a_off[j] : OOB,
+                      uint32_t(t * a.Kin) * 2u);
+        vm_wait<0>();
+    } else {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+            issue_w(s, s < total);
+        vm_wait_n(AI * (NS - 1));
+    }
     step_barrier();
     if (total > 0) read_frags(f0a, f0b, 0, 0);
 
@@ -256,7 +272,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         mma(f0a, f0b);
         // stage g+1 must have landed (own DMAs); stages g+2 and g+3 may stay in flight, and so may halos
         // issued in steps g-2 and g-1 (after stage g+1, when those steps began a chunk with a successor)
-        if (g + 1 < total) {
+        if (WRES) {
+            // the only in-loop DMA is the next chunk's halo (issued 9 steps ahead): retire it before its first read
+            if (g + 1 < total && (g + 1) % 9 == 0) vm_wait<0>();
+        } else if (g + 1 < total) {
             int pend = 2 * AI;
 #pragma unroll
             for (int b = 1; b <= 2; ++b) {
@@ -274,13 +293,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         issue_w(g + NS, g + NS < total);
         read_frags(f0a, f0b, g + 1, 0);
         mma(f1a, f1b);
+        if constexpr (!WRES) {
 #pragma unroll
-        for (int d = 0; d < AI; ++d) {
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // one weight DMA
-            __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (AI + 1), 0);  // MFMAs
+            for (int d = 0; d < AI; ++d) {
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // one weight DMA
+                __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (AI + 1), 0);  // MFMAs
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);                  // next-step reads
+            __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - AI * ((TM * TN) / (AI + 1)), 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);                  // next-step reads
-        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - AI * ((TM * TN) / (AI + 1)), 0);
         if (++ck < spt) continue;
         ck = 0;
 
@@ -396,13 +417,17 @@ HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad) {
     const int kin = dgrad ? d->cout : d->cin, nout = dgrad ? d->cin : d->cout;
     // >= 128 output channels: the 64-channel tile (8 MFMAs per half step and wave) measured slower than
     // conv_halo.hip on the 64-channel 80x80 layers (0.080 vs 0.070 ms fwd, s@640 bs64)
-    if (kin % 64 != 0 || nout % 8 != 0 || nout < 128) return p;
+    if (kin % 64 != 0 || nout % 8 != 0) return p;
+    // 64 -> 64: the weight-resident 64-channel tile (cfg 2; same process, s@640 bs64 80x80: fwd 67 -> 57 us,
+    // dgrad 57 -> 53 us against conv_halo); other < 128-channel layers stay on conv_halo
+    const bool wres = kin == 64 && nout == 64;
+    if (nout < 128 && !wres) return p;
     const int64_t in_ld = dgrad ? d->y_ld : d->x_ld, in_bs = dgrad ? d->y_bs : d->x_bs;
     const int64_t out_ld = dgrad ? d->x_ld : d->y_ld, out_bs = dgrad ? d->x_bs : d->y_bs;
     if (in_ld % 8 || in_bs % 8 || out_ld % 8 || out_bs % 8) return p;
     if (!dgrad && d->out_f32 == 1) return p;                     // Detect's fp32 bias convs: conv.hip
     if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31) || int64_t(d->n) * out_bs * 2 >= (int64_t(1) << 31)) return p;
-    p.cfg = nout >= 128 ? 0 : 1;
+    p.cfg = nout >= 128 ? 0 : (wres ? 2 : 1);
     const int bn = p.cfg == 0 ? 128 : 64;
     const int ntiles = (nout + bn - 1) / bn;
     const int64_t tiles = int64_t(d->n) * (d->h / TS) * (d->w / TS);
@@ -442,6 +467,11 @@ int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uin
     a.tpr = a.W / TS;
     a.tpi = (a.H / TS) * a.tpr;
     a.mt_total = a.N * a.tpi;
+    if (p.cfg == 2) {
+        if (!dgrad) conv_hpipe_kernel<64, 1, 8, HF, true><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+        else conv_hpipe_kernel<64, 1, 8, HD, true><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+        return 0;
+    }
     if (!dgrad) {
         if (p.cfg == 0) conv_hpipe_kernel<128, 2, 4, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
         else conv_hpipe_kernel<64, 1, 8, HF><<<dim3(p.grid), dim3(512), 0, st>>>(a);
