@@ -568,6 +568,8 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     // input channels, at >= 256 tiles; never the stride-2 data gradient
     if (mode == 3 && (os == 2 || (d->k == 3 && nout < 128 && (dgrad || kin < 128)))) return p;
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
+    // split_pix: in-image pixel indices as exact floats, row estimates within one of the truth
+    if (int64_t(OH) * OW >= (int64_t(1) << 24) || OH >= (1 << 16)) return p;
     const int64_t M = int64_t(d->n) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
     p.cfg = nout >= 128 ? 0 : 1;
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
