@@ -360,8 +360,8 @@ DIRECT = [
 
 @pytest.mark.parametrize("shape", DIRECT, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in DIRECT])
 def test_direct_kernel_vs_torch(shape):
-    """The direct register-weight kernel forced on (the stride-2 data gradient by row-parity class over
-    column pairs) vs PyTorch fp32 on the same rounded operands."""
+    """The direct register-weight kernel forced on (the stride-2 data gradient over 2x2-pixel quads, all four
+    output-parity classes per task; odd maps leave partial quads) vs PyTorch fp32 on the same rounded operands."""
     from yolomi._lib import call, lib, ConvDesc
     n, h, w, cin, cout, k, s, xe, ye = shape
     p = k // 2

@@ -8,8 +8,7 @@ namespace ym {
 struct DirectPlan {
     int ok;          // the direct kernel handles this conv
     int variant;     // template instance (conv_direct.hip: kVariants)
-    int grid;        // workgroups per output-parity class (= rows of the BN statistics partials)
-    int classes;     // output-parity classes (4: stride-2 data gradient, else 1)
+    int grid;        // workgroups (= rows of the BN statistics partials)
 };
 
 // -1: default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size

@@ -15,8 +15,8 @@
 // buffer offsets.  No LDS on the main path, no barriers; the only reduction is the BatchNorm
 // statistics (xor shuffles, then the waves in order through LDS: one partial row per workgroup).
 // Data gradients: stride 1 as a conv of dz with the transposed weight copy (taps mirrored by the
-// index formula), stride 2 as 4 output-parity classes, each task one class (its pixels every other
-// column, so the valid taps are the same for every lane).
+// index formula), stride 2 over 2x2-pixel quads (all four output-parity classes of a dz pixel's
+// neighbourhood in one task, conv_direct_quad_kernel).
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
@@ -41,8 +41,7 @@ struct DirArgs {
     int Kin, Nout, pad;
     int accumulate;
     int OHc, OWc;                              // class map (dgrad stride 2: ceil(O/2); else O)
-    int64_t tpc;                               // tasks per class
-    int ncls;
+    int64_t tpc;                               // tasks (16 x TP pixels, or 2x2-pixel quads, per lane group)
 };
 
 template <int MODE>
@@ -245,26 +244,24 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
     }
 }
 
-// Stride-2 3x3 data gradient by output-ROW parity PY: a task is 16 x TP column PAIRS (2j, 2j+1) of
-// rows 2i + PY, both column classes computed by the same wave — column 2j takes tap kw = 1 from dz
-// column j, column 2j + 1 taps kw = 0 / 2 from dz columns j + 1 / j — and the epilogue stores the
-// pair's two 16-pixel groups back to back, so each 128-B line of dx (two 32-channel bf16 pixels) is
-// completed by one wave at one time.  (One class per task wrote every other pixel: 64-B halves of
-// lines whose other half came from another grid row of classes much later — 2 TB/s on the s@640
-// model.1 data gradient whose HBM roof is ~6 TB/s.)
-template <int NT, int KC, int TP, int PY>
-__device__ __forceinline__ void direct_body_s2dg(const DirArgs& a, int64_t first, int64_t step, int64_t ntask,
-                                                 char* ep) {
+// Stride-2 3x3 data gradient, all four output-parity classes in one task: a lane owns the 2x2 dx
+// pixels (2i + py, 2j + px) of one (image, i, j) and loads the 2x2 dz pixels (i + dh, j + dw) they
+// read ONCE — each of the nine taps maps one dz pixel (dh = kh == 0, dw = kw == 0) onto one class
+// (py = kh != 1, px = kw != 1); the epilogue stores the quad's two rows as back-to-back column pairs,
+// so each 128-B line of dx (two 32-channel bf16 pixels) is completed by one wave at one time.
+// Round 3: the row-parity tasks it replaces (one launch row per row class, column pairs per task) read
+// every dz row twice, and the two classes (3 vs 6 taps) drifted apart so the second read missed L2:
+// s@640 model.1 data gradient 255 -> 188 us, bit-identical (same tap / chunk order per pixel).
+template <int NT, int KC, int TP>
+__device__ __forceinline__ void direct_body_s2dg_quad(const DirArgs& a, int64_t first, int64_t step, int64_t ntask,
+                                                      char* ep) {
     using F = bf16x8;
     const int lane = threadIdx.x & 63, fr = lane & 15, fc = lane >> 4;
-    auto live = [&](int t) constexpr -> bool { return ((PY + 1 - t / 3) & 1) == 0; };
-    auto pxof = [&](int t) constexpr -> int { return (t % 3) == 1 ? 0 : 1; };
     F wa[9][KC][NT];
     {
         const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, int64_t(a.Nout) * 9 * a.Kin * 2);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            if (!live(t)) continue;
+        for (int t = 0; t < 9; ++t)
 #pragma unroll
             for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
@@ -273,16 +270,14 @@ __device__ __forceinline__ void direct_body_s2dg(const DirArgs& a, int64_t first
                     const uint32_t off = co < a.Nout ? uint32_t(((co * 9 + t) * a.Kin + kc * 32 + fc * 8) * 2) : OOB;
                     wa[t][kc][nt] = __builtin_bit_cast(F, buf_load16(wr, off));
                 }
-        }
     }
     const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
     const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
-    // lane's pixel pair in each group: image n, dx row oh, pair j (columns 2j, 2j + 1)
-    struct Pairs {
-        int n[TP], oh[TP], j[TP];
+    struct Quads {
+        int n[TP], i[TP], j[TP];
         bool ok[TP];
     };
-    auto decode = [&](int64_t tl, Pairs& P) {
+    auto decode = [&](int64_t tl, Quads& P) {
         const uint32_t chw = uint32_t(a.OHc) * uint32_t(a.OWc);
 #pragma unroll
         for (int g = 0; g < TP; ++g) {
@@ -290,31 +285,30 @@ __device__ __forceinline__ void direct_body_s2dg(const DirArgs& a, int64_t first
             const uint32_t nn = uint32_t(m / chw), r = uint32_t(m - int64_t(nn) * chw);
             const uint32_t i = r / uint32_t(a.OWc), j = r - i * uint32_t(a.OWc);
             P.n[g] = int(nn);
-            P.oh[g] = int(i) * 2 + PY;
+            P.i[g] = int(i);
             P.j[g] = int(j);
-            P.ok[g] = int(nn) < a.N && P.oh[g] < a.OH;
+            P.ok[g] = int(nn) < a.N;
         }
     };
-    auto load = [&](const Pairs& P, F (&b)[9][TP][KC]) {
+    // b[g][dh][dw][kc]: dz pixel (i + dh, j + dw) of group g (zero outside the dz map)
+    auto load = [&](const Quads& P, F (&b)[TP][2][2][KC]) {
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            if (!live(t)) continue;
-            const int kh = t / 3, kw = t % 3;
+        for (int g = 0; g < TP; ++g)
 #pragma unroll
-            for (int g = 0; g < TP; ++g) {
-                const int ow = 2 * P.j[g] + pxof(t);
-                const int ih = (P.oh[g] + a.pad - kh) >> 1, iw = (ow + a.pad - kw) >> 1;
-                const bool in = P.ok[g] && ow < a.OW && unsigned(ih) < unsigned(a.GH) && unsigned(iw) < unsigned(a.GW);
-                const uint32_t base =
-                    in ? uint32_t((int64_t(P.n[g]) * a.x_bs + (int64_t(ih) * a.GW + iw) * a.x_ld + fc * 8) * 2) : OOB;
+            for (int dh = 0; dh < 2; ++dh)
 #pragma unroll
-                for (int kc = 0; kc < KC; ++kc)
-                    b[t][g][kc] = __builtin_bit_cast(F, buf_load16(xr, base == OOB ? OOB : base + kc * 64));
-            }
-        }
+                for (int dw = 0; dw < 2; ++dw) {
+                    const int ih = P.i[g] + dh, iw = P.j[g] + dw;
+                    const bool in = P.ok[g] && ih < a.GH && iw < a.GW;
+                    const uint32_t base =
+                        in ? uint32_t((int64_t(P.n[g]) * a.x_bs + (int64_t(ih) * a.GW + iw) * a.x_ld + fc * 8) * 2) : OOB;
+#pragma unroll
+                    for (int kc = 0; kc < KC; ++kc)
+                        b[g][dh][dw][kc] = __builtin_bit_cast(F, buf_load16(xr, base == OOB ? OOB : base + kc * 64));
+                }
     };
-    Pairs P;
-    F b[9][TP][KC];
+    Quads P;
+    F b[TP][2][2][KC];
     int64_t task = first;
     if (task < ntask) {
         decode(task, P);
@@ -322,51 +316,55 @@ __device__ __forceinline__ void direct_body_s2dg(const DirArgs& a, int64_t first
     }
     float ssum[NT][4], ssq[NT][4];     // unused (no statistics in a data gradient)
     for (; task < ntask; task += step) {
-        // acc[2g + px]: the pair's two columns as adjacent 16-pixel groups
-        f32x4 accT[NT][2 * TP];
+        // accT[4g + 2 py + px]: the quad's rows as two back-to-back column pairs
+        f32x4 accT[NT][4 * TP];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
-            for (int q = 0; q < 2 * TP; ++q) accT[nt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int q = 0; q < 4 * TP; ++q) accT[nt][q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-            if (!live(t)) continue;
+            const int kh = t / 3, kw = t % 3;
+            const int py = kh != 1, px = kw != 1, dh = kh == 0, dw = kw == 0;
 #pragma unroll
             for (int g = 0; g < TP; ++g)
 #pragma unroll
                 for (int kc = 0; kc < KC; ++kc)
 #pragma unroll
                     for (int nt = 0; nt < NT; ++nt)
-                        accT[nt][2 * g + pxof(t)] = mma(wa[t][kc][nt], b[t][g][kc], accT[nt][2 * g + pxof(t)]);
+                        accT[nt][4 * g + 2 * py + px] = mma(wa[t][kc][nt], b[g][dh][dw][kc], accT[nt][4 * g + 2 * py + px]);
         }
-        const Pairs Q = P;
+        const Quads Q = P;
         if (task + step < ntask) {
             decode(task + step, P);
             load(P, b);
         }
-        uint32_t own[2 * TP];
+        uint32_t own[4 * TP];
 #pragma unroll
         for (int g = 0; g < TP; ++g)
 #pragma unroll
-            for (int px = 0; px < 2; ++px) {
-                const int ow = 2 * Q.j[g] + px;
-                own[2 * g + px] = Q.ok[g] && ow < a.OW
-                                      ? uint32_t((int64_t(Q.n[g]) * a.y_bs + (int64_t(Q.oh[g]) * a.OW + ow) * a.y_ld) * 2)
-                                      : OOB;
-            }
+            for (int py = 0; py < 2; ++py)
+#pragma unroll
+                for (int px = 0; px < 2; ++px) {
+                    const int oh = 2 * Q.i[g] + py, ow = 2 * Q.j[g] + px;
+                    own[4 * g + 2 * py + px] =
+                        Q.ok[g] && oh < a.OH && ow < a.OW
+                            ? uint32_t((int64_t(Q.n[g]) * a.y_bs + (int64_t(oh) * a.OW + ow) * a.y_ld) * 2)
+                            : OOB;
+                }
         auto pix_off = [&](int q) -> uint32_t {
             uint32_t v = 0;
 #pragma unroll
-            for (int k = 0; k < 2 * TP; ++k)
+            for (int k = 0; k < 4 * TP; ++k)
                 if ((q >> 4) == k) v = own[k];
             return uint32_t(__shfl(int(v), q & 15, 64));
         };
-        epilogue_store<NT, 2 * TP>(accT, ssum, ssq, false, ep, lane, 0, a.Nout, yres, false, a.accumulate != 0,
+        epilogue_store<NT, 4 * TP>(accT, ssum, ssq, false, ep, lane, 0, a.Nout, yres, false, a.accumulate != 0,
                                    pix_off);
     }
 }
 
-// grid (blocks, classes): blockIdx.y is the output-parity class of a stride-2 data gradient
+// forward / stride-1 data gradient (the stride-2 data gradient is conv_direct_quad_kernel)
 template <int NT, int KC, int KS, int S, int MODE, int TP>
 __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     __shared__ float red[2][4][16 * NT];
@@ -384,15 +382,8 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
     const int64_t lo = a.tpc * xcd / 8, hi = a.tpc * (xcd + 1) / 8;
     const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
-    if constexpr (S == 2 && MODE == 1) {
-        static_assert(KS == 3 && (NT == 2 || NT == 4), "stride-2 data gradient: 3x3, 32 / 64 output channels");
-        // row-parity classes (blockIdx.y), column pairs per task (direct_body_s2dg)
-        if (blockIdx.y == 0) direct_body_s2dg<NT, KC, TP, 0>(a, first, step, hi, epl[wave]);
-        else direct_body_s2dg<NT, KC, TP, 1>(a, first, step, hi, epl[wave]);
-        return;
-    } else {
-        direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]);
-    }
+    static_assert(!(S == 2 && MODE == 1), "the stride-2 data gradient runs conv_direct_quad_kernel");
+    direct_body<NT, KC, KS, S, MODE, TP, 0, 0>(a, ssum, ssq, first, step, hi, epl[wave]);
     if constexpr (MODE == 0) {
         if (!a.st_sum) return;
         // 16 pixel lanes per channel group, then the 4 waves in order
@@ -419,6 +410,17 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     }
 }
 
+// the four-class stride-2 data gradient: 2 workgroups per CU (256 VGPRs per lane at most)
+template <int NT, int KC, int TP>
+__global__ void __launch_bounds__(256, 2) conv_direct_quad_kernel(DirArgs a) {
+    __shared__ __attribute__((aligned(16))) char epl[4][16 * 16 * NT * 2];
+    const int wave = threadIdx.x >> 6;
+    const int xcd = blockIdx.x & 7, q = blockIdx.x >> 3, nq = gridDim.x >> 3;
+    const int64_t lo = a.tpc * xcd / 8, hi = a.tpc * (xcd + 1) / 8;
+    const int64_t first = lo + int64_t(q) * 4 + wave, step = int64_t(nq) * 4;
+    direct_body_s2dg_quad<NT, KC, TP>(a, first, step, hi, epl[wave]);
+}
+
 using KernFn = void (*)(DirArgs);
 
 struct Variant {
@@ -432,7 +434,7 @@ struct Variant {
 // measured slower than the implicit GEMM: 0.083 vs 0.076 ms)
 const Variant kVariants[] = {
     DIR_VARIANT(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
-    DIR_VARIANT(2, 2, 3, 2, 1, 1),   // dgrad of it: dz 64 -> dx 32, row-parity classes x column pairs
+    {2, 2, 3, 2, 1, 1, conv_direct_quad_kernel<2, 2, 1>},   // dgrad of it: dz 64 -> dx 32, 2x2-pixel quads
     DIR_VARIANT(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
     DIR_VARIANT(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
     DIR_VARIANT(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
@@ -473,10 +475,8 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
         const int os = dgrad ? d->stride : 1;
         const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
         const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
-        // stride-2 data gradients as 2 row-parity classes over column pairs
-        p.classes = os == 2 ? 2 : 1;
-        constexpr int64_t GCAP = 1024;    // total workgroups over the classes (512-4096 measured within 3 %)
-        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(GCAP / p.classes, (tpc + 3) / 4)) & ~int64_t(7));
+        constexpr int64_t GCAP = 1024;    // workgroups (512-4096 measured within 3 %)
+        p.grid = int(std::max<int64_t>(8, std::min<int64_t>(GCAP, (tpc + 3) / 4)) & ~int64_t(7));
         return p;
     }
     return p;
@@ -497,10 +497,9 @@ int direct_launch(const DirectPlan& p, const ym_conv_desc* d, int dgrad, const u
     }
     a.N = d->n; a.pad = d->pad; a.accumulate = d->accumulate;
     const int os = dgrad ? d->stride : 1;
-    a.OHc = (a.OH + os - 1) / os; a.OWc = (a.OW + os - 1) / os;   // (pairs mode: OWc = column pairs)
-    a.ncls = p.classes;
+    a.OHc = (a.OH + os - 1) / os; a.OWc = (a.OW + os - 1) / os;   // (stride 2: quad rows / columns)
     a.tpc = (int64_t(a.N) * a.OHc * a.OWc + 16 * v.tp - 1) / (16 * v.tp);
-    hipLaunchKernelGGL(v.fn, dim3(p.grid, a.ncls), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(v.fn, dim3(p.grid), dim3(256), 0, st, a);
     return 0;
 }
 
