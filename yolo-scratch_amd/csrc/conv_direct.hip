@@ -410,7 +410,8 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(DirArgs a) {
     }
 }
 
-// the four-class stride-2 data gradient: 2 workgroups per CU (256 VGPRs per lane at most)
+// the four-class stride-2 data gradient: 2 workgroups per CU (256 VGPRs per lane at most; one quad group per
+// task — two, at one workgroup per CU, measured 6 % slower)
 template <int NT, int KC, int TP>
 __global__ void __launch_bounds__(256, 2) conv_direct_quad_kernel(DirArgs a) {
     __shared__ __attribute__((aligned(16))) char epl[4][16 * 16 * NT * 2];
@@ -433,14 +434,14 @@ struct Variant {
 // C3k2 64->64 1x1 / 32->32 3x3 / 96->128 1x1) in both directions (an 80x80 128->128 1x1 variant
 // measured slower than the implicit GEMM: 0.083 vs 0.076 ms)
 const Variant kVariants[] = {
-    DIR_VARIANT(4, 1, 3, 2, 0, 1),   // fwd 32 -> 64, 3x3 s2
+    DIR_VARIANT(4, 1, 3, 2, 0, 2),   // fwd 32 -> 64, 3x3 s2 (two 16-pixel groups per task: 204 -> 191 us vs one)
     {2, 2, 3, 2, 1, 1, conv_direct_quad_kernel<2, 2, 1>},   // dgrad of it: dz 64 -> dx 32, 2x2-pixel quads
     DIR_VARIANT(2, 1, 3, 1, 0, 2),   // fwd 32 -> 32, 3x3 s1
     DIR_VARIANT(2, 1, 3, 1, 1, 2),   // dgrad 32 -> 32, 3x3 s1
     DIR_VARIANT(4, 2, 1, 1, 0, 4),   // 64 -> 64 1x1 (fwd and dgrad)
     DIR_VARIANT(4, 2, 1, 1, 1, 4),
     DIR_VARIANT(8, 3, 1, 1, 0, 2),   // fwd 96 -> 128 1x1
-    DIR_VARIANT(6, 4, 1, 1, 1, 2),   // dgrad: dz 128 -> dx 96
+    DIR_VARIANT(6, 4, 1, 1, 1, 4),   // dgrad: dz 128 -> dx 96 (four groups per task: 176 -> 164 us vs two)
 };
 #undef DIR_VARIANT
 
