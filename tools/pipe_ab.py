@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--also", nargs="*", default=[], help="other setters applied first, NAME=VALUE")
+    ap.add_argument("--kinds", nargs="+", default=["fwd", "dgrad"], help="fwd / dgrad / wgrad")
     args = ap.parse_args()
     import torch
     import yaml
@@ -50,9 +51,13 @@ def main():
             d = op.desc
             for v in args.variants:
                 setter(v)
-                for kind in ("fwd", "dgrad"):
+                for kind in args.kinds:
                     if kind == "dgrad" and not plan.needs_grad(op.x):
                         continue
+                    if kind == "wgrad":
+                        lib().ym_conv_wgrad_workspace_size.restype = ctypes.c_size_t
+                        nws = lib().ym_conv_wgrad_workspace_size(ctypes.byref(d))
+                        ws = torch.empty(max(1, nws // 4), dtype=torch.float32, device=dev)
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     for r in range(args.reps + 2):
                         if r == 2:
@@ -60,15 +65,18 @@ def main():
                         if kind == "fwd":
                             call("ym_conv_fwd", ctypes.byref(d), op.x.ptr(), op.wf.data_ptr(), op.z.data_ptr(), None,
                                  op.ps[0].data_ptr(), op.ps[1].data_ptr(), st)
-                        else:
+                        elif kind == "dgrad":
                             call("ym_conv_dgrad", ctypes.byref(d), op.z.data_ptr(), op.wt.data_ptr(), op.x.gptr(), st)
+                        else:
+                            call("ym_conv_wgrad", ctypes.byref(d), op.z.data_ptr(), op.x.ptr(), ws.data_ptr(),
+                                 ws.numel() * 4, plan.gptr(op.m.conv.weight), 0, st)
                     e1.record()
                     torch.cuda.synchronize()
                     res.setdefault((i, kind, v), []).append(e0.elapsed_time(e1) / args.reps)
     setter(0)
     for i in args.only:
         d = plan.ops[i].desc
-        for kind in ("fwd", "dgrad"):
+        for kind in args.kinds:
             if (i, kind, args.variants[0]) not in res:
                 continue
             line = f"op {i:3d} {d.cin:4d}->{d.cout:<4d} k{d.k} s{d.stride} {d.oh}x{d.ow} {kind:5s}:"
