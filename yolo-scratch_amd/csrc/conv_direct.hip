@@ -447,6 +447,22 @@ const Variant kVariants[] = {
 
 int direct_mode() { return g_direct_force >= 0 ? g_direct_force : 1; }
 
+// workgroups of variant i the whole chip holds at once (CUs x the kernel's occupancy), cached per variant
+int resident_blocks(int i) {
+    static int cache[16] = {0};
+    if (cache[i] == 0) {
+        int dev = 0, cus = 256, per = 1;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kVariants[i].fn), 256, 0) !=
+                hipSuccess || per < 1)
+            per = 1;
+        cache[i] = std::max(8, (cus * per) & ~7);
+    }
+    return cache[i];
+}
+
 }  // namespace
 
 DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
@@ -476,7 +492,9 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
         const int os = dgrad ? d->stride : 1;
         const int64_t OHc = (OH + os - 1) / os, OWc = (OW + os - 1) / os;
         const int64_t tpc = (int64_t(d->n) * OHc * OWc + 16 * v.tp - 1) / (16 * v.tp);
-        constexpr int64_t GCAP = 1024;    // workgroups (512-4096 measured within 3 %)
+        // persistent: as many workgroups as the chip holds at once (1024 before: model.1 forward -12 %, its data
+        // gradient -5.5 %, the other stem-stage layers -1..-10 %, profiles/r03/direct_grid_ab.txt)
+        const int64_t GCAP = resident_blocks(i);
         p.grid = int(std::max<int64_t>(8, std::min<int64_t>(GCAP, (tpc + 3) / 4)) & ~int64_t(7));
         return p;
     }
