@@ -385,24 +385,6 @@ static bool pick_rect(int OH, int OW, int tp, int hpad, int& TH, int& TW) {
 }  // namespace
 
 int g_halo_force = -1;
-int g_halo_grid = 0;
-
-// workgroups of configuration c the chip holds at once (CUs x occupancy), cached
-static int halo_resident(int c) {
-    static int cache[2] = {0, 0};
-    if (cache[c] == 0) {
-        int dev = 0, cus = 256, per = 1;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
-        const void* fn = c == 0 ? reinterpret_cast<const void*>(conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD>)
-                                : reinterpret_cast<const void*>(conv_halo_kernel<2, 2, 4, 2, 4, 3, H_FWD>);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, c == 0 ? 512 : 256, 0) != hipSuccess || per < 1)
-            per = 1;
-        cache[c] = cus * per;
-    }
-    return cache[c];
-}
 
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
     HaloPlan p{};
@@ -439,7 +421,6 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
         p.nco = nco;
         int gx = (p.ntiles + 7) & ~7;
         gx = std::min(gx, std::max(8, (2048 / nco) & ~7));   // bounded BN partial rows
-        if (g_halo_grid < 0) gx = std::min(gx, std::max(8, (halo_resident(c) / nco) & ~7));
         p.gx = gx;
         return p;
     }
@@ -482,5 +463,3 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
 }
 
 }  // namespace ym
-
-extern "C" void ym_conv_set_halo_grid(int v) { ym::g_halo_grid = v; }
