@@ -5,7 +5,10 @@ One step = one full training iteration on a synthetic 640x640 batch of 64 images
 forward (HIP plan) + v8 loss (fused kernels) + backward + RCCL gradient all-reduce (N > 1)
 + clip_grad_norm_(10) + AdamW — exactly train_yolo11_cuda.train_one_epoch's body.
 
-    python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torchrun)
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: either launched by torchrun (one process per GPU, RANK / WORLD_SIZE in the environment), or run
+directly, in which case this process starts torchrun with N ranks as a child and relays rank 0's line.
 
 Rank 0 prints ONE JSON line.  `roofline` is the dense 3x3 conv family against the 16-bit MFMA peak
 (the north star's target: every fwd / dgrad / wgrad launch of a k=3 Conv block bracketed with HIP
@@ -132,7 +135,47 @@ def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 2, steps: int =
                       f"oracle fp32 restatement, median of {steps} steps after {warmup} warm-up"}
 
 
+def needs_launch(gpus: int, env=None) -> bool:
+    """True when `--gpus N` (N > 1) was asked for but this process is not a rank of an N-process job: the
+    driver's one-GPU command form (`python bench.py --gpus N`) then starts the ranks itself."""
+    env = os.environ if env is None else env
+    return gpus > 1 and "WORLD_SIZE" not in env and "RANK" not in env
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(gpus: int, argv, port: int):
+    """The torchrun command that runs this script as `gpus` ranks on one node (one process per GPU,
+    rendezvous on 127.0.0.1), with the caller's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+
+
+def launch(gpus: int, argv) -> int:
+    """Parent of an N-rank run: never touches the GPU (the ranks do), starts torchrun as a child process,
+    relays its output (rank 0 prints the JSON line) and returns its exit code."""
+    import subprocess
+    cmd = launch_cmd(gpus, argv, free_port())
+    log("launching", " ".join(cmd))
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
+    # `--gpus N` without a torchrun environment: start the N ranks (before importing anything that could
+    # initialise the GPU in this parent process)
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args()
+    if needs_launch(known.gpus):
+        sys.exit(launch(known.gpus, sys.argv[1:]))
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=150)
@@ -156,9 +199,28 @@ def main():
     rank = ctx.rank if ctx else 0
     world = ctx.world if ctx else 1
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but this job has {world} rank(s) (WORLD_SIZE); "
+                         f"run it as `python bench.py --gpus N` or under torchrun with N processes")
+    if os.environ.get("YM_BENCH_RANKS_ONLY") == "1":
+        # launcher check (tests/test_bench_launch_cpu.py): the job's rank count over a host all-reduce, no GPU
+        one = torch.ones(1)
+        if ctx:
+            dist.all_reduce(one)
+        if rank == 0:
+            print(json.dumps({"n_gpus": world, "ranks_seen": int(one.item())}), flush=True)
+        ydist.shutdown()
+        return
     dev = torch.device("cuda", ctx.local_rank if ctx else 0)
     torch.cuda.set_device(dev)
+    # every rank answers: the count of ranks that took part in one all-reduce of ones (RCCL, or gloo in a
+    # one-GPU rehearsal), reported in the JSON line
+    ranks_seen = 1
+    if ctx:
+        one = torch.ones(1, device=dev)
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        if ranks_seen != world:
+            raise SystemExit(f"bench.py: all-reduce saw {ranks_seen} ranks, expected {world}")
 
     cfg = yaml.safe_load((PKG / "configs" / "yolo11n_crater.yaml").read_text())
     cfg["scale"] = args.scale
@@ -356,6 +418,7 @@ def main():
         "value": round(value, 2),
         "unit": "images/sec",
         "n_gpus": world,
+        "ranks_seen": ranks_seen,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),

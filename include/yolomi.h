@@ -132,36 +132,51 @@ typedef struct {
     int32_t cout_t;            /* row length of dst_t (>= cout; zero padding is the caller's) */
 } ym_wprep_entry;
 
-/* Number of grid-x blocks (= rows of the BN statistics partials) of the implicit-GEMM forward
- * for m output pixels (kept for callers sizing buffers by shape only). */
+/* Rows of the BN statistics partials of the 2-stage implicit GEMM's forward alone, for m output pixels
+ * (kept for callers that size by shape only; NOT the row count of other conv kernels — use
+ * ym_conv_fwd_stat_rows). */
 int ym_conv_stat_blocks(int64_t m, int cout);
-/* Rows of the BN statistics partials ym_conv_fwd writes for this conv (the halo-staged 3x3
- * kernel and the implicit GEMM use different grids); size stat_sum / stat_sq with it. */
+/* Rows of the BN statistics partials ym_conv_fwd writes for this bias-free conv: the kernels use
+ * different grids (the direct kernel: CUs x occupancy; the pipelined kernels: 256 / channel tiles;
+ * the halo kernel: its tile grid; the implicit GEMM: ym_conv_stat_blocks).  stat_sum / stat_sq MUST
+ * hold ym_conv_fwd_stat_rows(d) x cout floats each, with the selection policies below unchanged
+ * between this call and the forward. */
 int ym_conv_fwd_stat_rows(const ym_conv_desc* d);
-/* Which kernel ym_conv_fwd (dgrad = 0) / ym_conv_dgrad (dgrad = 1) runs for d: 3 = the direct
- * register-weight kernel, 2 = the persistent pipelined implicit GEMM, 1 = the halo-staged 3x3
- * stride-1 kernel, 0 = the 2-stage implicit GEMM. */
+/* Which kernel ym_conv_fwd (dgrad = 0, bias-free) / ym_conv_dgrad (dgrad = 1) runs for d: 4 = the
+ * halo-staged pipelined 3x3 kernel, 3 = the direct register-weight kernel, 2 = the persistent
+ * pipelined implicit GEMM, 1 = the halo-staged 3x3 stride-1 kernel, 0 = the 2-stage implicit GEMM. */
 int ym_conv_algo(const ym_conv_desc* d, int dgrad);
-/* Selection policy of the halo-staged kernel for later calls: -1 YM_CONV_HALO / default, 0 never,
- * 1 wherever it applies, 2 maps <= 24 wide, 3 (default) maps <= 48 wide or <= 64 output channels.
- * Returns the previous setting.  Process-wide; not for use while other threads launch convolutions. */
+/* The kernel INSTANCE a bias-free forward (dir 0), data gradient (1) or weight gradient (2) of d runs:
+ * returns an id (algo x 1000 + template instance; weight gradients >= 10000; -1 for a bad argument) and,
+ * if name != NULL, writes its name (e.g. "direct v3", "pipe 256x128", "wgrad3 s2 64x64 8x8 deep"). */
+int ym_conv_kernel(const ym_conv_desc* d, int dir, char* name, int name_len);
+/* Kernel selection as if the batch held n images (0: the real batch, the default): every size rule
+ * and tile choice below evaluates at n, the launch geometry at the real batch — a small-batch parity
+ * test runs the kernel instances of a large-batch step.  Returns the previous setting.  Process-wide;
+ * not for use while other threads plan or launch convolutions. */
+int ym_conv_set_select_batch(int n);
+/* Selection policy of the halo-staged kernel for later calls: -1 default, 0 never, 1 wherever it
+ * applies, 2 maps <= 24 wide, 3 (default) maps <= 48 wide or <= 64 output channels.  Returns the
+ * previous setting.  Process-wide; not for use while other threads launch convolutions. */
 int ym_conv_set_halo(int mode);
 /* Selection policy of the persistent pipelined implicit GEMM (conv_pipe.hip) for later calls: -1
- * YM_CONV_PIPE / default, 0 never, 1 layers of >= 1024 256-pixel tiles with >= 128 output channels,
- * 2 every eligible layer of >= 256 tiles, 3 (default) every 1x1 and the 3x3 with >= 128 output
- * channels (forward: or inputs) at >= 256 tiles, never a stride-2 data gradient.  Returns the
- * previous setting.  Process-wide, like ym_conv_set_halo. */
+ * default, 0 never, 1 layers of >= 1024 256-pixel tiles with >= 128 output channels, 2 every eligible
+ * layer of >= 256 tiles, 3 (default) every 1x1 and the 3x3 with >= 128 output channels (forward: or
+ * inputs) at >= 256 tiles, never a stride-2 data gradient.  Returns the previous setting.
+ * Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_pipe(int mode);
 /* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
- * layers) for later calls: -1 YM_CONV_DIRECT / default, 0 never, 1 maps of >= 1 M output pixels
- * (default), 2 any size.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+ * layers) for later calls: -1 default, 0 never, 1 maps of >= 1 M output pixels (default), 2 any size.
+ * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_direct(int mode);
 /* Selection policy of the halo-staged pipelined 3x3 stride-1 kernel (conv_hpipe.hip: 16x16-pixel tiles,
  * each 64-channel chunk of the 18x18 input halo staged once for all nine taps): -1 default, 0 never,
  * 1 eligible layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
 int ym_conv_set_hpipe(int mode);
-/* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block channel sum / sum-of-squares partials
- * [ym_conv_stat_blocks][cout] for training BatchNorm (BatchNorm2d batch stats). */
+/* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block
+ * channel sum / sum-of-squares partials [ym_conv_fwd_stat_rows(d)][cout] for training BatchNorm
+ * (BatchNorm2d batch stats; not together with a bias).  accumulate is not supported for fp16 output
+ * (out_f32 = 2). */
 int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                 float* stat_sum, float* stat_sq, void* stream);
 /* dx (+)= conv_transpose(dz, w) using the [cin][kh][kw][cout] weight copy. */

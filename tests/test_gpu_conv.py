@@ -355,6 +355,9 @@ DIRECT = [
     (2, 11, 23, 96, 128, 1, 1, 32, 0),
     (1, 19, 9, 64, 64, 1, 1, 0, 0),
     (2, 21, 16, 32, 64, 3, 2, 32, 0),
+    # >= 1 M input pixels: more tasks than the chip holds workgroups, so the persistent grid (CUs x occupancy)
+    # is the resident cap and every workgroup runs many tasks (the BN partial rows = that grid)
+    (10, 320, 320, 32, 64, 3, 2, 0, 0),
 ]
 
 
@@ -384,6 +387,10 @@ def test_direct_kernel_vs_torch(shape):
         xbuf[..., :cin] = x.to(dev)
         ybuf = torch.full((n, oh, ow, cout + ye), 7.0, dtype=torch.float16, device=dev)
         rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+        if n * oh * ow >= 1 << 18:
+            # resident-capped persistent grid: CUs (256 on MI355X) x 1 or 2 workgroups per CU, far fewer than
+            # the 16-pixel tasks (so each workgroup strides over many)
+            assert rows in (256, 512) and rows * 64 < n * oh * ow // 16, rows
         ss = torch.full((rows, cout), float("nan"), device=dev)
         sq = torch.full((rows, cout), float("nan"), device=dev)
         st = torch.cuda.current_stream().cuda_stream
@@ -421,3 +428,33 @@ def test_direct_kernel_vs_torch(shape):
     assert rel(d1[..., :cin], dx_ref) < 1e-2
     assert (d1[..., cin:] == 3.0).all()
     assert rel(dxbuf[..., :cin], 2 * dx_ref) < 1e-2
+
+
+@pytest.mark.parametrize("k,out_f32", [(3, 2), (3, 0), (1, 2)])
+def test_conv_fwd_bias_on_every_policy(k, out_f32):
+    """y = conv(x, w) + bias on a layer the halo-pipelined / direct kernels would take (3x3 stride 1, 80x80,
+    128 channels; those kernels have no bias term): with every policy forced on, ym_conv_fwd must still add the
+    bias (it routes a conv with bias to the kernels that have one).  vs PyTorch fp32 on the same rounded operands."""
+    from yolomi._lib import call, lib, ConvDesc
+    n, h, w, cin, cout, p = 2, 80, 80, 128, 128, k // 2
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, h, w, cout, k, 1, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * cin, cin, h * w * cout, cout
+    d.out_f32, d.accumulate = out_f32, 0
+    g = torch.Generator().manual_seed(7 + k)
+    dev = torch.device("cuda", 0)
+    x = torch.randn(n, h, w, cin, generator=g).half()
+    wt = (torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5).half()
+    bias = torch.randn(cout, generator=g) * 4
+    L = lib()
+    prev = (L.ym_conv_set_hpipe(2), L.ym_conv_set_direct(2), L.ym_conv_set_pipe(2), L.ym_conv_set_halo(1))
+    try:
+        y = torch.zeros(n, h, w, cout, dtype=torch.float16 if out_f32 == 2 else torch.bfloat16, device=dev)
+        call("ym_conv_fwd", ctypes.byref(d), x.to(dev).data_ptr(), wt.permute(0, 2, 3, 1).contiguous().to(dev).data_ptr(),
+             y.data_ptr(), bias.to(dev).data_ptr(), None, None, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    finally:
+        L.ym_conv_set_hpipe(prev[0]); L.ym_conv_set_direct(prev[1]); L.ym_conv_set_pipe(prev[2]); L.ym_conv_set_halo(prev[3])
+    ref = (F.conv2d(x.float().permute(0, 3, 1, 2), wt.float(), bias, padding=p)).permute(0, 2, 3, 1)
+    err = float((y.float().cpu() - ref).abs().max() / ref.abs().max())
+    assert err < (2e-3 if out_f32 == 2 else 1e-2), err

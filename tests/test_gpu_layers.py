@@ -93,6 +93,46 @@ def _relaunch_dgrad(op, dz_ptr, wt_ptr, desc, x_view, st):
     return buf[..., x_view.c0:x_view.c0 + x_view.c].permute(0, 3, 1, 2).to(D).cpu()
 
 
+def kernel_of(desc, direction):
+    """(id, name) of the conv kernel instance the library runs for desc (0 fwd, 1 dgrad, 2 wgrad)."""
+    from yolomi._lib import lib
+    buf = ctypes.create_string_buffer(96)
+    kid = lib().ym_conv_kernel(ctypes.byref(desc), direction, buf, 96)
+    return kid, buf.value.decode()
+
+
+def conv_launches(plan):
+    """Every implicit-GEMM conv launch of a training plan: (op index, direction, desc) for the ConvBN forwards,
+    data gradients (where the input takes a gradient) and weight gradients, and Detect's bias 1x1 convs."""
+    out = []
+    for i, op in enumerate(plan.ops):
+        kind = type(op).__name__
+        if kind == "ConvBN":
+            out += [(i, 0, op.desc), (i, 2, op.desc)]
+            if plan.needs_grad(op.x):
+                out.append((i, 1, op.desc))
+        elif kind == "HeadLevel":
+            for tag, df, db in (("box", op.fb, op.bb), ("cls", op.fc, op.bc)):
+                out += [(f"{i}{tag}", 0, df), (f"{i}{tag}", 1, db), (f"{i}{tag}", 2, db)]
+    return out
+
+
+def selection_at(plan, n):
+    """{(op, direction): (kernel id, name)} the library selects for this plan's convs with n images per batch
+    (the same descriptors with n in place of the plan's batch; no override)."""
+    from yolomi._lib import ConvDesc, lib
+    prev = lib().ym_conv_set_select_batch(0)
+    try:
+        sel = {}
+        for i, dr, d in conv_launches(plan):
+            dn = ConvDesc.from_buffer_copy(d)
+            dn.n = n
+            sel[(i, dr)] = kernel_of(dn, dr)
+        return sel
+    finally:
+        lib().ym_conv_set_select_batch(prev)
+
+
 def teacher_forced(scale, imgsz, bs, seed):
     from losses import v8DetectionLoss
     from datasets.synthetic import synth_batch
@@ -117,6 +157,10 @@ def teacher_forced(scale, imgsz, bs, seed):
     bufs = {k: v for k, v in m.named_buffers()}
     bnames = {id(v): k for k, v in bufs.items()}
     R = Report()
+    R.kernels = {}                       # (op, direction) -> kernel (id, name) whose output was checked
+
+    def seen(i, dr, d):
+        R.kernels[(i, dr)] = kernel_of(d, dr)
 
     def pgrad(p):
         return plan.grad_view(p).to(D).cpu()
@@ -154,6 +198,8 @@ def teacher_forced(scale, imgsz, bs, seed):
                 y = y + vt(op.res)
             z_h, bnv_h = snap[i]
             R.check(f"{tag} z", mat(z_h, B, oh, ow, as_fp16=True), z.detach(), TOL)
+            if kind == "ConvBN":
+                seen(i, 0, op.desc)
             R.check(f"{tag} y", vt(op.y), y.detach(), TOL)
             # batch means may sit near 0: their error is stated relative to the batch standard deviations
             sd = float(var_u.detach().sqrt().norm())
@@ -168,11 +214,14 @@ def teacher_forced(scale, imgsz, bs, seed):
             if kind != "StemConvBN":          # the stem's fused backward never writes dz (ym_stem_bwd_wgrad_stored)
                 R.check(f"{tag} dz", mat(op.z, B, oh, ow), z.grad, TOL)
             R.check(f"{tag} dW", pgrad(mod.conv.weight), W.grad, TOL, gmax)
+            if kind == "ConvBN":
+                seen(i, 2, op.desc)
             R.check(f"{tag} dgamma", pgrad(mod.bn.weight), gam.grad, TOL, gmax)
             R.check(f"{tag} dbeta", pgrad(mod.bn.bias), bet.grad, TOL, gmax)
             if kind == "ConvBN" and plan.needs_grad(op.x):
                 dx = _relaunch_dgrad(op, op.z.data_ptr(), op.wt.data_ptr(), op.desc, op.x, st)
                 R.check(f"{tag} dx", dx, x.grad, TOL_DX)
+                seen(i, 1, op.desc)
             elif kind == "DWConvBN":
                 from yolomi._lib import lib
                 buf = torch.zeros_like(op.x.act.t, dtype=torch.bfloat16)
@@ -208,6 +257,10 @@ def teacher_forced(scale, imgsz, bs, seed):
                     xb.grad, TOL_DX)
             R.check(f"{tag} cls dx", _relaunch_dgrad(op, op.dzc.data_ptr(), op.wc_t.data_ptr(), op.bc, op.xc, st),
                     xc.grad, TOL_DX)
+            for t_, df, db in (("box", op.fb, op.bb), ("cls", op.fc, op.bc)):
+                seen(f"{i}{t_}", 0, df)
+                seen(f"{i}{t_}", 1, db)
+                seen(f"{i}{t_}", 2, db)
         elif kind == "AttnCore":
             qkv = vt(op.qkv)
             Bq, C, H, Wd = qkv.shape
@@ -246,22 +299,42 @@ def teacher_forced(scale, imgsz, bs, seed):
             x, y = vt(op.x), vt(op.y)
             want = F.interpolate(x, scale_factor=2, mode="nearest") if kind == "Upsample2" else x
             assert torch.equal(y, want), f"{tag} forward not bit-exact"
+    R.plan = plan
     worst = sorted(R.rows)[-6:]
     print(f"{scale}@{imgsz} bs{bs}: {len(R.rows)} checks; worst err/tol", [(f"{r:.2f}", w, f"{e:.2e}") for r, w, e in worst])
     assert not R.fail, R.fail
     return R
 
 
-@pytest.mark.parametrize("scale,imgsz,bs,hpipe", [("s", 640, 2, 2), ("m", 256, 1, -1)])
-def test_teacher_forced_every_layer(scale, imgsz, bs, hpipe):
-    """hpipe = 2 forces the halo-pipelined 3x3 kernel on every eligible layer (at bs2 the default policy
-    leaves the 80x80 / 160x160 layers below its tile threshold), so the s@640 run pins it in the network."""
+@pytest.mark.parametrize("scale,imgsz,bs,select", [("s", 640, 2, 64), ("m", 256, 1, 0)])
+def test_teacher_forced_every_layer(scale, imgsz, bs, select):
+    """select = 64: every conv kernel choice (kernel, template instance, tile) is made as for the bench's
+    s@640 bs64 step (ym_conv_set_select_batch) while the batch is 2, so this test checks, op by op, exactly
+    the kernels the benchmarked step runs — the direct / quad kernels on the persistent grids of the 160x160
+    stem stage, the halo-pipelined, pipelined, halo and implicit-GEMM instances and every weight-gradient
+    instance.  The set of (op, direction, kernel) the bs64 plan selects is computed from the plan's own
+    descriptors and every element of it must have been checked.  select = 0: m@256 bs1 at its own sizes."""
     from yolomi._lib import lib
     torch.set_num_threads(min(16, torch.get_num_threads()))
-    prev = lib().ym_conv_set_hpipe(hpipe)
+    prev = lib().ym_conv_set_select_batch(select)
     try:
         R = teacher_forced(scale, imgsz, bs, seed=31)
+        # the override reproduces the bs64 choice launch by launch
+        if select:
+            want = selection_at(R.plan, select)
+            got = {(i, dr): kernel_of(d, dr) for i, dr, d in conv_launches(R.plan)}
+            assert got == want, sorted(set(got.items()) ^ set(want.items()))[:8]
+        else:
+            want = selection_at(R.plan, R.plan.B)
     finally:
-        lib().ym_conv_set_hpipe(prev)
+        lib().ym_conv_set_select_batch(prev)
+    missing = sorted(((str(k[0]), k[1]), v) for k, v in want.items() if R.kernels.get(k) != v)
+    assert not missing, f"selected but not checked: {missing[:10]}"
+    names = sorted({v[1] for v in want.values()})
+    print(f"{scale}@{imgsz}: {len(want)} conv launches checked over {len(names)} kernel instances: {names}")
+    if select == 64:
+        # the instances the bs64 plan is known to run must be among them
+        fams = {n.split(" ")[0] for n in names}
+        assert {"direct", "hpipe", "pipe", "halo", "wgrad3", "wgrad1"} <= fams, fams
     kinds = {w.split(" ")[0].split(":")[1] for _, w, _ in R.rows}
     assert any("model.0" in k for k in kinds)                   # the stem was checked

@@ -32,6 +32,16 @@ void set_error(const char* fmt, ...);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Conv kernel selection batch (ym_conv_set_select_batch): when > 0 the selection rules of every conv
+// kernel (size thresholds, tile shapes) evaluate as if the batch held this many images, while the
+// launch geometry still follows the real batch — so a small-batch parity test runs exactly the kernel
+// instances a large-batch training step selects.  0 (the default): the real batch.
+extern int g_select_n;
+static inline int64_t select_n(const ym_conv_desc* d) { return g_select_n > 0 ? int64_t(g_select_n) : int64_t(d->n); }
+
+// the weight-gradient kernel instance ym_conv_wgrad runs for d (wgrad.hip; ym_conv_kernel dir 2)
+int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len);
+
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }

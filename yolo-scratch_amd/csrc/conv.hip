@@ -37,6 +37,8 @@
 #include "tile.h"
 
 namespace ym {
+int g_select_n = 0;
+
 namespace {
 
 constexpr int MODE_FWD = 0;
@@ -757,18 +759,34 @@ static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st
                                      : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
 }
 
-static int pick_and_launch(GemmArgs a, int mode, int max_blocks, hipStream_t st) {
+// nsel: the batch the tile choice is made for (select_n: the real batch unless a parity test pins the
+// selection of a larger one)
+static int pick_and_launch(GemmArgs a, int mode, int max_blocks, int64_t nsel, hipStream_t st) {
     const int os = a.ostep;
-    const int64_t Mc = int64_t(a.N) * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);
+    const int64_t Mc = nsel * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);
     const Tile t = pick_tile(Mc, os == 2 ? 4 : 1, a.Nout);
     return mode == MODE_FWD ? launch_tile<MODE_FWD>(a, t, max_blocks, st) : launch_tile<MODE_DGRAD>(a, t, max_blocks, st);
 }
 
-extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
-    // grid-x used for the stats partials by ym_conv_fwd (callers size the partial buffers with it)
-    const Tile t = pick_tile(M, 1, Cout);
+// rows of the BN statistics partials of the 2-stage implicit GEMM's forward: M output pixels, the tile
+// chosen for Msel of them
+static int gemm_stat_rows(int64_t M, int64_t Msel, int Cout) {
+    const Tile t = pick_tile(Msel, 1, Cout);
     const int mtiles = int((M + t.bm - 1) / t.bm);
     return grid_x(mtiles, (Cout + t.bn - 1) / t.bn, true, FWD_STAT_BLOCKS);
+}
+
+extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
+    // grid-x of the 2-stage implicit GEMM's statistics partials (the generic kernel only; the row count of
+    // any conv forward is ym_conv_fwd_stat_rows)
+    return gemm_stat_rows(M, M, Cout);
+}
+
+extern "C" int ym_conv_set_select_batch(int n) {
+    // kernel selection as if the batch held n images (0: the real batch); returns the previous setting
+    const int prev = g_select_n;
+    g_select_n = n > 0 ? n : 0;
+    return prev;
 }
 
 extern "C" int ym_conv_set_halo(int mode) {
@@ -814,6 +832,45 @@ extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
     return d && halo_plan(d, dgrad ? 1 : 0).ok ? 1 : 0;
 }
 
+extern "C" int ym_conv_kernel(const ym_conv_desc* d, int dir, char* name, int name_len) {
+    // the kernel instance a bias-free forward (dir 0), data gradient (1) or weight gradient (2) of this conv
+    // runs: an id (algo x 1000 + template instance; weight gradients 10000 + ...) and, when name is given,
+    // its name, e.g. "direct v3", "pipe 256x128", "wgrad3 s2 64x64 8x8 deep"
+    char buf[96];
+    int id = -1;
+    if (!d || dir < 0 || dir > 2) {
+        snprintf(buf, sizeof buf, "invalid");
+    } else if (dir == 2) {
+        id = wgrad_kernel(d, buf, sizeof buf);
+    } else {
+        const DirectPlan dp = direct_plan(d, dir);
+        const HPipePlan hq = hpipe_plan(d, dir);
+        const PipePlan pp = pipe_plan(d, dir);
+        const HaloPlan hp = halo_plan(d, dir);
+        if (dp.ok) {
+            id = 3000 + dp.variant;
+            snprintf(buf, sizeof buf, "direct v%d", dp.variant);
+        } else if (hq.ok) {
+            id = 4000 + hq.cfg;
+            snprintf(buf, sizeof buf, "hpipe %s", hq.cfg == 0 ? "16x16px x 128" : hq.cfg == 1 ? "16x16px x 64" : "16x16px x 64 wres");
+        } else if (pp.ok) {
+            id = 2000 + pp.cfg;
+            snprintf(buf, sizeof buf, "pipe %s", pp.cfg == 0 ? "256x128" : "256x64");
+        } else if (hp.ok) {
+            id = 1000 + 100 * hp.cfg + std::min(hp.TW, 99);
+            snprintf(buf, sizeof buf, "halo %s %dx%d", hp.cfg == 0 ? "C8" : "C4", hp.TH, hp.TW);
+        } else {
+            const int os = dir ? d->stride : 1;
+            const int OH = dir ? d->h : d->oh, OW = dir ? d->w : d->ow, nout = dir ? d->cin : d->cout;
+            const Tile t = pick_tile(select_n(d) * ((OH + os - 1) / os) * ((OW + os - 1) / os), os == 2 ? 4 : 1, nout);
+            id = t.bn;
+            snprintf(buf, sizeof buf, "gemm %dx%d%s", t.bm, t.bn, os == 2 ? " 4-class" : "");
+        }
+    }
+    if (name && name_len > 0) snprintf(name, size_t(name_len), "%s", buf);
+    return id;
+}
+
 extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     // rows of the BN statistics partials ym_conv_fwd writes for this conv (halo or implicit-GEMM grid)
     if (!d) return 0;
@@ -825,7 +882,7 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     if (pp.ok) return pp.rows;
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) return hp.gx;
-    return ym_conv_stat_blocks(int64_t(d->n) * d->oh * d->ow, d->cout);
+    return gemm_stat_rows(int64_t(d->n) * d->oh * d->ow, select_n(d) * d->oh * d->ow, d->cout);
 }
 
 static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
@@ -836,6 +893,9 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     YM_CHECK_ARG(d->x_ld % 8 == 0 && d->x_bs % 8 == 0, "ym_conv_fwd: input view not 16-byte aligned");
     YM_CHECK_ARG(d->out_f32 == 1 || (d->y_ld % 4 == 0 && d->y_bs % 4 == 0), "ym_conv_fwd: output view not 8-byte aligned");
     YM_CHECK_ARG((stat_sum == nullptr) == (stat_sq == nullptr), "ym_conv_fwd: stats pointers");
+    // the statistics row count (ym_conv_fwd_stat_rows) describes the bias-free forward of a Conv block
+    YM_CHECK_ARG(!(bias && stat_sum), "ym_conv_fwd: BN statistics of a conv with bias are not supported");
+    YM_CHECK_ARG(!(d->accumulate && d->out_f32 == 2), "ym_conv_fwd: accumulate into an fp16 output is not supported");
     GemmArgs a{};
     a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
     a.w = w;
@@ -850,14 +910,15 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     a.ostep = 1;
     a.ep_lds = 0;                 // forward: fragment stores (the LDS-transposed epilogue measured equal)
     if (a.M == 0) return YM_OK;
-    const DirectPlan dp = direct_plan(d, 0);
+    // the direct and halo-pipelined kernels have no bias term: a conv with bias takes the kernels below
+    const DirectPlan dp = bias ? DirectPlan{} : direct_plan(d, 0);
     if (dp.ok) {
         direct_launch(dp, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (direct)");
         return YM_OK;
     }
     YM_CHECK_ARG(a.M < (int64_t(1) << 31), "ym_conv_fwd: too many pixels");
-    const HPipePlan hq = hpipe_plan(d, 0);
+    const HPipePlan hq = bias ? HPipePlan{} : hpipe_plan(d, 0);
     if (hq.ok) {
         hpipe_launch(hq, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (hpipe)");
@@ -876,7 +937,7 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
-    pick_and_launch(a, MODE_FWD, FWD_STAT_BLOCKS, as_stream(stream));
+    pick_and_launch(a, MODE_FWD, FWD_STAT_BLOCKS, select_n(d), as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
 }
@@ -936,7 +997,7 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
         YM_LAUNCH_CHECK("ym_conv_dgrad (halo)");
         return YM_OK;
     }
-    pick_and_launch(a, MODE_DGRAD, 4096, as_stream(stream));
+    pick_and_launch(a, MODE_DGRAD, 4096, select_n(d), as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_dgrad");
     return YM_OK;
 }

@@ -18,6 +18,7 @@
 // index formula), stride 2 over 2x2-pixel quads (all four output-parity classes of a dz pixel's
 // neighbourhood in one task, conv_direct_quad_kernel).
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -447,20 +448,24 @@ const Variant kVariants[] = {
 
 int direct_mode() { return g_direct_force >= 0 ? g_direct_force : 1; }
 
-// workgroups of variant i the whole chip holds at once (CUs x the kernel's occupancy), cached per variant
+// workgroups of variant i the whole chip holds at once (CUs x the kernel's occupancy), cached per device and
+// variant; the cache entries are atomics, so concurrent planners at worst compute the same value twice
+constexpr int kMaxDev = 64;
 int resident_blocks(int i) {
-    static int cache[16] = {0};
-    if (cache[i] == 0) {
-        int dev = 0, cus = 256, per = 1;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
-            cus = 256;
+    static std::atomic<int> cache[kMaxDev][16];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+    int v = cache[dev][i].load(std::memory_order_relaxed);
+    if (v == 0) {
+        int cus = 256, per = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(kVariants[i].fn), 256, 0) !=
                 hipSuccess || per < 1)
             per = 1;
-        cache[i] = std::max(8, (cus * per) & ~7);
+        v = std::max(8, (cus * per) & ~7);
+        cache[dev][i].store(v, std::memory_order_relaxed);
     }
-    return cache[i];
+    return v;
 }
 
 }  // namespace
@@ -481,7 +486,7 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
     if (int64_t(d->n) * in_bs * 2 >= (int64_t(1) << 31) || int64_t(d->n) * out_bs * 2 >= (int64_t(1) << 31)) return p;
     // high-resolution maps only (where the implicit GEMMs are latency-bound): >= 1 M output pixels
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
-    const int64_t M = int64_t(d->n) * OH * OW;
+    const int64_t M = select_n(d) * OH * OW;
     if (mode == 1 && M < (int64_t(1) << 20)) return p;
     for (int i = 0; i < int(sizeof(kVariants) / sizeof(kVariants[0])); ++i) {
         const Variant& v = kVariants[i];

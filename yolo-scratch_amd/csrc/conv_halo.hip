@@ -412,7 +412,8 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
         const int RT = (OH + TH - 1) / TH, CT = (OW + TW - 1) / TW;
         const int64_t tiles = int64_t(d->n) * RT * CT;
         const int nco = (cout + cf.bn - 1) / cf.bn;
-        if (c == 0 && (tiles * nco < 256 || cout <= 64)) continue;   // 128-channel tiles need >= 65 channels
+        const int64_t sel_tiles = select_n(d) * RT * CT;
+        if (c == 0 && (sel_tiles * nco < 256 || cout <= 64)) continue;   // 128-channel tiles need >= 65 channels
         if (tiles >= (int64_t(1) << 30)) continue;
         p.ok = 1;
         p.cfg = c;

@@ -430,7 +430,7 @@ HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad) {
     p.cfg = nout >= 128 ? 0 : (wres ? 2 : 1);
     const int bn = p.cfg == 0 ? 128 : 64;
     const int ntiles = (nout + bn - 1) / bn;
-    const int64_t tiles = int64_t(d->n) * (d->h / TS) * (d->w / TS);
+    const int64_t tiles = select_n(d) * (d->h / TS) * (d->w / TS);
     if (mode == 1 && tiles * ntiles < 512) return p;          // several tiles per CU (tail imbalance)
     int grid = 256;
     const int unit = 8 * ntiles;

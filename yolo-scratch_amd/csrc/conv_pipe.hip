@@ -570,7 +570,7 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
     // split_pix: in-image pixel indices as exact floats, row estimates within one of the truth
     if (int64_t(OH) * OW >= (int64_t(1) << 24) || OH >= (1 << 16)) return p;
-    const int64_t M = int64_t(d->n) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
+    const int64_t M = select_n(d) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
     p.cfg = nout >= 128 ? 0 : 1;
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
     const int ntiles = (nout + bn - 1) / bn;

@@ -580,6 +580,22 @@ WgPlan wg_plan(const ym_conv_desc* d) {
 }
 
 }  // namespace
+
+int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len) {
+    const WgPlan p = wg_plan(d);
+    if (p.kind == 3) {
+        const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);
+        snprintf(name, len, "wgrad3 s%d %dx%d %dx%d%s", d->stride, p.T, p.T2, p.tw, p.th, p.deep ? " deep" : "");
+        return 13000 + (d->stride == 2 ? 500 : 0) + 100 * tc + (p.tw == 20 ? 10 : p.tw == 10 ? 20 : 0) + (p.deep ? 1 : 0);
+    }
+    if (p.kind == 1) {
+        snprintf(name, len, "wgrad1 %d", p.T);
+        return 11000 + p.T;
+    }
+    snprintf(name, len, "wgrad generic %d", p.T);
+    return 10000 + p.T;
+}
+
 }  // namespace ym
 
 using namespace ym;

@@ -56,6 +56,8 @@ SIGNATURES = {
     "ym_conv_stat_blocks": (R, [I64, INT]),
     "ym_conv_fwd_stat_rows": (R, [P]),
     "ym_conv_algo": (R, [P, INT]),
+    "ym_conv_kernel": (R, [P, INT, P, INT]),
+    "ym_conv_set_select_batch": (R, [INT]),
     "ym_conv_set_halo": (R, [INT]),
     "ym_conv_set_pipe": (R, [INT]),
     "ym_conv_set_direct": (R, [INT]),

@@ -84,6 +84,7 @@ class Buckets:
         self.handles = []
         self.remaining = []
         self.streams = None        # callable -> the producing plan's streams (yolomi.graph.Plan.comm_streams)
+        self.comm = None           # the stream the bucket collectives are issued from (created on first use)
 
     def _close(self, start, size, members):
         b = len(self.ranges)
@@ -96,25 +97,39 @@ class Buckets:
         self.remaining = [len(m) for m in self.members]
         self.launched = [False] * len(self.ranges)
         self.handles = []
+        self.writes = [{} for _ in self.ranges]      # bucket -> {stream: event after its last write there}
 
-    def ready(self, params):
+    def ready(self, params, writes=None):
+        """params: parameters whose gradients an op has finished; writes: the (stream, event) pairs
+        recorded right after that op's gradient-writing launches (yolomi.graph.Plan.note_grad_write)."""
         for p in params:
             b = self.bucket_of.get(id(p))
             if b is None:
                 continue
+            for st, ev in writes or ():
+                self.writes[b][st] = ev           # later writes on a stream supersede earlier ones
             self.remaining[b] -= 1
             if self.remaining[b] == 0:
                 self._launch(b)
 
     def _launch(self, b):
         s, e = self.ranges[b]
+        writes = self.writes[b] if getattr(self, "writes", None) else {}
         streams = self.streams() if self.streams else []
-        if len(streams) <= 1:
+        if writes:
+            # the collective waits for exactly the launches that wrote this bucket (the BN finalizes on
+            # the scheduler's streams, the weight gradients on the side stream), on a stream of its own:
+            # neither it nor the backward's streams wait for the other's unrelated work
+            if self.comm is None:
+                self.comm = torch.cuda.Stream(device=self.flat.device)
+            for ev in writes.values():
+                self.comm.wait_event(ev)
+            with torch.cuda.stream(self.comm):
+                self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+        elif len(streams) <= 1:
             self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
         else:
-            # the bucket's gradients come from several streams (BN backward on the scheduler's
-            # streams, weight gradients on the side stream): the collective is issued from the last
-            # of them after it has caught up with the others, so RCCL orders it after all writers
+            # writers unknown: issue from the last stream after it has caught up with all the others
             comm = streams[-1]
             for o in streams[:-1]:
                 comm.wait_stream(o)
@@ -125,6 +140,7 @@ class Buckets:
     def finish(self, world: int):
         for b in range(len(self.ranges)):        # parameters no op reported (none in a full plan)
             if not self.launched[b]:
+                self.writes[b] = {}
                 self._launch(b)
         for h in self.handles:
             h.wait()
@@ -156,14 +172,20 @@ class GradSync:
         b.streams = getattr(plan, "comm_streams", None)
         self.buckets[id(plan)] = b
 
-        def hook(params, _b=b):
+        def hook(params, writes=None, _b=b, _plan=plan):
+            if getattr(_plan, "pooled", False):
+                return                    # reduced after the backwards (sync), not bucket by bucket
             if not _b.remaining:
                 _b.begin()
-            _b.ready(params)
+            _b.ready(params, writes)
         plan.grad_hook = hook
 
     def sync(self):
         plan = self.model.__dict__.get("_ym_last_plan")
+        if plan is not None and getattr(plan, "pooled", False):
+            # several forwards were in flight before the backward (yolomi.graph.run_model): their plans'
+            # gradients were added together into .grad, which is reduced below as one buffer
+            plan = None
         if plan is not None:
             b = self.buckets.get(id(plan))
             if b is not None and b.remaining:

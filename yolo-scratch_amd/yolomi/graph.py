@@ -19,6 +19,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import weakref
 
 import numpy as np
 import torch
@@ -310,6 +311,7 @@ class ConvBN:
                 call("ym_bn_bwd_apply", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
                      mu, rs, self.act, self.coef.data_ptr(), self.z.data_ptr(), st)
         self._timed(plan, "bn", plan._cur_stream, run, work)
+        plan.note_grad_write(plan._cur_stream)          # dgamma / dbeta (finalize) are in the stream now
         if r is not None:
             r.mark()
 
@@ -323,6 +325,7 @@ class ConvBN:
         self._timed(plan, "wgrad", plan.side_stream or plan._cur_stream, lambda: call(
             "ym_conv_wgrad", ctypes.byref(self.desc), dz.data_ptr(), self.x.ptr(), ws.data_ptr(), ws.numel() * 4,
             plan.gptr(self.m.conv.weight), 0, sst))
+        plan.note_grad_write(plan.side_stream or plan._cur_stream)
         # data gradient
         if plan.needs_grad(self.x):
             acc = self.x.grad_for_write(st)
@@ -680,6 +683,7 @@ class Plan:
         self.dhead = None
         self._scratch = []
         self.grad_hook = None      # called with each op's finished parameters during backward (DP buckets)
+        self._writes = []          # (stream, event) after each parameter-gradient write of the current op
         self.side_stream = None    # weight-gradient stream (see side())
         self._cur_stream = None    # torch stream the current op is issued on (scheduler)
         # flat parameter-gradient buffer; each .grad is a view of it
@@ -717,6 +721,32 @@ class Plan:
             ev = evs[src.cuda_stream] = torch.cuda.Event()
         ev.record(src)
         dst.wait_event(ev)
+
+    def note_grad_write(self, stream):
+        """Under DP (a grad hook is set): record an event on `stream` right after a launch that wrote
+        parameter gradients of the current op, so the bucket holding them waits for exactly that launch
+        and not for the later, unrelated work of the same stream (the op's data gradient).  One
+        persistent event per (op position, write), re-recorded every step."""
+        if self.grad_hook is None or stream is None:
+            return
+        evs = self.__dict__.setdefault("_wevents", {})
+        key = (self._op_pos, len(self._writes))
+        ev = evs.get(key)
+        if ev is None:
+            ev = evs[key] = torch.cuda.Event()
+        ev.record(stream)
+        self._writes.append((stream, ev))
+
+    def take_grad_writes(self, op):
+        """The (stream, event) writes the op just noted; an op that noted none (the few that do not
+        instrument their launches) is covered by its stream's and the side stream's tails."""
+        w, self._writes = self._writes, []
+        if not w and self.grad_hook is not None and self.dev.type == "cuda":
+            for st in (self._cur_stream, self.side_stream):
+                if st is not None:
+                    self.note_grad_write(st)
+            w, self._writes = self._writes, []
+        return w
 
     def _begin_side(self):
         use = self.dev.type == "cuda" and os.environ.get("YM_SIDE_STREAM", "1") != "0"
@@ -855,7 +885,8 @@ class Plan:
             self._cur = 0
             self._active_streams = [torch.cuda.current_stream(self.dev)]
             self._cur_stream = self._active_streams[0]
-            for op in ops:
+            for i, op in enumerate(ops):
+                self._op_pos = i
                 getattr(op, phase == "fwd" and "forward" or "backward")(self, st)
                 if after is not None:
                     after(op)
@@ -887,6 +918,7 @@ class Plan:
                 else:
                     s.wait_event(evs[j])
             self._cur, self._cur_stream = k, s
+            self._op_pos = i
             if fwd:
                 op.forward(self, ptrs[k])
             else:
@@ -993,20 +1025,36 @@ class Plan:
     def _backward_ops(self, ops):
         for a in self.acts:
             a.written[:] = False
+        # gradient accumulation without zero_grad(): the parameters' .grad still alias this plan's flat
+        # buffer (install_grads) and hold the previous backward's sum, which the zero fill below would
+        # drop — keep it and add it back after this backward (single-process; under DP the buffer is
+        # on the wire during the backward, and the reference's loop zeroes its gradients every step)
+        keep = None
+        if self.grad_hook is None and self.params:
+            p0 = self.params[0]
+            if p0.grad is not None and p0.grad.data_ptr() == self.grad_views[id(p0)].data_ptr():
+                keep = self.grad_flat.clone()
         self.grad_flat.zero_()
         for t in self._scratch:
             t.zero_()
         hook = None if self._graph_ok() else self.grad_hook
         self._begin_side()
-        self._run(list(reversed(ops)), "bwd", (lambda op: hook(op_params(op))) if hook is not None else None)
+        self._writes = []
+        self._run(list(reversed(ops)), "bwd",
+                  (lambda op: hook(op_params(op), self.take_grad_writes(op))) if hook is not None else None)
         self._join_side()
+        if keep is not None:
+            self.grad_flat.add_(keep)
 
-    # --------------------------------------------------------------- single-in-flight contract
-    # A plan owns ONE set of activation buffers per input shape: a second forward of the same shape
-    # overwrites what the first one's backward needs.  Each forward takes a generation number and the
-    # backward refuses to run on a plan that has since run a newer forward (the reference's autograd
-    # graph would keep both sets alive; this path keeps one and says so instead of returning wrong
-    # gradients).
+    # --------------------------------------------------------------- forwards in flight
+    # A plan owns ONE set of activation buffers.  While a training forward's autograd graph is alive
+    # and its backward has not run, the plan is "pending" (a weak reference to the graph node); the
+    # next forward of the same shape then takes another plan of the model's pool for that shape (its
+    # own activation set, the same parameters), as the reference's autograd keeps one set of saved
+    # tensors per forward (train_yolo11_cuda.py:51-57).  A plan is reused once its backward has run or
+    # its graph has been freed.  The generation check stays as a guard: a backward whose plan has since
+    # run another forward raises instead of returning wrong gradients, and so does a second backward
+    # through one forward (the backward overwrites z with dz in place).
     def new_generation(self):
         self.gen = getattr(self, "gen", 0) + 1
         return self.gen
@@ -1015,6 +1063,14 @@ class Plan:
         if gen != getattr(self, "gen", 0):
             raise YolomiError("backward of a forward whose activations a newer forward of the same input shape has "
                               "overwritten: run backward (or detach the outputs) before the next forward")
+
+    def set_pending(self, ctx):
+        self._pending = weakref.ref(ctx) if ctx is not None else None
+
+    @property
+    def pending(self):
+        r = self.__dict__.get("_pending")
+        return r is not None and r() is not None
 
     def install_grads(self):
         """Expose the flat buffer as parameter .grad (accumulating if a grad already exists)."""
@@ -1227,12 +1283,18 @@ class _ModelFn(torch.autograd.Function):
         plan.img = img.contiguous()
         plan.forward()
         ctx.plan, ctx.gen = plan, plan.new_generation()
+        plan.set_pending(ctx)
         return plan.head.detach()
 
     @staticmethod
     def backward(ctx, dhead):
         plan = ctx.plan
         plan.check_generation(ctx.gen)
+        if getattr(ctx, "done", False):
+            raise YolomiError("a second backward through one forward (retain_graph=True): the first backward "
+                              "consumed the forward's activations in place; run the forward again")
+        ctx.done = True
+        plan.set_pending(None)
         plan.dhead = dhead.contiguous()
         plan.backward()
         plan.install_grads()
@@ -1381,13 +1443,20 @@ def run_model(model, img: torch.Tensor):
         raise YolomiError(f"stem kernel supports ch=1 input (got {C})")
     key = ("model", B, H, W, model.training)
     cache = model.__dict__.setdefault("_ym_plans", {})
-    plan = cache.get(key)
+    pool = cache.setdefault(key, [])
+    # the first plan of this shape whose activations no pending backward still needs (see Plan.pending)
+    plan = next((p for p in pool if not p.pending), None)
     if plan is None:
         plan = Plan(model, B, H, W, img.device, model.training)
         plan.input_requires_grad = False
         plan.is_model = True
         lower_model(plan, model, (B, H, W))
-        cache[key] = plan
+        pool.append(plan)
+        if len(pool) > 1:
+            # several forwards in flight: their gradients meet in .grad (install_grads adds), so data
+            # parallelism all-reduces .grad after the backwards instead of each plan's buffer during its own
+            for p_ in pool:
+                p_.pooled = True
     if model.training:
         model.__dict__["_ym_last_plan"] = plan
     anchor = model.__dict__.setdefault("_ym_anchor", torch.zeros(1, device=img.device, requires_grad=True))
