@@ -168,7 +168,10 @@ def test_two_forwards_before_one_backward():
     e1, e2 = err(single[0], gl), err(single[1], g2)
     e12 = err(both, [a + b for a, b in zip(gl, g2)])
     print(f"gradient rel L2 vs oracle: single {e1:.2e} / {e2:.2e}, two in flight {e12:.2e}")
-    assert e12 <= 1.5 * max(e1, e2) + 1e-3 and e12 < 5e-2, (e1, e2, e12)
+    # whole-network gradients of a 16-bit path differ from the fp32 oracle by up to ~0.1-0.25 (backbone BN
+    # parameters behind SPPF's max routing; test_gpu_network.py's cap is 0.3): the summed loss must
+    # be as close as the single forwards are
+    assert e12 <= 1.5 * max(e1, e2) + 1e-3 and e12 < 0.3, (e1, e2, e12)
     # a second backward through one forward: refused (the first consumed z in place)
     l3, _ = crit(m(b1["img"]), b1)
     l3.backward(retain_graph=True)

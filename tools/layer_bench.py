@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", type=int, nargs="*", help="plan op indices to time (default: every ConvBN)")
     ap.add_argument("--hpipe", type=int, default=-1, help="ym_conv_set_hpipe policy for this run (A/B)")
+    ap.add_argument("--pipe", type=int, default=-1, help="ym_conv_set_pipe policy for this run (A/B)")
+    ap.add_argument("--halo", type=int, default=-1, help="ym_conv_set_halo policy for this run (A/B)")
+    ap.add_argument("--direct", type=int, default=-1, help="ym_conv_set_direct policy for this run (A/B)")
+    ap.add_argument("--names", action="store_true", help="append each launch's kernel instance (ym_conv_kernel)")
     ap.add_argument("--seq-out", help="counter-pass mode: write the (op, kind, k, flops, launches) order of the "
                                       "timed groups here and separate the groups with a marker kernel "
                                       "(tools/pmc_layers.py splits a rocprofv3 --pmc pass on the markers)")
@@ -38,6 +42,9 @@ def main():
 
     from yolomi._lib import lib
     lib().ym_conv_set_hpipe(args.hpipe)
+    lib().ym_conv_set_pipe(args.pipe)
+    lib().ym_conv_set_halo(args.halo)
+    lib().ym_conv_set_direct(args.direct)
     dev = torch.device("cuda", 0)
     cfg = yaml.safe_load((ROOT / "yolo-scratch_amd" / "configs" / "yolo11n_crater.yaml").read_text())
     cfg["scale"] = args.scale
@@ -102,13 +109,20 @@ def main():
         for m, b in zip(ms, byts):
             t_floor = max(fl / 2.5e15, b / 8e12)
             frac.append(t_floor / (m * 1e-3) if m > 0 else 0.0)
+        names = []
+        if args.names:
+            for dr in range(3):
+                b_ = ctypes.create_string_buffer(96)
+                lib().ym_conv_kernel(ctypes.byref(d), dr, b_, 96)
+                names.append(b_.value.decode())
         rows.append((i, d.cin, d.cout, d.k, d.stride, d.oh, d.ow, fl / 1e9, ms, tf, frac,
-                     "hbm" if byts[0] / 8e12 > fl / 2.5e15 else "mfma"))
+                     "hbm" if byts[0] / 8e12 > fl / 2.5e15 else "mfma", names))
     print(f"{'op':>4} {'cin':>4} {'cout':>4} k s {'out':>7} {'GFLOP':>7} roof | {'fwd ms':>7} {'TF/s':>5} {'frac':>5} | "
           f"{'dgrad':>7} {'TF/s':>5} {'frac':>5} | {'wgrad':>7} {'TF/s':>5} {'frac':>5}")
-    for i, ci, co, k, s, oh, ow, gf, ms, tf, fr, roof in rows:
+    for i, ci, co, k, s, oh, ow, gf, ms, tf, fr, roof, names in rows:
         print(f"{i:4d} {ci:4d} {co:4d} {k} {s} {oh:3d}x{ow:<3d} {gf:7.1f} {roof:>4} | {ms[0]:7.3f} {tf[0]:5.0f} {fr[0]:5.2f} | "
-              f"{ms[1]:7.3f} {tf[1]:5.0f} {fr[1]:5.2f} | {ms[2]:7.3f} {tf[2]:5.0f} {fr[2]:5.2f}")
+              f"{ms[1]:7.3f} {tf[1]:5.0f} {fr[1]:5.2f} | {ms[2]:7.3f} {tf[2]:5.0f} {fr[2]:5.2f}" +
+              ("".join(f" | {n}" for n in names) if names else ""))
     print(f"total ms: fwd {tot[0]:.3f}  dgrad {tot[1]:.3f}  wgrad {tot[2]:.3f}")
     if args.seq_out:
         import json

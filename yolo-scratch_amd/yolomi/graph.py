@@ -684,6 +684,7 @@ class Plan:
         self._scratch = []
         self.grad_hook = None      # called with each op's finished parameters during backward (DP buckets)
         self._writes = []          # (stream, event) after each parameter-gradient write of the current op
+        self.on_op = None          # tools: called with (op index, op, phase) before each op runs (launch maps)
         self.side_stream = None    # weight-gradient stream (see side())
         self._cur_stream = None    # torch stream the current op is issued on (scheduler)
         # flat parameter-gradient buffer; each .grad is a view of it
@@ -887,6 +888,8 @@ class Plan:
             self._cur_stream = self._active_streams[0]
             for i, op in enumerate(ops):
                 self._op_pos = i
+                if self.on_op is not None:
+                    self.on_op(i, op, phase)
                 getattr(op, phase == "fwd" and "forward" or "backward")(self, st)
                 if after is not None:
                     after(op)
@@ -919,6 +922,8 @@ class Plan:
                     s.wait_event(evs[j])
             self._cur, self._cur_stream = k, s
             self._op_pos = i
+            if self.on_op is not None:
+                self.on_op(i, op, phase)
             if fwd:
                 op.forward(self, ptrs[k])
             else:
