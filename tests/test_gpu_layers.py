@@ -335,6 +335,6 @@ def test_teacher_forced_every_layer(scale, imgsz, bs, select):
     if select == 64:
         # the instances the bs64 plan is known to run must be among them
         fams = {n.split(" ")[0] for n in names}
-        assert {"direct", "hpipe", "pipe", "halo", "wgrad3", "wgrad1"} <= fams, fams
+        assert {"direct", "hpipe", "pipe", "halo", "gemm", "wgrad3", "wgrad1"} <= fams, fams
     kinds = {w.split(" ")[0].split(":")[1] for _, w, _ in R.rows}
     assert any("model.0" in k for k in kinds)                   # the stem was checked

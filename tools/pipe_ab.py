@@ -51,6 +51,10 @@ def main():
             d = op.desc
             for v in args.variants:
                 setter(v)
+                # the variant's own statistics rows: a selection setter can move a layer to a kernel with a
+                # larger grid than the plan's buffers were sized for (ym_conv_fwd_stat_rows)
+                rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+                stats = torch.empty(2, max(rows, 1), d.cout, dtype=torch.float32, device=dev)
                 for kind in args.kinds:
                     if kind == "dgrad" and not plan.needs_grad(op.x):
                         continue
@@ -64,7 +68,7 @@ def main():
                             e0.record()
                         if kind == "fwd":
                             call("ym_conv_fwd", ctypes.byref(d), op.x.ptr(), op.wf.data_ptr(), op.z.data_ptr(), None,
-                                 op.ps[0].data_ptr(), op.ps[1].data_ptr(), st)
+                                 stats[0].data_ptr(), stats[1].data_ptr(), st)
                         elif kind == "dgrad":
                             call("ym_conv_dgrad", ctypes.byref(d), op.z.data_ptr(), op.wt.data_ptr(), op.x.gptr(), st)
                         else:

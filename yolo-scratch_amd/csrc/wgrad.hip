@@ -81,7 +81,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
 // rows — 20 x 3 — on the 20-wide maps, where 8x8 tiles cover 24x24 = 1.44x the pixels).  The units
 // of a split are staged through two register sets: while unit t is multiplied, the loads of units
 // t + 1 and t + 2 are in flight.
-template <int S, int TCO, int TCI, int WCO, int WCI, int TW, int TH, bool DEEP>
+// DB: two LDS buffers — the next unit is written into the other buffer while this one is multiplied, one
+// barrier per unit (single buffer: the store between two barriers, every wave off the MFMA pipe meanwhile).
+template <int S, int TCO, int TCI, int WCO, int WCI, int TW, int TH, bool DEEP, bool DB = false>
 __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(WgArgs a) {
     constexpr int NWC = TCI / WCI;            // waves along ci
     constexpr int NWV = (TCO / WCO) * NWC;
@@ -98,8 +100,9 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
     constexpr int HW = (TW - 1) * S + 3, HR = ((TH - 1) * S + 3) * HW;   // halo width / rows
     constexpr int XI = (HR + RPX - 1) / RPX;  // 16-B halo chunks per thread
     static_assert(TP <= 64, "wgrad3 unit");
-    __shared__ __attribute__((aligned(16))) char Dz[64 * RSD];
-    __shared__ __attribute__((aligned(16))) char Xh[HR * RSX];
+    constexpr int NB = DB ? 2 : 1;
+    __shared__ __attribute__((aligned(16))) char Dzb[NB][64 * RSD];
+    __shared__ __attribute__((aligned(16))) char Xhb[NB][HR * RSX];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wr = wave / NWC, wc = wave % NWC;
@@ -168,7 +171,9 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
             rx[it] = buf_load16(rxs, ok ? uint32_t(((ih * a.IW + iw) * int(a.x_ld) + ci0 + xsc * 8) * 2) : OOB);
         }
     };
-    auto store = [&](const uint4 (&rdz)[DI], const uint4 (&rx)[XI]) {
+    auto store = [&](int buf, const uint4 (&rdz)[DI], const uint4 (&rx)[XI]) {
+        char* Dz = Dzb[buf];
+        char* Xh = Xhb[buf];
 #pragma unroll
         for (int it = 0; it < DI; ++it)
             if (dsrow + RPD * it < 64) *reinterpret_cast<uint4*>(Dz + (dsrow + RPD * it) * RSD + dsc * 16) = rdz[it];
@@ -177,7 +182,9 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
             if (xsrow + RPX * it < HR)
                 *reinterpret_cast<uint4*>(Xh + (xsrow + RPX * it) * RSX + xsc * 16) = h8_to_bf8(rx[it]);
     };
-    auto compute = [&]() {
+    auto compute = [&](int buf) {
+        const char* Dz = Dzb[buf];
+        const char* Xh = Xhb[buf];
         int hl[2] = {hb_lo[0], hb_lo[1]}, hh[2] = {hb_hi[0], hb_hi[1]};
         asm volatile("" : "+v"(hl[0]), "+v"(hl[1]), "+v"(hh[0]), "+v"(hh[1]));
 #pragma unroll
@@ -209,26 +216,63 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
         }
     };
 
-    if constexpr (DEEP) {
+    if constexpr (DB && DEEP) {
+        // units in pairs over the two register sets and the two LDS buffers: unit t + 1 is written into the
+        // other buffer (its loads issued a unit ago) while unit t is multiplied, then unit t + 3's loads go out
+        if (t_begin < t_end) {
+            load(t_begin, da, xa);
+            load(t_begin + 1, db, xb);
+            store(0, da, xa);
+            __syncthreads();
+            load(t_begin + 2, da, xa);
+        }
+        for (int64_t t = t_begin; t < t_end; t += 2) {
+            compute(0);                       // unit t
+            store(1, db, xb);                 // unit t + 1 into the other buffer (read two barriers ago)
+            load(t + 3, db, xb);
+            __syncthreads();
+            compute(1);                       // unit t + 1
+            store(0, da, xa);                 // unit t + 2
+            load(t + 4, da, xa);
+            __syncthreads();
+        }
+    } else if constexpr (DB) {
+        if (t_begin < t_end) {
+            load(t_begin, da, xa);
+            store(0, da, xa);
+            __syncthreads();
+            load(t_begin + 1, da, xa);
+        }
+        int buf = 0;
+        for (int64_t t = t_begin; t < t_end; ++t) {
+            compute(buf);
+            if (t + 1 < t_end) {
+                store(buf ^ 1, da, xa);
+                load(t + 2, da, xa);
+            }
+            __syncthreads();
+            buf ^= 1;
+        }
+    } else if constexpr (DEEP) {
         // units go in pairs, one per register set (static indexing; a split with an odd count multiplies
         // one unit of zeros at its end): the loop has one exit, so the accumulators are not copied
         // between the two bodies' register assignments
         if (t_begin < t_end) {
             load(t_begin, da, xa);
             load(t_begin + 1, db, xb);
-            store(da, xa);
+            store(0, da, xa);
             __syncthreads();
             load(t_begin + 2, da, xa);
         }
         for (int64_t t = t_begin; t < t_end; t += 2) {
-            compute();                        // unit t (set a's, staged)
+            compute(0);                       // unit t (set a's, staged)
             __syncthreads();
-            store(db, xb);
+            store(0, db, xb);
             __syncthreads();
             load(t + 3, db, xb);
-            compute();                        // unit t + 1
+            compute(0);                       // unit t + 1
             __syncthreads();
-            store(da, xa);
+            store(0, da, xa);
             __syncthreads();
             load(t + 4, da, xa);
         }
@@ -236,15 +280,15 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
         // one register set: unit t + 1 in flight while unit t is multiplied
         if (t_begin < t_end) {
             load(t_begin, da, xa);
-            store(da, xa);
+            store(0, da, xa);
             __syncthreads();
             load(t_begin + 1, da, xa);
         }
         for (int64_t t = t_begin; t < t_end; ++t) {
-            compute();
+            compute(0);
             __syncthreads();
             if (t + 1 >= t_end) break;
-            store(da, xa);
+            store(0, da, xa);
             __syncthreads();
             load(t + 2, da, xa);
         }
@@ -585,8 +629,11 @@ int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len) {
     const WgPlan p = wg_plan(d);
     if (p.kind == 3) {
         const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);
-        snprintf(name, len, "wgrad3 s%d %dx%d %dx%d%s", d->stride, p.T, p.T2, p.tw, p.th, p.deep ? " deep" : "");
-        return 13000 + (d->stride == 2 ? 500 : 0) + 100 * tc + (p.tw == 20 ? 10 : p.tw == 10 ? 20 : 0) + (p.deep ? 1 : 0);
+        const bool db = d->stride == 1 || p.deep;        // two LDS buffers (ym_conv_wgrad)
+        snprintf(name, len, "wgrad3 s%d %dx%d %dx%d%s%s", d->stride, p.T, p.T2, p.tw, p.th, p.deep ? " deep" : "",
+                 db ? " db" : "");
+        return 13000 + (d->stride == 2 ? 500 : 0) + 100 * tc + (p.tw == 20 ? 10 : p.tw == 10 ? 20 : 0) + (p.deep ? 1 : 0) +
+               (db ? 2 : 0);
     }
     if (p.kind == 1) {
         snprintf(name, len, "wgrad1 %d", p.T);
@@ -641,23 +688,33 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
         YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
-#define WG3_LAUNCH(S_, D_)                                                                                        \
+#define WG3_LAUNCH(S_, D_, B_)                                                                                    \
         if (p.tw == 20) {                                                                                   \
-            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 20, 3, false>), grid, dim3(512), 0, st, a); \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 20, 3, false, B_>), grid, dim3(512), 0, st, a); \
         } else if (p.tw == 10) {                                                                            \
-            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 10, 6, false>), grid, dim3(512), 0, st, a); \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 10, 6, false, B_>), grid, dim3(512), 0, st, a); \
         } else {                                                                                            \
             switch (tc) {                                                                                   \
-                case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 8, 8, D_>), grid, dim3(512), 0, st, a); break; \
-                case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 64, 16, 16, 8, 8, D_>), grid, dim3(512), 0, st, a); break; \
-                case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 32, 32, 16, 8, 8, D_>), grid, dim3(256), 0, st, a); break; \
-                default: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 32, 16, 16, 8, 8, D_>), grid, dim3(256), 0, st, a); break; \
+                case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 8, 8, D_, B_>), grid, dim3(512), 0, st, a); break; \
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 64, 16, 16, 8, 8, D_, B_>), grid, dim3(512), 0, st, a); break; \
+                case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 32, 32, 16, 8, 8, D_, B_>), grid, dim3(256), 0, st, a); break; \
+                default: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 32, 16, 16, 8, 8, D_, B_>), grid, dim3(256), 0, st, a); break; \
             }                                                                                               \
         }
-        if (d->stride == 1) {
-            if (p.deep) { WG3_LAUNCH(1, true) } else { WG3_LAUNCH(1, false) }
+        // two LDS buffers on the stride-1 layers and the deep stride-2 ones (same-process A/B: -4..-10 % on the
+        // 80x80 / 160x160 layers, +3.5..+4.8 % on the narrow stride-2 maps; profiles/r04/wgrad3_db_ab.txt)
+        if (d->stride == 1 || p.deep) {
+            if (d->stride == 1) {
+                if (p.deep) { WG3_LAUNCH(1, true, true) } else { WG3_LAUNCH(1, false, true) }
+            } else {
+                if (p.deep) { WG3_LAUNCH(2, true, true) } else { WG3_LAUNCH(2, false, true) }
+            }
         } else {
-            if (p.deep) { WG3_LAUNCH(2, true) } else { WG3_LAUNCH(2, false) }
+            if (d->stride == 1) {
+                if (p.deep) { WG3_LAUNCH(1, true, false) } else { WG3_LAUNCH(1, false, false) }
+            } else {
+                if (p.deep) { WG3_LAUNCH(2, true, false) } else { WG3_LAUNCH(2, false, false) }
+            }
         }
 #undef WG3_LAUNCH
     } else if (p.kind == 1) {
