@@ -104,7 +104,7 @@ def host_cpus():
     return usable, {"nproc": n, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
-def cpu_baseline(batch: int = 4, imgsz: int = 640, warmup: int = 2, steps: int = 3):
+def cpu_baseline(batch: int = 16, imgsz: int = 640, warmup: int = 1, steps: int = 3):
     """Oracle (fp32 CPU restatement of the reference) train step on a bounded sample, on every usable
     host CPU (SURVEY §8(d) CPU-baseline plan: torch.set_num_threads(os.cpu_count()), nproc and the CPU
     model stated)."""

@@ -171,7 +171,7 @@ int ym_conv_set_pipe(int mode);
 int ym_conv_set_direct(int mode);
 /* Selection policy of the halo-staged pipelined 3x3 stride-1 kernel (conv_hpipe.hip: 16x16-pixel tiles,
  * each 64-channel chunk of the 18x18 input halo staged once for all nine taps): -1 default, 0 never,
- * 1 eligible layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
+ * 1 the weight-resident 64 -> 64 layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
 int ym_conv_set_hpipe(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block
  * channel sum / sum-of-squares partials [ym_conv_fwd_stat_rows(d)][cout] for training BatchNorm

@@ -232,9 +232,9 @@ def test_hpipe_kernel_vs_torch(shape):
 
 
 def test_hpipe_selection():
-    """By default the halo-pipelined kernel takes the 3x3 stride-1 convs on 16-multiple maps with >= 512 tiles
-    (the 80x80 / 160x160 layers at bs64) and >= 128 output channels or 64 -> 64 (weights resident), in either
-    direction; never stride 2 or other maps."""
+    """By default the halo-pipelined kernel takes the 64 -> 64 3x3 stride-1 convs (weights resident in LDS) on
+    16-multiple maps with >= 512 tiles (the 80x80 / 160x160 layers at bs64), in either direction; the >= 128-
+    output-channel layers run the pipelined implicit GEMM (faster since round 4); never stride 2 or other maps."""
     from yolomi._lib import lib
 
     def desc(*shape):
@@ -242,9 +242,9 @@ def test_hpipe_selection():
         d.out_f32 = 2                    # a Conv block's fp16 z
         return d
     d = desc(64, 80, 80, 128, 128, 3, 1, 1)
-    assert lib().ym_conv_algo(ctypes.byref(d), 0) == 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
-    d = desc(64, 80, 80, 128, 64, 3, 1, 1)          # 64 output channels: forward elsewhere, dgrad (128) here
-    assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) == 2 and lib().ym_conv_algo(ctypes.byref(d), 1) == 2
+    d = desc(64, 80, 80, 128, 64, 3, 1, 1)
+    assert lib().ym_conv_algo(ctypes.byref(d), 0) != 4 and lib().ym_conv_algo(ctypes.byref(d), 1) != 4
     d = desc(64, 80, 80, 64, 64, 3, 1, 1)
     assert lib().ym_conv_algo(ctypes.byref(d), 0) == 4 and lib().ym_conv_algo(ctypes.byref(d), 1) == 4
     for shape in [(64, 40, 40, 128, 128, 3, 1, 1), (64, 160, 160, 64, 64, 3, 2, 1), (2, 80, 80, 128, 128, 3, 1, 1),

@@ -12,7 +12,7 @@ struct HPipePlan {
     int rows;        // rows of the BN statistics partials (= grid / channel tiles)
 };
 
-// selection policy (ym_conv_set_hpipe): -1 default (1); 0 never; 1 eligible layers with >= 512 tiles;
+// selection policy (ym_conv_set_hpipe): -1 default (1); 0 never; 1 the weight-resident 64 -> 64 layers with >= 512 tiles;
 // 2 every eligible layer
 extern int g_hpipe_force;
 

@@ -432,6 +432,11 @@ HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad) {
     const int ntiles = (nout + bn - 1) / bn;
     const int64_t tiles = select_n(d) * (d->h / TS) * (d->w / TS);
     if (mode == 1 && tiles * ntiles < 512) return p;          // several tiles per CU (tail imbalance)
+    // default: the weight-resident 64 -> 64 tile only — since round 4 the pipelined implicit GEMM (conv_pipe.hip)
+    // runs the >= 128-output-channel 80x80 layers 9-12 % faster than the 128-channel halo tile (same-process
+    // A/B, profiles/r04/hpipe_vs_pipe_ab.txt; round 3 measured the opposite before conv_pipe's 16-wave rework);
+    // policy 2 still runs every eligible configuration (parity tests)
+    if (mode == 1 && p.cfg != 2) return p;
     int grid = 256;
     const int unit = 8 * ntiles;
     grid = (grid / unit) * unit;

@@ -22,6 +22,11 @@ import torch
 import torch.distributed as dist
 
 
+# tools/dp_trace.sh: one tiny marker kernel on the comm stream where each bucket's collective is enqueued, so a
+# kernel trace shows when the buckets go out against the backward's kernels
+_MARK = os.environ.get("YM_DP_MARK") == "1"
+
+
 @dataclass
 class DPContext:
     rank: int
@@ -125,6 +130,8 @@ class Buckets:
             for ev in writes.values():
                 self.comm.wait_event(ev)
             with torch.cuda.stream(self.comm):
+                if _MARK:
+                    torch.cuda._sleep(64)         # a marker kernel on the comm stream (tools/dp_trace.sh)
                 self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
         elif len(streams) <= 1:
             self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
