@@ -38,6 +38,10 @@ def conv_kind(name):
         return "fwd" if t[6] == "0" else "dgrad"
     if n.startswith("conv_direct_kernel<"):         # <NT,KC,KS,S,MODE,TP>
         return "fwd" if t[4] == "0" else "dgrad"
+    if n.startswith("conv_direct_quad_kernel<"):    # stride-2 data gradient over 2x2-pixel quads
+        return "dgrad"
+    if n.startswith("conv_hpipe_kernel<"):          # <BN,WM,WN,MODE,WRES>
+        return "fwd" if t[3] == "0" else "dgrad"
     if n.startswith(("wgrad3_kernel", "wgrad1_kernel", "wgrad_generic_kernel", "wgrad_reduce_kernel")):
         return "wgrad"
     if n.startswith(("bn_apply_kernel", "bn_bwd_reduce_kernel", "bn_bwd_apply_kernel", "bn_finalize_fused_kernel",

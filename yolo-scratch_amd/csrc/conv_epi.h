@@ -86,17 +86,19 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
 // fr): one 16-B store per lane and channel subtile, 32 pixels x 32 B per instruction, TM * TN / 2 stores per lane.
 // No LDS: an LDS transpose makes hipcc drain every in-flight LDS-DMA stage (vmcnt(0)) in front of it.
 // pix_off(q) as above (byte offset of wave-local pixel q's channel wch0, OOB outside); nout % 8 == 0.
-template <int TM, int TN, class PixOff>
+// pix_ok(q): pixel q of the wave lies inside the output (the statistics' mask; a compare, where pix_off also
+// decomposes the pixel).
+template <int TM, int TN, class PixOff, class PixOk>
 __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
                                               bool stats, int lane, int wch0, int nout,
                                               __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
-                                              PixOff pix_off) {
+                                              PixOff pix_off, PixOk pix_ok) {
     static_assert(TN % 2 == 0, "subtile pairs");
     const int fc = lane >> 4, fr = lane & 15;
     if (stats) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            if (pix_off(j * 16 + fr) == OOB) continue;
+            if (!pix_ok(j * 16 + fr)) continue;
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int cb = wch0 + i * 16 + fc * 4;

@@ -44,7 +44,7 @@ struct HaloArgs {
     int RT, CT;                               // tiles per image: rows, cols
     int ntiles;
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
-    int ep_lds;                               // 16-bit output via the LDS-transposed epilogue (conv_epi.h)
+    int ep_lds;                               // 16-bit output via the register-transposed epilogue (conv_epi.h)
 };
 
 // 64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1).
@@ -144,13 +144,16 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
             h_chk[j] = uint32_t((lane & 3) ^ fsw64(r)) * 8u;
             h_off[j] = ok ? uint32_t(gh * a.GW + gw) * xld_b : OOB;
         }
-        // halo row of each fragment pixel (tap (0,0) in forward order)
+        // halo row of each fragment pixel (tap (0,0) in forward order); vmask bit j: fragment pixel j lies in the
+        // output (the register epilogue's statistics mask)
         int hb[TPW];
+        uint32_t vmask = 0;
 #pragma unroll
         for (int j = 0; j < TPW; ++j) {
             const int p = (wp * TPW + j) * 16 + fr;
             const int ph = p / a.TW, pw = p - ph * a.TW;
             hb[j] = p < ntp ? ph * HWd + pw : 0;
+            vmask |= (p < ntp && oh0 + ph < a.OH && ow0 + pw < a.OW ? 1u : 0u) << j;
         }
 
         auto issue_halo = [&](int cc) {
@@ -250,10 +253,8 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
         }
 
         if (a.ep_lds) {
-            // transposed through LDS (the halo buffers are free once every wave has read the last
-            // step: barrier; the next tile's prologue waits at its own barrier) and stored as 16-B
-            // pieces of each pixel's channel run
-            raw_barrier();
+            // register-only transpose (conv_epi.h epilogue_regs: no LDS, no barrier; the statistics masked by the
+            // tile's vmask) — round 4: -2..-6 % against the LDS transpose it replaced (halo_reg_epilogue_ab.txt)
             const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
             const int wch0 = n0 + wc * (TCW * 16);
             auto pix_off = [&](int q) -> uint32_t {
@@ -263,8 +264,9 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 if (p >= ntp || oh >= a.OH || ow >= a.OW) return OOB;
                 return uint32_t((int64_t(n) * a.y_bs + int64_t(oh * a.OW + ow) * a.y_ld + wch0) * 2);
             };
-            epilogue_store<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, smem + wave * (16 * TCW * 16 * 2), lane, wch0,
-                                     a.Nout, yres, a.out_mode == 2, a.accumulate != 0 && a.out_mode == 0, pix_off);
+            auto pix_ok = [&](int q) -> bool { return (vmask >> (q >> 4)) & 1u; };
+            epilogue_regs<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_mode == 2,
+                                    a.accumulate != 0 && a.out_mode == 0, pix_off, pix_ok);
             continue;
         }
         // epilogue: lane holds channels cb..cb+3 of pixel p
@@ -448,7 +450,8 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     }
     a.accumulate = d->accumulate;
     a.TH = p.TH; a.TW = p.TW; a.HWd = p.TW + 2; a.HP = (p.TH + 2) * (p.TW + 2);
-    // LDS-transposed 16-B epilogue stores (64-ch 80x80 fwd 0.076 -> 0.070 ms, dgrad 0.066 -> 0.058)
+    // 16-B epilogue stores of transposed pixel rows (round 2 through LDS: 64-ch 80x80 fwd 0.076 -> 0.070 ms, dgrad
+    // 0.066 -> 0.058; round 4 in registers)
     a.ep_lds = !bias && a.out_mode != 1 && a.y_ld % 8 == 0 && a.y_bs % 8 == 0 &&
                int64_t(d->n) * a.y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
@@ -457,8 +460,10 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
         if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_DGRAD>), grid, dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD>), grid, dim3(512), 0, st, a);
     } else {
-        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 3, H_DGRAD>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 3, H_FWD>), grid, dim3(256), 0, st, a);
+        // 4-deep weight ring (round 4, same-process A/B: -1..-5 % against 3 slots; 6 slots cost the second
+        // workgroup per CU: +47..+61 %, profiles/r04/halo_ring_depth_ab.txt)
+        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_DGRAD>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_FWD>), grid, dim3(256), 0, st, a);
     }
     return 0;
 }

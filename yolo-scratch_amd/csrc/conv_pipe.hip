@@ -250,9 +250,10 @@ struct Issuer {
     }
 };
 
-// EPI: 0 LDS-transposed epilogue (forward); 2 register-only epilogue (epilogue_regs: no LDS, so hipcc does not
-// drain the in-flight stages in front of it) whose stores the next step's wait leaves in flight (data gradient)
-template <int BM, int BN, int WM, int WN, int MODE, int EPI = 0>
+// EPI 2: the register-only epilogue (epilogue_regs: no LDS, so hipcc does not drain the in-flight stages in front of
+// it) whose stores the next step's wait leaves in flight — both directions since round 4 (the LDS-transposed form
+// measured 2-7 % slower on every forward, profiles/r04/pipe_fwd_reg_epilogue_ab.txt)
+template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
     constexpr int NS = 3;                     // LDS ring: stage g computing, g+1 and g+2 in flight
     constexpr int RB = 128;                   // 64 K x 2 B per LDS row
@@ -264,12 +265,12 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     constexpr int TN = BM / WN / 16;          // 16-pixel subtiles per wave
     constexpr int STAGE = (BM + BN) * RB;
     static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile too small for 8-row DMA pieces");
-    // epilogue transpose area: 16 pixels x (BN / WM) channels x 2 B per wave, after the ring
+    static_assert(EPI == 2, "register-only epilogue");
     constexpr int WCH = BN / WM;                          // channels per wave
-    constexpr int EPW = 16 * WCH * 2;                     // bytes per wave
-    constexpr int EPS = EPI == 2 ? TM * TN / 2 : TN * (16 / (64 / (WCH * 2 / 16)));   // epilogue stores per lane
-    static_assert(NS * STAGE + NW * EPW <= 160 * 1024, "LDS budget");
-    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE + NW * EPW];
+    constexpr int EPS = TM * TN / 2;                      // epilogue stores per lane
+    // the ring; the statistics' cross-wave reduction reuses its first bytes after the last tile
+    static_assert(NS * STAGE <= 160 * 1024 && 2 * (BM / (BM / WN)) * BN * 4 <= NS * STAGE, "LDS budget");
+    __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -404,10 +405,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         ++ct;
 
         // epilogue: D[channel][pixel] (a lane holds 4 consecutive channels of one pixel per subtile) is
-        // transposed through this wave's LDS area 16 pixels at a time, so every store is a 16-B piece of
-        // a pixel's contiguous channel run (8 lanes = one 128-B segment), issued as buffer stores whose
-        // out-of-tile pixels fall out of range (no branches, a fixed count per tile)
-        if constexpr (EPI == 2) {
+        // transposed in registers (conv_epi.h epilogue_regs: pairs of 16-pixel subtiles exchanged with
+        // v_permlane16_swap), so every store is a 16-B piece of a pixel's contiguous channel run, issued as
+        // buffer stores whose out-of-tile pixels fall out of range (no branches, a fixed count per tile)
+        {
             const int wch0 = n0 + wr * WCH;
             const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
             const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
@@ -419,72 +420,9 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW + int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
                 return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
             };
-            epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_f32 == 2,
-                                  a.accumulate != 0, pix_off);
-        } else {
-            char* ep = smem + NS * STAGE + wave * EPW;
-            const int wch0 = n0 + wr * WCH;                   // first channel of this wave
-            const bool half = a.out_f32 == 2;                  // fp16 z (forward) or bf16 (data gradient)
-            const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
-            const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
-            constexpr int CPR = WCH * 2 / 16;                  // 16-B chunks per pixel row of this wave
-            constexpr int RPS = 64 / CPR;                      // pixel rows per store instruction
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                // stats (fp32, before rounding) and the rounded values into LDS: row fr, channel i*16+fc*4
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const int cb = wch0 + i * 16 + fc * 4;
-                    if (a.st_sum && m0 + wc * (BM / WN) + j * 16 + fr < cc.Mc) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (cb + r < a.Nout) {
-                                const float v = acc[i][j][r];
-                                ssum[i][r] += v;
-                                ssq[i][r] += v * v;
-                            }
-                    }
-                    uint2 o;
-                    if (half) {
-                        o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
-                        o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
-                    } else {
-                        o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
-                        o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
-                    }
-                    const int byte = (i * 16 + fc * 4) * 2;                       // within the row
-                    const int chunk = (byte >> 4) ^ (fr & (CPR - 1));            // swizzled 16-B chunk
-                    *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);           // lgkmcnt(0): this wave's LDS writes landed
-#pragma unroll
-                for (int h = 0; h < 16 / RPS; ++h) {
-                    const int p = h * RPS + lane / CPR, c = lane % CPR;
-                    const uint4 v = *reinterpret_cast<const uint4*>(ep + p * (WCH * 2) + ((c ^ (p & (CPR - 1))) * 16));
-                    const int64_t m = m0 + wc * (BM / WN) + j * 16 + p;
-                    uint32_t off = OOB;
-                    if (m < cc.Mc && wch0 + c * 8 < a.Nout) {
-                        uint32_t n, pix, ci_;
-                        split_pix(t_n, t_p, uint32_t(m - m0), cc.OHW, uint32_t(cc.OWc), inv_owc, n, pix, ci_);
-                        const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW +
-                                             int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
-                        off = uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0 + c * 8) * 2);
-                    }
-                    uint4 w = v;
-                    if (a.accumulate) {                        // gradient fan-in: dx += conv^T(dz) (bf16)
-                        const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
-                        uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
-                                          bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
-                        w = make_uint4(ww[0], ww[1], ww[2], ww[3]);
-                    }
-                    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, w),
-                                                           yres, off, 0, 0);
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);           // reads done before the next j rewrites the area
-            }
+            auto pix_ok = [&](int qp) -> bool { return m0 + wc * (BM / WN) + qp < cc.Mc; };
+            epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
+                                  a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
         }
     }
 
@@ -535,9 +473,11 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
+    // both directions: the register-only epilogue (round 4 for the forward, with the statistics masked by a compare:
+    // same-process A/B 2-7 % faster on every pipelined forward, profiles/r04/pipe_fwd_reg_epilogue_ab.txt)
     if (mode == PF) {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PF><<<dim3(grid), dim3(1024), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PF><<<dim3(grid), dim3(512), 0, st>>>(a);
+        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PF, 2><<<dim3(grid), dim3(1024), 0, st>>>(a);
+        else conv_pipe_kernel<256, 64, 1, 8, PF, 2><<<dim3(grid), dim3(512), 0, st>>>(a);
     } else {
         // data gradient: register-only epilogue (same-process A/B, s@640 bs64: 1-8 % faster on 9 of 10 layers)
         if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PD, 2><<<dim3(grid), dim3(1024), 0, st>>>(a);
