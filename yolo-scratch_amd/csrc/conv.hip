@@ -291,10 +291,8 @@ conv_gemm_kernel(GemmArgs a) {
 
         if constexpr (BN / WM >= 32) {
             if (a.ep_lds) {
-                // bf16 data gradient (+ fan-in accumulate): transposed through LDS and stored as
-                // 16-B pieces of each pixel's channel run; the staging ring is free once every wave
-                // has read the last stage (the next tile's prologue waits at its own barrier)
-                raw_barrier();
+                // 16-bit output (fp16 z + statistics, or the bf16 data gradient + fan-in accumulate): transposed in
+                // registers (conv_epi.h epilogue_regs) and stored as 16-B pieces of each pixel's channel run
                 const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
                 const int wch0 = n0 + wr * (BN / WM);
                 auto pix_off = [&](int q) -> uint32_t {
@@ -305,9 +303,9 @@ conv_gemm_kernel(GemmArgs a) {
                     const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(pix - ci_ * uint32_t(OWc)) * os + px;
                     return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
                 };
-                epilogue_store<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr,
-                                       smem + wave * (16 * (BN / WM) * 2), lane, wch0, a.Nout, yres, MODE == MODE_FWD,
-                                       MODE == MODE_DGRAD && a.accumulate != 0, pix_off);
+                auto pix_ok = [&](int q) -> bool { return m0 + wc * (BM / WN) + q < Mc; };
+                epilogue_regs<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr, lane, wch0, a.Nout, yres,
+                                      MODE == MODE_FWD, MODE == MODE_DGRAD && a.accumulate != 0, pix_off, pix_ok);
                 continue;
             }
         }
@@ -908,7 +906,9 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     a.out_f32 = d->out_f32; a.accumulate = d->accumulate;
     a.N = d->n;
     a.ostep = 1;
-    a.ep_lds = 0;                 // forward: fragment stores (the LDS-transposed epilogue measured equal)
+    // fp16 z: the register-transposed epilogue with 16-B row stores (round 4; fp32 / bias outputs: fragment stores)
+    a.ep_lds = d->out_f32 == 2 && !bias && d->y_ld % 8 == 0 && d->y_bs % 8 == 0 &&
+               int64_t(d->n) * d->y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     if (a.M == 0) return YM_OK;
     // the direct and halo-pipelined kernels have no bias term: a conv with bias takes the kernels below
     const DirectPlan dp = bias ? DirectPlan{} : direct_plan(d, 0);

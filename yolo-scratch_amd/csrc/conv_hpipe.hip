@@ -19,7 +19,7 @@
 //  * the barrier in the middle of a K step: every LDS read has 16 MFMAs to hide behind;
 //  * persistent workgroups (one per CU), tiles grouped per XCD, the channel tiles of one pixel tile on
 //    one XCD; BatchNorm statistics in registers across a workgroup's tiles, one partial row each;
-//  * LDS-transposed epilogue with 16-B row stores.
+//  * register-transposed epilogue with 16-B row stores (round 4; the LDS transpose before it).
 // Halo LDS rows are 128 B (64 channels); row r stores logical 16-B chunk c at slot c ^ (r & 7), which is
 // conflict-free for ds_read_b128 at EVERY starting row (the tap shifts start fragments at arbitrary rows;
 // conv_pipe's (r >> 1) & 7 swizzle conflicts 2-way there — checked with a bank model of the four
@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include "common.h"
+#include "conv_epi.h"
 #include "conv_hpipe.h"
 #include "tile.h"
 
@@ -117,12 +118,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     constexpr int TN = TS / WN;               // tile rows (16-pixel subtiles) per wave
     constexpr int WSLOT = BN * RB;
     constexpr int WCH = BN / WM;              // channels per wave
-    constexpr int EPW = 16 * WCH * 2;         // epilogue transpose area per wave
     constexpr int HI_MAX = (HPIECES + NW - 1) / NW;   // halo pieces of wave 0 (others one fewer or equal)
-    static_assert(AI >= 1 && TM >= 1 && TN >= 1, "tile");
-    // the epilogue's transpose area is the halo buffer of the tile's last chunk: after the middle barrier of
-    // the tile's last K step no wave reads it, and the next halo DMA into it is issued a K step later
-    static_assert(NW * EPW <= HBUF, "epilogue area inside a halo buffer");
+    static_assert(AI >= 1 && TM >= 1 && TN >= 1 && TN % 2 == 0, "tile");
     static_assert(2 * HBUF + NS * WSLOT <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char smem[2 * HBUF + NS * WSLOT];
     char* const hbuf0 = smem;
@@ -305,70 +302,23 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         if (++ck < spt) continue;
         ck = 0;
 
-        // ---- epilogue of tile ct (conv_pipe's LDS-transposed 16-B row stores)
+        // ---- epilogue of tile ct: register-transposed 16-B row stores (conv_epi.h epilogue_regs; round 4: no LDS
+        // area, no waits on LDS round trips)
         const int mt = mt_lo + ct * qstride;
         ++ct;
         const int n = mt / a.tpi, rem = mt - n * a.tpi;
         const int ty = rem / a.tpr, tx = rem - ty * a.tpr;
-        char* ep = hbuf0 + ((ct * CC - 1) & 1) * HBUF + wave * EPW;     // (ct already advanced)
         const int wch0 = n0 + wr * WCH;
-        const bool half = a.out_f32 == 2;
         const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.H) * a.W * a.y_ld) * 2;
         const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
-        constexpr int CPR = WCH * 2 / 16;
-        constexpr int RPS = 64 / CPR;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int cb = wch0 + i * 16 + fc * 4;
-                if (a.st_sum) {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (cb + r < a.Nout) {
-                            const float v = acc[i][j][r];
-                            ssum[i][r] += v;
-                            ssq[i][r] += v * v;
-                        }
-                }
-                uint2 o;
-                if (half) {
-                    o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
-                    o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
-                } else {
-                    o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
-                    o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
-                }
-                const int byte = (i * 16 + fc * 4) * 2;
-                const int chunk = (byte >> 4) ^ (fr & (CPR - 1));
-                *reinterpret_cast<uint2*>(ep + fr * (WCH * 2) + chunk * 16 + (byte & 15)) = o;
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            const int oy = ty * TS + wc * TN + j;
-#pragma unroll
-            for (int h = 0; h < 16 / RPS; ++h) {
-                const int p = h * RPS + lane / CPR, c = lane % CPR;
-                const uint4 v = *reinterpret_cast<const uint4*>(ep + p * (WCH * 2) + ((c ^ (p & (CPR - 1))) * 16));
-                const int ox = tx * TS + p;
-                const uint32_t off = wch0 + c * 8 < a.Nout
-                                         ? uint32_t((int64_t(n) * a.y_bs + (int64_t(oy) * a.W + ox) * a.y_ld + wch0 +
-                                                     c * 8) * 2)
-                                         : OOB;
-                uint4 wv = v;
-                if (a.accumulate) {
-                    const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
-                    uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
-                                      bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
-                    wv = make_uint4(ww[0], ww[1], ww[2], ww[3]);
-                }
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, wv),
-                                                       yres, off, 0, 0);
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-        }
+        // wave-local pixel q: tile row wc * TN + (q >> 4), column q & 15 (every pixel of a tile is in the map)
+        auto pix_off = [&](int q) -> uint32_t {
+            const int oy = ty * TS + wc * TN + (q >> 4), ox = tx * TS + (q & 15);
+            return uint32_t((int64_t(n) * a.y_bs + (int64_t(oy) * a.W + ox) * a.y_ld + wch0) * 2);
+        };
+        auto pix_ok = [](int) -> bool { return true; };
+        epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_f32 == 2,
+                              a.accumulate != 0, pix_off, pix_ok);
     }
 
     if (a.st_sum) {
