@@ -195,6 +195,7 @@ PIPE = [
     (18, 61, 63, 128, 192, 3, 1, 1, 64, 8),
     (16, 64, 64, 64, 128, 3, 1, 1, 0, 64),
     (16, 128, 128, 64, 128, 3, 2, 1, 0, 0),
+    (70, 63, 61, 128, 128, 3, 2, 1, 0, 0),     # odd map: unequal stride-2 classes (class-major tile order)
     (16, 64, 64, 256, 128, 1, 1, 0, 128, 0),
     (12, 80, 80, 64, 64, 3, 1, 1, 0, 0),
 ]

@@ -663,21 +663,17 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
 
 // ------------------------------------------------------------------ weight preparation
 // fp32 OIHW master weights -> fp16 [Cout][KH][KW][Cin] (fwd, blockIdx.y 0) and bf16
-// [Cin][KH][KW][Cout_t] (dgrad, blockIdx.y 1).  A thread owns one DESTINATION element (coalesced
-// 2-B stores; the fp32 gathers hit L2), its table entry found by binary search over the offsets.
-__global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int n_entries, int64_t total) {
-    const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= total) return;
-    int lo = 0, hi = n_entries - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (tab[mid].elem_offset <= i) lo = mid;
-        else hi = mid - 1;
-    }
-    const ym_wprep_entry t = tab[lo];
-    const int j = int(i - t.elem_offset);
+// [Cin][KH][KW][Cout_t] (dgrad, blockIdx.y 1).  A thread owns DESTINATION elements (coalesced 2-B
+// stores; the fp32 gathers hit L2).  A block owns PREP_CHUNK consecutive elements of the concatenated
+// index space: one block-uniform binary search finds the chunk's first entry; a chunk inside one entry
+// (nearly all of them) runs PREP_PER independent gathers per thread before its stores, a chunk that
+// crosses entries walks the table element by element.  (Round 3's one-element-per-thread kernel with a
+// binary search per element: 168 us per step on s@640.)
+constexpr int PREP_PER = 16, PREP_CHUNK = 256 * PREP_PER;
+
+__device__ __forceinline__ void prep_one(const ym_wprep_entry& t, int j, int pass) {
     const int T = t.kh * t.kw;
-    if (blockIdx.y == 0) {
+    if (pass == 0) {
         if (!t.dst_fwd) return;
         const int ci = j % t.cin, r = j / t.cin;
         const int tap = r % T, co = r / T;
@@ -687,6 +683,57 @@ __global__ void prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int 
         const int co = j % t.cout, r = j / t.cout;
         const int tap = r % T, ci = r / T;
         t.dst_t[(int64_t(ci) * T + tap) * t.cout_t + co] = f2bf(t.src[(int64_t(co) * t.cin + ci) * T + tap]);
+    }
+}
+
+__global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int n_entries,
+                                                           int64_t total) {
+    const int64_t c0 = int64_t(blockIdx.x) * PREP_CHUNK, c1 = min(c0 + PREP_CHUNK, total);
+    const int pass = blockIdx.y;
+    int lo = 0, hi = n_entries - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[mid].elem_offset <= c0) lo = mid;
+        else hi = mid - 1;
+    }
+    const ym_wprep_entry t = tab[lo];
+    const int64_t t_end = lo + 1 < n_entries ? tab[lo + 1].elem_offset : total;
+    if (c1 <= t_end) {
+        uint16_t* dst = pass == 0 ? t.dst_fwd : t.dst_t;
+        if (!dst) return;
+        const int T = t.kh * t.kw;
+        const int jb = int(c0 - t.elem_offset) + threadIdx.x, nj = int(c1 - t.elem_offset);
+        float v[PREP_PER];
+        int64_t di[PREP_PER];
+#pragma unroll
+        for (int k = 0; k < PREP_PER; ++k) {
+            const int j = min(jb + k * 256, nj - 1);
+            int64_t si;
+            if (pass == 0) {
+                const int ci = j % t.cin, r = j / t.cin;
+                const int tap = r % T, co = r / T;
+                si = (int64_t(co) * t.cin + ci) * T + tap;
+                di[k] = j;
+            } else {
+                const int co = j % t.cout, r = j / t.cout;
+                const int tap = r % T, ci = r / T;
+                si = (int64_t(co) * t.cin + ci) * T + tap;
+                di[k] = (int64_t(ci) * T + tap) * t.cout_t + co;
+            }
+            v[k] = t.src[si];
+        }
+#pragma unroll
+        for (int k = 0; k < PREP_PER; ++k) {
+            if (jb + k * 256 >= nj) break;
+            dst[di[k]] = pass == 0 ? f2h(v[k]) : f2bf(v[k]);
+        }
+        return;
+    }
+    // the chunk crosses entries: walk the table per element (entries are sorted by offset)
+    int e = lo;
+    for (int64_t i = c0 + threadIdx.x; i < c1; i += 256) {
+        while (e + 1 < n_entries && tab[e + 1].elem_offset <= i) ++e;
+        prep_one(tab[e], int(i - tab[e].elem_offset), pass);
     }
 }
 
@@ -1076,7 +1123,8 @@ extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
 
 extern "C" int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream) {
     if (total_elems == 0) return YM_OK;
-    hipLaunchKernelGGL(prep_weights_kernel, dim3(unsigned((total_elems + 255) / 256), 2), dim3(256), 0, as_stream(stream),
+    hipLaunchKernelGGL(prep_weights_kernel, dim3(unsigned((total_elems + PREP_CHUNK - 1) / PREP_CHUNK), 2), dim3(256), 0,
+                       as_stream(stream),
                        table_dev, n_entries, total_elems);
     YM_LAUNCH_CHECK("ym_prep_weights");
     return YM_OK;
