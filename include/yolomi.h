@@ -165,11 +165,6 @@ int ym_conv_set_halo(int mode);
  * inputs) at >= 256 tiles, never a stride-2 data gradient.  Returns the previous setting.
  * Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_pipe(int mode);
-/* The 1x1 streaming kernel of the pipelined family (conv_pipe.hip cfg 2: 1x1 stride-1 layers with <= 512
- * input channels, the 128-channel weight slice resident in LDS, activation fragments loaded straight into
- * registers): -1 default (on), 0 never (those layers take the 256-pixel tiles), 1 on.  Returns the previous
- * setting.  Process-wide, like ym_conv_set_halo. */
-int ym_conv_set_pipe1x1(int mode);
 /* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
  * layers) for later calls: -1 default, 0 never, 1 maps of >= 1 M output pixels (default), 2 any size.
  * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */

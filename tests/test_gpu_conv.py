@@ -208,47 +208,6 @@ def test_pipe_kernel_vs_torch(shape):
     _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
 
 
-# 1x1 streaming kernel (conv_pipe.hip cfg 2; on by default inside the pipelined family): 128-channel weight
-# slices resident in LDS, activation fragments loaded straight into registers.  K = 64 .. 512 (K steps of 2 / 4 /
-# 6 / 8, one or two passes), partial channel ranges, pixel counts that are not multiples of the 32-pixel wave
-# tile, channel-slice views in and out, fp16 z + BN partials, bf16 data gradient overwrite and accumulate
-PIPE1X1 = [
-    (16, 64, 64, 256, 128, 1, 1, 0, 128, 0),
-    (5, 37, 29, 192, 256, 1, 1, 0, 64, 8),
-    (3, 40, 40, 384, 192, 1, 1, 0, 0, 64),
-    (2, 20, 20, 512, 64, 1, 1, 0, 0, 0),
-    (4, 33, 17, 128, 512, 1, 1, 0, 8, 0),
-]
-
-
-@pytest.mark.parametrize("shape", PIPE1X1, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}" for s in PIPE1X1])
-def test_pipe1x1_stream_vs_torch(shape):
-    from yolomi._lib import lib, ConvDesc
-    n, h, w, cin, cout, k, s, p, xe, ye = shape
-    d = ConvDesc()
-    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, h, w, cout, 1, 1, 0
-    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * (cin + xe), cin + xe, h * w * (cout + ye), cout + ye
-    prev = lib().ym_conv_set_pipe(2)
-    try:
-        for dr in (0, 1):
-            b = ctypes.create_string_buffer(96)
-            lib().ym_conv_kernel(ctypes.byref(d), dr, b, 96)
-            assert b.value.decode() == "pipe 1x1 stream", (dr, b.value)
-    finally:
-        lib().ym_conv_set_pipe(prev)
-    _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
-
-
-def test_pipe1x1_off_keeps_the_tiled_kernel():
-    """ym_conv_set_pipe1x1(0): the 1x1 layer runs on the 256-pixel tiles again, same numerics bar."""
-    from yolomi._lib import lib
-    prev = lib().ym_conv_set_pipe1x1(0)
-    try:
-        _views_fwd_dgrad_check(PIPE1X1[0], lib().ym_conv_set_pipe, 2, 2)
-    finally:
-        lib().ym_conv_set_pipe1x1(prev)
-
-
 # halo-staged PIPELINED 3x3 stride-1 kernel (conv_hpipe.hip), forced on with ym_conv_set_hpipe(2): 16x16-pixel
 # tiles on maps whose sides are multiples of 16, 128-channel tiles (a partial second channel tile at 192),
 # 2-4 input chunks of 64 channels, channel-slice views in and out, fp16 z + BN statistic partials,

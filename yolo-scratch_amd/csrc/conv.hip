@@ -851,13 +851,6 @@ extern "C" int ym_conv_set_pipe(int mode) {
     return prev;
 }
 
-extern "C" int ym_conv_set_pipe1x1(int mode) {
-    // the 1x1 streaming kernel inside the pipelined family: -1 default (on), 0 never, 1 on; returns the previous setting
-    const int prev = g_s1_mode;
-    g_s1_mode = mode < -1 || mode > 1 ? -1 : mode;
-    return prev;
-}
-
 extern "C" int ym_conv_set_direct(int mode) {
     // selection policy of the direct register-weight kernel: -1 default, 0 never, 1 maps of
     // >= 1 M output pixels (default), 2 any size; returns the previous setting
@@ -907,7 +900,7 @@ extern "C" int ym_conv_kernel(const ym_conv_desc* d, int dir, char* name, int na
             snprintf(buf, sizeof buf, "hpipe %s", hq.cfg == 0 ? "16x16px x 128" : hq.cfg == 1 ? "16x16px x 64" : "16x16px x 64 wres");
         } else if (pp.ok) {
             id = 2000 + pp.cfg;
-            snprintf(buf, sizeof buf, "pipe %s", pp.cfg == 0 ? "256x128" : pp.cfg == 1 ? "256x64" : "1x1 stream");
+            snprintf(buf, sizeof buf, "pipe %s", pp.cfg == 0 ? "256x128" : "256x64");
         } else if (hp.ok) {
             id = 1000 + 100 * hp.cfg + std::min(hp.TW, 99);
             snprintf(buf, sizeof buf, "halo %s %dx%d", hp.cfg == 0 ? "C8" : "C4", hp.TH, hp.TW);

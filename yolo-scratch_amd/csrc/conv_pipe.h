@@ -9,7 +9,7 @@ namespace ym {
 
 struct PipePlan {
     int ok;          // the pipelined kernel handles this conv
-    int cfg;         // tile configuration (conv_pipe.hip: kCfg; 2 = the 1x1 streaming kernel)
+    int cfg;         // tile configuration (conv_pipe.hip: kCfg)
     int grid;        // workgroups (persistent; a multiple of 8 * channel tiles)
     int rows;        // rows of the BN statistics partials (= grid / channel tiles)
 };
@@ -17,8 +17,6 @@ struct PipePlan {
 // -1: default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
 // tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
 extern int g_pipe_force;
-// the 1x1 streaming kernel (pipe cfg 2): -1 default (on), 0 never, 1 on (ym_conv_set_pipe1x1)
-extern int g_s1_mode;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);

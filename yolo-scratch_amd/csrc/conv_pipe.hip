@@ -40,8 +40,6 @@ namespace ym {
 // output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
 // wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
 int g_pipe_force = -1;
-// 1x1 streaming kernel (ym_conv_set_pipe1x1): -1 default (on), 0 never, 1 on
-int g_s1_mode = -1;
 
 namespace {
 
@@ -464,255 +462,6 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     }
 }
 
-// ------------------------------------------------------------------ 1x1 streaming kernel (cfg 2)
-// A 1x1 stride-1 conv moves Cin + Cout 16-bit values per pixel for Cin * Cout MACs: at most 341 MAC/B
-// on this graph, under the 2.5 PF / 8 TB/s ridge — every 1x1 layer is HBM-bound.  The pipelined
-// kernel above stages A through its LDS ring with two 48-KB stages in flight per CU; on the 1x1 layers
-// that left the loop at 2-3 TB/s even with the epilogue removed (profiles/r04/pipe_fwd_epilogue_
-// ablation.txt: 80x80 192->256 79 us of loads + MFMA for 157 MB).  Here:
-//  * the workgroup's 128-channel weight slice [128][Kin] sits in LDS for the whole kernel (Kin <= 512:
-//    <= 128 KB, one workgroup of 8 waves per CU);
-//  * no A staging at all: a 16x16x32 MFMA B-fragment is 8 consecutive channels of one pixel, i.e. 16
-//    contiguous bytes of an NHWC row, so each lane loads its activation fragments straight from HBM
-//    into registers (one 16-B buffer load per 16 pixels x 32 channels);
-//  * the waves never synchronise after the weight load: each streams its own 32-pixel tiles, and the
-//    register holding K step s is refilled with the NEXT unit's step s right after its MFMAs consume it
-//    — a whole unit (32 pixels x 32*KS channels, 2-16 KB) of loads in flight per wave, 8 waves per CU;
-//  * the 4 x 16-B LDS weight reads per K step feed 16 MFMAs (16 MAC/B of LDS traffic);
-//  * channel ranges of one pixel-tile sequence run on the same XCD (the second range's A hits L2);
-//  * BatchNorm statistics accumulate in registers over a wave's tiles, reduce through LDS in a fixed
-//    order and land as one partial row per workgroup (bit-reproducible), as the kernel above.
-struct S1Args {
-    const bf16_t* x; int64_t x_bs, x_ld;       // A view (n, hw, Kin)
-    const bf16_t* w;                            // [Nout][Kin]
-    void* y; int64_t y_bs, y_ld;                // output view
-    const float* bias;                          // [Nout] or null
-    float* st_sum; float* st_sq;                // [rows][Nout] or null
-    int HW, Kin, Nout, N, nr, half, accumulate;
-    float inv_hw;
-};
-
-// sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15), every lane of the row receiving it: quad xor 1 / 2, then
-// row rotations by 4 and 8 (VALU DPP moves; __shfl_xor lowers to ds_bpermute, an LDS round trip per step)
-__device__ __forceinline__ float row16_sum(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
-    return v;
-}
-
-template <int KS, int P, int MODE, bool ACC>
-__global__ void __launch_bounds__(512, 1) conv_s1_kernel(S1Args a) {
-    constexpr int TM = 8, TN = 2, NWV = 8;
-    __shared__ __attribute__((aligned(16))) char smem[128 * 512 * 2 + 128 * 4];
-    float* bias_s = reinterpret_cast<float*>(smem + 128 * 512 * 2);   // the range's bias (an LDS read in the
-                                                                       // epilogue: a global load there would drain
-                                                                       // the prefetched A with a vmcnt(0))
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int fc = lane >> 4, fr = lane & 15;
-    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
-    const int nrange = slot % a.nr, group = slot / a.nr, groups = int(gridDim.x >> 3) / a.nr;
-    const int n0 = nrange * 128;
-    const int RB = a.Kin * 2, cpr = a.Kin >> 3;            // LDS row bytes, 16-B chunks per row
-    // row swizzle of the 16-B chunks: XOR with the row's low 4 bits when a row has a multiple of 16 chunks (a
-    // ds_read_b128 lane group then covers all 16 slots of the 256-B bank row), else 3 bits (Kin 64 / 192)
-    const int swm = (cpr & 15) ? 7 : 15;
-    const int64_t M = int64_t(a.N) * a.HW;
-    const int mt = int((M + 31) >> 5);
-    const int wslot = (group * 8 + xcd) * NWV + wave, wstride = groups * 8 * NWV;
-    const int ntw = wslot < mt ? (mt - 1 - wslot) / wstride + 1 : 0;
-    const __amdgpu_buffer_rsrc_t xr = make_rsrc(a.x, int64_t(a.N) * a.x_bs * 2);
-    const __amdgpu_buffer_rsrc_t yr = make_rsrc(a.y, int64_t(a.N) * a.y_bs * 2);
-    // (image, pixel) of lane row fr of subtile j of tile t -> element offset in a view (OOB past the map)
-    auto pix_of = [&](int t, int j, int64_t bs, int64_t ld) -> uint32_t {
-        const int64_t p = int64_t(t) * 32 + j * 16 + fr;
-        if (p >= M) return OOB;
-        int n = int(float(p) * a.inv_hw);
-        int64_t rem = p - int64_t(n) * a.HW;
-        if (rem < 0) { --n; rem += a.HW; }
-        else if (rem >= a.HW) { ++n; rem -= a.HW; }
-        return uint32_t(int64_t(n) * bs + rem * ld);
-    };
-    uint4 A[KS][TN];
-    auto unit_off = [&](int t_idx, int pass, uint32_t (&o)[TN]) {
-        const int t = wslot + t_idx * wstride;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const uint32_t e = t_idx < ntw ? pix_of(t, j, a.x_bs, a.x_ld) : OOB;
-            o[j] = e == OOB ? OOB : e * 2u + uint32_t(pass * KS * 64 + fc * 16);
-        }
-    };
-    // the first unit's activation loads go out before the weight prologue (in flight across it)
-    {
-        uint32_t aoff[TN];
-        unit_off(0, 0, aoff);
-#pragma unroll
-        for (int s = 0; s < KS; ++s)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) A[s][j] = buf_load16(xr, aoff[j] == OOB ? OOB : aoff[j] + s * 64);
-    }
-    {
-        // weights [128][Kin] of this channel range -> LDS, 16-B chunks swizzled by row; every load of a
-        // thread in flight at once (a load-then-store loop paid one L2 round trip per chunk)
-        constexpr int WQ = 128 * 512 * 2 / 16 / 512;
-        const __amdgpu_buffer_rsrc_t wr = make_rsrc(a.w, int64_t(a.Nout) * RB);
-        uint4 wv[WQ];
-#pragma unroll
-        for (int q = 0; q < WQ; ++q) {
-            const int e = tid + q * 512, r = e / cpr, c = e - r * cpr;
-            const int ch = n0 + r;
-            wv[q] = buf_load16(wr, e < 128 * cpr && ch < a.Nout ? uint32_t(ch * RB + c * 16) : OOB);
-        }
-#pragma unroll
-        for (int q = 0; q < WQ; ++q) {
-            const int e = tid + q * 512, r = e / cpr, c = e - r * cpr;
-            if (e < 128 * cpr) *reinterpret_cast<uint4*>(smem + r * RB + ((c ^ (r & swm)) << 4)) = wv[q];
-        }
-        if (a.bias && tid < 128) bias_s[tid] = n0 + tid < a.Nout ? a.bias[n0 + tid] : 0.f;
-    }
-    __syncthreads();
-    // fragment-read offsets of the weights in LDS: row i*16 + fr, chunk (kstep*4 + fc) swizzled by the row
-    const int wrow = fr * RB;
-    const int wsw = fr & swm;
-
-    f32x4 acc[TM][TN];
-    float ssum[TM][4], ssq[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
-    }
-    const bool stats = a.st_sum != nullptr;
-    const char* wb = smem + wrow;
-    auto read_w = [&](bf16x8 (&f)[TM], int kstep) {
-        const int co = ((kstep * 4 + fc) ^ wsw) << 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) f[i] = *reinterpret_cast<const bf16x8*>(wb + i * 16 * RB + co);
-    };
-    // Straight-line per tile (P passes unrolled) with UNCONDITIONAL prefetch loads (OOB past the wave's last tile)
-    // and stores: every path issues the same memory operations, so the compiler's vmcnt waits are exact — with a
-    // conditional prefetch or a conditional epilogue it merged the paths to the smaller count and each unit's last
-    // step waited for the next unit's loads (vmcnt(0)).
-    for (int ti = 0; ti < ntw; ++ti) {
-#pragma unroll
-        for (int pass = 0; pass < P; ++pass) {
-            uint32_t noff[TN];
-            unit_off(pass + 1 < P ? ti : ti + 1, pass + 1 < P ? pass + 1 : 0, noff);
-            // weight fragments double-buffered across K steps (KS <= 4; at 6 / 8 the second buffer spills)
-            constexpr bool DB = KS <= 4;
-            bf16x8 fw[2][TM];
-            read_w(fw[0], pass * KS);
-#pragma unroll
-            for (int s = 0; s < KS; ++s) {
-                if constexpr (DB) {
-                    if (s + 1 < KS) read_w(fw[(s + 1) & 1], pass * KS + s + 1);
-                } else if (s > 0) {
-                    read_w(fw[s & 1], pass * KS + s);
-                }
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) {
-                        if constexpr (MODE == PF)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fw[s & 1][i]),
-                                                                                __builtin_bit_cast(f16x8, A[s][j]),
-                                                                                acc[i][j], 0, 0, 0);
-                        else
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                                fw[s & 1][i], __builtin_bit_cast(bf16x8, A[s][j]), acc[i][j], 0, 0, 0);
-                    }
-#pragma unroll
-                for (int j = 0; j < TN; ++j) A[s][j] = buf_load16(xr, noff[j] == OOB ? OOB : noff[j] + s * 64);
-                // keep each refill behind its step's MFMAs: hoisted, the loads need a second copy of A (spills)
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        const int t = wslot + ti * wstride;
-        if (a.bias) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float bv = bias_s[i * 16 + fc * 4 + r];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j][r] += bv;
-                }
-        }
-        uint32_t yo[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const uint32_t e = pix_of(t, j, a.y_bs, a.y_ld);
-            yo[j] = e == OOB ? OOB : (e + uint32_t(n0)) * 2u;
-        }
-        const int64_t pbase = int64_t(t) * 32;
-        epilogue_regs<TM, TN>(acc, ssum, ssq, stats, lane, n0, a.Nout, yr, MODE == PF && a.half != 0, ACC,
-                              [&](int q) { return q < 16 ? yo[0] : yo[1]; }, [&](int q) { return pbase + q < M; });
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (stats) {
-        // wave partials (lanes fr == 0 after the butterfly) -> LDS in wave order -> one row per workgroup
-        __syncthreads();                         // every wave is done with the weights
-        float* red = reinterpret_cast<float*>(smem);           // [2][NWV][128]
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float s = row16_sum(ssum[i][r]), sq = row16_sum(ssq[i][r]);
-                if (fr == 0) {
-                    const int cl = i * 16 + fc * 4 + r;
-                    red[wave * 128 + cl] = s;
-                    red[(NWV + wave) * 128 + cl] = sq;
-                }
-            }
-        __syncthreads();
-        const int row = xcd + 8 * group;
-        if (tid < 128 && n0 + tid < a.Nout) {
-            float ps = 0.f, pq = 0.f;
-#pragma unroll
-            for (int w = 0; w < NWV; ++w) { ps += red[w * 128 + tid]; pq += red[(NWV + w) * 128 + tid]; }
-            a.st_sum[int64_t(row) * a.Nout + n0 + tid] = ps;
-            a.st_sq[int64_t(row) * a.Nout + n0 + tid] = pq;
-        }
-    }
-}
-
-template <int MODE, bool ACC>
-void launch_s1(int ks, int np, const S1Args& a, int grid, hipStream_t st) {
-    const dim3 g(grid), b(512);
-    if (np == 1) {
-        switch (ks) {
-            case 2: conv_s1_kernel<2, 1, MODE, ACC><<<g, b, 0, st>>>(a); break;
-            case 4: conv_s1_kernel<4, 1, MODE, ACC><<<g, b, 0, st>>>(a); break;
-            case 6: conv_s1_kernel<6, 1, MODE, ACC><<<g, b, 0, st>>>(a); break;
-            default: conv_s1_kernel<8, 1, MODE, ACC><<<g, b, 0, st>>>(a); break;
-        }
-    } else if (ks == 6) {
-        conv_s1_kernel<6, 2, MODE, ACC><<<g, b, 0, st>>>(a);
-    } else {
-        conv_s1_kernel<8, 2, MODE, ACC><<<g, b, 0, st>>>(a);
-    }
-}
-
-// K steps of 32 per pass for the instantiated depths: one pass of 2 / 4 / 6 / 8 steps (Kin 64 / 128 / 192 / 256) or
-// two of 6 / 8 (Kin 384 / 512); 0 = not handled
-int s1_ks(int kin) {
-    switch (kin) {
-        case 64: return 2;
-        case 128: return 4;
-        case 192: case 384: return 6;
-        case 256: case 512: return 8;
-        default: return 0;
-    }
-}
-
 // tile configurations
 struct Cfg {
     int bm, bn;
@@ -759,21 +508,6 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     // input channels, at >= 256 tiles; never the stride-2 data gradient
     if (mode == 3 && (os == 2 || (d->k == 3 && nout < 128 && (dgrad || kin < 128)))) return p;
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
-    // 1x1 stride-1 layers: the streaming kernel (cfg 2) where its limits hold
-    if (g_s1_mode != 0 && d->k == 1 && d->stride == 1 && d->pad == 0 && kin <= 512 && s1_ks(kin) &&
-        in_ld % 8 == 0 && out_ld % 8 == 0 && out_bs % 8 == 0) {
-        const int64_t Mr = int64_t(d->n) * OH * OW;
-        const int nr = (nout + 127) / 128;
-        const int grid = (256 / (8 * nr)) * 8 * nr;
-        if (grid >= 8 * nr && Mr < (int64_t(1) << 24) && int64_t(d->n) * in_bs * 2 < (int64_t(1) << 31) &&
-            int64_t(d->n) * out_bs * 2 < (int64_t(1) << 31)) {
-            p.cfg = 2;
-            p.grid = grid;
-            p.rows = grid / nr;
-            p.ok = 1;
-            return p;
-        }
-    }
     // split_pix: in-image pixel indices as exact floats, row estimates within one of the truth
     if (int64_t(OH) * OW >= (int64_t(1) << 24) || OH >= (1 << 16)) return p;
     const int64_t M = select_n(d) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
@@ -797,29 +531,6 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
 
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
                 const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
-    if (p.cfg == 2) {
-        S1Args b{};
-        b.x = x; b.w = w; b.y = y;
-        b.bias = bias; b.st_sum = st_sum; b.st_sq = st_sq;
-        b.N = d->n;
-        if (!dgrad) {
-            b.x_bs = d->x_bs; b.x_ld = d->x_ld; b.y_bs = d->y_bs; b.y_ld = d->y_ld;
-            b.HW = d->h * d->w; b.Kin = d->cin; b.Nout = d->cout;
-            b.half = d->out_f32 == 2;
-        } else {
-            b.x_bs = d->y_bs; b.x_ld = d->y_ld; b.y_bs = d->x_bs; b.y_ld = d->x_ld;
-            b.HW = d->oh * d->ow; b.Kin = d->cout; b.Nout = d->cin;
-            b.half = 0;
-        }
-        b.accumulate = d->accumulate;
-        b.nr = (b.Nout + 127) / 128;
-        b.inv_hw = 1.0f / float(b.HW);
-        const int ks = s1_ks(b.Kin), np = b.Kin / (32 * ks);
-        if (!dgrad) launch_s1<PF, false>(ks, np, b, p.grid, st);
-        else if (b.accumulate) launch_s1<PD, true>(ks, np, b, p.grid, st);
-        else launch_s1<PD, false>(ks, np, b, p.grid, st);
-        return YM_OK;
-    }
     PipeArgs a{};
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
     if (!dgrad) {

@@ -60,7 +60,6 @@ SIGNATURES = {
     "ym_conv_set_select_batch": (R, [INT]),
     "ym_conv_set_halo": (R, [INT]),
     "ym_conv_set_pipe": (R, [INT]),
-    "ym_conv_set_pipe1x1": (R, [INT]),
     "ym_conv_set_direct": (R, [INT]),
     "ym_conv_set_hpipe": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
