@@ -292,9 +292,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    marks = []
     for i in range(args.steps):
         loss = step(args.warmup + i)
+        marks.append(time.perf_counter())
     torch.cuda.synchronize()
+    if os.environ.get("YM_BENCH_STEP_TIMES"):
+        # host time at which each step() returned (no sync inside the loop): a host that runs ahead of
+        # the GPU returns faster than the GPU step; one blocked every step returns at the GPU's pace
+        log("host step returns (ms): " + " ".join(f"{1e3 * (b - a):.1f}" for a, b in zip([t0] + marks, marks)))
     if dp:
         dist.barrier()
     elapsed = time.perf_counter() - t0

@@ -53,6 +53,30 @@ def main():
             cur_e = max(cur_e, e)
     busy += cur_e - cur_s
     print(f"union busy {busy / 1e6:.3f} ms of {wall / 1e6:.3f} ({busy / wall:.1%})")
+    # idle gaps (no kernel on any stream): where the wall time the union misses goes
+    gaps, cur_e, prev = [], seg[0][1], seg[0]
+    for k in seg[1:]:
+        if k[0] > cur_e:
+            gaps.append((k[0] - cur_e, cur_e - t0, prev[2], k[2]))
+        if k[1] >= cur_e:
+            cur_e, prev = k[1], k
+    tail = ks[starts[mid + 1]][0] - cur_e
+    big = sorted(gaps, reverse=True)
+    hist = collections.Counter()
+    for g, *_ in gaps:
+        hist["<2us" if g < 2000 else "2-10us" if g < 10000 else "10-50us" if g < 50000 else ">=50us"] += g
+    print(f"idle gaps: {len(gaps)}, {sum(g for g, *_ in gaps) / 1e6:.3f} ms (" +
+          ", ".join(f"{k} {v / 1e6:.3f}" for k, v in sorted(hist.items())) + f"); after the last kernel {tail / 1e6:.3f} ms")
+    for g, at, a, b in big[:12]:
+        print(f"  gap {g / 1e3:7.1f} us at {at / 1e6:7.3f} ms  after {family(a)[:40]:40} before {family(b)[:40]}")
+    if "--windows" in sys.argv:
+        # the kernels of every stream around the largest gaps: what was the GPU waiting for
+        for g, at, a, b in big[:6]:
+            lo, hi = t0 + at - 60000, t0 + at + g + 60000
+            print(f"-- window around the {g / 1e3:.1f}-us gap at {at / 1e6:.3f} ms")
+            for s_, e_, n_, q_ in seg:
+                if e_ >= lo and s_ <= hi:
+                    print(f"   q{q_} {(s_ - t0) / 1e6:8.3f} .. {(e_ - t0) / 1e6:8.3f}  {family(n_)[:60]}")
     last = sorted(seg, key=lambda k: k[1])[-25:]
     print("last kernels to finish:")
     for s, e, n, q in last:
