@@ -185,6 +185,12 @@ def main():
     ap.add_argument("--scale", default="s")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    # N > 1: the DP comm stream and RCCL's own stream join the 4 compute streams (default, 2 DAG, weight
+    # gradients); with HIP's default 4 hardware queues they would share queues with compute streams (a
+    # collective queued behind weight-gradient kernels).  8 queues, set before HIP initialises, give each
+    # stream its own; at N = 1 8 vs 4 queues measured equal (profiles/r04/hw_queues_ab.txt).
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import torch
     import torch.distributed as dist
