@@ -224,6 +224,32 @@ int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t tota
  * plus ticket counters.  Zero it once before first use (the library leaves the counters at zero
  * after every call); calls sharing one workspace must be ordered (same stream). */
 size_t ym_bn_workspace_size(int c);
+/* BatchNorm parameters for ym_conv_fwd_bn: the arguments of ym_bn_finalize after the statistics rows. */
+typedef struct {
+    const float* gamma;
+    const float* beta;
+    float* running_mean;       /* running statistics (momentum update) or NULL */
+    float* running_var;
+    int64_t* num_batches_tracked;
+    float* scale;              /* outputs, [c] each: gamma * rstd, beta - mean * scale, mean, rstd */
+    float* shift;
+    float* mean;
+    float* rstd;
+    void* workspace;           /* ym_bn_workspace_size(c) bytes, zeroed once (shared with ym_bn_finalize) */
+    double count;              /* elements per channel (n * oh * ow) */
+    float momentum;
+    float eps;
+} ym_bn_fold;
+/* Conv forward + BatchNorm statistics AND their finalize: ym_conv_fwd (stat_sum / stat_sq as there, bias-free,
+ * fp16 z) followed by ym_bn_finalize over its rows, with the same outputs.  Where ym_conv_fwd_bn_fused(d) is 1
+ * the finalize runs as the conv launch's tail (the last workgroup of each channel tile folds the tile's rows in
+ * fp64, fixed order) instead of a second launch; elsewhere the two launches run in order. */
+int ym_conv_fwd_bn_fused(const ym_conv_desc* d);
+int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, float* stat_sum,
+                   float* stat_sq, const ym_bn_fold* bn, void* stream);
+/* Fold policy of ym_conv_fwd_bn for later calls: -1 default (on), 0 never (conv, then ym_bn_finalize), 1 on.
+ * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+int ym_conv_set_fold(int mode);
 int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                    float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* workspace,

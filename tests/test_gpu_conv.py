@@ -459,3 +459,68 @@ def test_conv_fwd_bias_on_every_policy(k, out_f32):
     ref = (F.conv2d(x.float().permute(0, 3, 1, 2), wt.float(), bias, padding=p)).permute(0, 2, 3, 1)
     err = float((y.float().cpu() - ref).abs().max() / ref.abs().max())
     assert err < (2e-3 if out_f32 == 2 else 1e-2), err
+
+
+# ym_conv_fwd_bn: conv forward + BatchNorm finalize, the finalize folded into the pipelined kernel's tail where
+# ym_conv_fwd_bn_fused says so (tickets per channel tile, fixed-order fp64 fold), else conv + ym_bn_finalize.
+# Both against the two-call path (ym_conv_fwd, ym_bn_finalize): z bit-identical, the coefficients and running
+# statistics to 1e-6 (the fold order differs), num_batches_tracked +1 exactly; three calls in a row (the tickets
+# re-arm themselves).
+FOLD = [
+    (16, 64, 64, 128, 128, 3, 1),      # pipe 256x128, one channel tile, fused
+    (16, 64, 64, 256, 192, 1, 0),      # pipe 1x1, 2 channel tiles (192 = 128 + 64), fused
+    (16, 128, 128, 64, 128, 3, 1),     # stride 1 128-channel: pipe
+    (2, 20, 20, 128, 128, 3, 1),       # small map: halo kernel, not fused (conv + finalize)
+]
+
+
+@pytest.mark.parametrize("shape", FOLD, ids=[f"n{s[0]}h{s[1]}c{s[3]}o{s[4]}k{s[5]}" for s in FOLD])
+def test_conv_fwd_bn_fold_matches_two_calls(shape):
+    from yolomi._lib import BnFold, ConvDesc, call, lib
+    n, h, w, cin, cout, k, p = shape
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, h, w, cout, k, 1, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * cin, cin, h * w * cout, cout
+    d.out_f32, d.accumulate = 2, 0
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, h, w, cin, generator=g).half().to(dev)
+    wt = (torch.randn(cout, k, k, cin, generator=g) * (2.0 / (cin * k * k)) ** 0.5).half().to(dev)
+    gamma = (1 + 0.1 * torch.randn(cout, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(cout, generator=g)).to(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
+    fused = lib().ym_conv_fwd_bn_fused(ctypes.byref(d))
+    assert fused == (0 if h == 20 else 1)
+
+    def run(fold):
+        z = torch.empty(n, h, w, cout, dtype=torch.float16, device=dev)
+        ss = torch.empty(rows, cout, device=dev)
+        sq = torch.empty(rows, cout, device=dev)
+        rm, rv = torch.zeros(cout, device=dev), torch.ones(cout, device=dev)
+        nbt = torch.zeros(1, dtype=torch.int64, device=dev)
+        out = torch.empty(4, cout, device=dev)
+        ws = torch.zeros(lib().ym_bn_workspace_size(cout), dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            if fold:
+                f = BnFold(gamma=gamma.data_ptr(), beta=beta.data_ptr(), running_mean=rm.data_ptr(),
+                           running_var=rv.data_ptr(), num_batches_tracked=nbt.data_ptr(), scale=out[0].data_ptr(),
+                           shift=out[1].data_ptr(), mean=out[2].data_ptr(), rstd=out[3].data_ptr(),
+                           workspace=ws.data_ptr(), count=float(n * h * w), momentum=0.03, eps=1e-3)
+                call("ym_conv_fwd_bn", ctypes.byref(d), x.data_ptr(), wt.data_ptr(), z.data_ptr(), ss.data_ptr(),
+                     sq.data_ptr(), ctypes.byref(f), st)
+            else:
+                call("ym_conv_fwd", ctypes.byref(d), x.data_ptr(), wt.data_ptr(), z.data_ptr(), None, ss.data_ptr(),
+                     sq.data_ptr(), st)
+                call("ym_bn_finalize", ss.data_ptr(), sq.data_ptr(), rows, cout, float(n * h * w), gamma.data_ptr(),
+                     beta.data_ptr(), rm.data_ptr(), rv.data_ptr(), nbt.data_ptr(), 0.03, 1e-3, out[0].data_ptr(),
+                     out[1].data_ptr(), out[2].data_ptr(), out[3].data_ptr(), ws.data_ptr(), st)
+        torch.cuda.synchronize()
+        return z, out, rm, rv, nbt, ws
+    z0, o0, rm0, rv0, n0, _ = run(False)
+    z1, o1, rm1, rv1, n1, ws1 = run(True)
+    assert torch.equal(z0, z1)
+    for a, b in ((o0, o1), (rm0, rm1), (rv0, rv1)):
+        assert float(((a - b).abs() / b.abs().clamp_min(1e-3)).max()) < 1e-6
+    assert int(n0) == int(n1) == 3
+    assert int(ws1[:256].view(torch.int32).abs().sum()) == 0          # every ticket re-armed

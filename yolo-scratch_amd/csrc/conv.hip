@@ -952,8 +952,12 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
     return gemm_stat_rows(int64_t(d->n) * d->oh * d->ow, select_n(d) * d->oh * d->ow, d->cout);
 }
 
+// ym_conv_fwd_bn's fold policy (ym_conv_set_fold): -1 default (on), 0 off, 1 on
+static int g_fold_mode = -1;
+
+// fold: the BatchNorm finalize as the pipelined kernel's tail (ym_conv_fwd_bn), null elsewhere
 static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
-                         float* stat_sum, float* stat_sq, void* stream) {
+                         float* stat_sum, float* stat_sq, void* stream, const ym_bn_fold* fold = nullptr) {
     YM_CHECK_ARG(d && x && w && y, "ym_conv_fwd: null argument");
     YM_CHECK_ARG(d->cin % 8 == 0, "ym_conv_fwd: Cin %% 8 != 0 (Cin=%d)", d->cin);
     YM_CHECK_ARG(d->k >= 1 && d->k <= 3, "ym_conv_fwd: kernel size %d unsupported (1..3)", d->k);
@@ -996,7 +1000,7 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     YM_CHECK_ARG(offsets_fit(d->x_bs, int64_t(d->oh) * d->ow), "ym_conv_fwd: input image stride too large");
     const PipePlan pp = pipe_plan(d, 0);
     if (pp.ok) {
-        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        pipe_launch(pp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream), fold);
         YM_LAUNCH_CHECK("ym_conv_fwd (pipe)");
         return YM_OK;
     }
@@ -1014,6 +1018,36 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
 extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
                            float* stat_sum, float* stat_sq, void* stream) {
     return conv_fwd_impl(d, x, w, y, bias, stat_sum, stat_sq, stream);
+}
+
+extern "C" int ym_conv_fwd_bn_fused(const ym_conv_desc* d) {
+    // the pipelined forward (bias-free, with statistics) folds the finalize into its tail; the kernels ahead of it
+    // in the selection (direct, halo-pipelined) and the rest run conv + ym_bn_finalize
+    if (!d || g_fold_mode == 0) return 0;
+    if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok) return 0;
+    return pipe_plan(d, 0).ok ? 1 : 0;
+}
+
+extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, float* stat_sum,
+                              float* stat_sq, const ym_bn_fold* bn, void* stream) {
+    YM_CHECK_ARG(d && bn && stat_sum && stat_sq, "ym_conv_fwd_bn: null argument");
+    YM_CHECK_ARG(bn->gamma && bn->beta && bn->scale && bn->shift && bn->mean && bn->rstd && bn->workspace,
+                 "ym_conv_fwd_bn: null BatchNorm argument");
+    YM_CHECK_ARG(bn->count > 0, "ym_conv_fwd_bn: count must be > 0");
+    YM_CHECK_ARG(d->cout <= 2048, "ym_conv_fwd_bn: Cout=%d > 2048", d->cout);
+    if (ym_conv_fwd_bn_fused(d)) return conv_fwd_impl(d, x, w, y, nullptr, stat_sum, stat_sq, stream, bn);
+    const int r = conv_fwd_impl(d, x, w, y, nullptr, stat_sum, stat_sq, stream);
+    if (r != YM_OK) return r;
+    return ym_bn_finalize(stat_sum, stat_sq, ym_conv_fwd_stat_rows(d), d->cout, bn->count, bn->gamma, bn->beta,
+                          bn->running_mean, bn->running_var, bn->num_batches_tracked, bn->momentum, bn->eps,
+                          bn->scale, bn->shift, bn->mean, bn->rstd, bn->workspace, stream);
+}
+
+extern "C" int ym_conv_set_fold(int mode) {
+    // ym_conv_fwd_bn's fold policy: -1 default (on), 0 off, 1 on; returns the previous setting
+    const int prev = g_fold_mode;
+    g_fold_mode = mode < -1 || mode > 1 ? -1 : mode;
+    return prev;
 }
 
 extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream) {

@@ -44,6 +44,13 @@ class BnEvalEntry(ctypes.Structure):
                 ("c", I32), ("eps", _c.c_float)]
 
 
+class BnFold(ctypes.Structure):
+    """ym_bn_fold (include/yolomi.h)."""
+    _fields_ = [("gamma", P), ("beta", P), ("running_mean", P), ("running_var", P), ("num_batches_tracked", P),
+                ("scale", P), ("shift", P), ("mean", P), ("rstd", P), ("workspace", P), ("count", F64),
+                ("momentum", _c.c_float), ("eps", _c.c_float)]
+
+
 R = _c.c_int
 # name -> (restype, argtypes); must match include/yolomi.h
 SIGNATURES = {
@@ -76,6 +83,9 @@ SIGNATURES = {
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
     "ym_bn_workspace_size": (SZ, [INT]),
+    "ym_conv_fwd_bn_fused": (R, [P]),
+    "ym_conv_fwd_bn": (R, [P, P, P, P, P, P, P, P]),
+    "ym_conv_set_fold": (R, [INT]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
     "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
     "ym_bn_eval_coeff_batch": (R, [P, INT, P]),

@@ -24,7 +24,7 @@ import weakref
 import numpy as np
 import torch
 
-from ._lib import BnEvalEntry, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
+from ._lib import BnEvalEntry, BnFold, ConvDesc, WPrepEntry, YolomiError, call, lib, stream_ptr
 
 BF16 = torch.bfloat16
 F16 = torch.float16
@@ -256,17 +256,44 @@ class ConvBN:
             a = self._sa = (bnv, ss, sq, apply)
         return a
 
-    def _bn_fwd(self, plan, st, ss, sq):
+    def _fused(self, plan):
+        """Whether the training forward runs ym_conv_fwd_bn with the BatchNorm finalize folded into the conv
+        launch's tail (the pipelined forward; YM_FOLD=0: conv, then ym_bn_finalize, as for the other kernels)."""
+        f = self.__dict__.get("_fused_c")
+        if f is None:
+            f = self._fused_c = (os.environ.get("YM_FOLD", "1") != "0"
+                                 and bool(lib().ym_conv_fwd_bn_fused(ctypes.byref(self.desc))))
+        return f
+
+    def _fold(self, plan):
+        """ym_bn_fold argument of this layer; the BatchNorm parameters are looked up per call (a replaced
+        Parameter or buffer is seen), the struct rebuilt only when one of them changed."""
+        bn = self.m.bn
+        (sc, sh, mu, rs), _, _, _ = self._static_args(plan)
+        key = (_p(bn.weight), _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
+               plan.bn_ws.data_ptr(), float(bn.momentum), float(bn.eps))
+        f = self.__dict__.get("_fold_s")
+        if f is None or f[0] != key:
+            fs = BnFold(gamma=key[0], beta=key[1], running_mean=key[2], running_var=key[3],
+                        num_batches_tracked=key[4], scale=sc, shift=sh, mean=mu, rstd=rs, workspace=key[5],
+                        count=float(self.M), momentum=key[6], eps=key[7])
+            f = self._fold_s = (key, fs, ctypes.byref(fs))
+        return f[2]
+
+    def _bn_fwd(self, plan, st, ss, sq, finalize=True):
         """BatchNorm finalize + apply (+ SiLU, + residual) of the forward: 'bn' family, algorithmic bytes
-        = the partial rows read + z read + y written (+ residual read)."""
+        = the partial rows read + z read + y written (+ residual read).  finalize=False: the conv launch
+        already folded the statistics (ym_conv_fwd_bn), only the apply pass runs here."""
         bn = self.m.bn
         (sc, sh, mu, rs), ssp, sqp, apply = self._static_args(plan)
         r = self.res
         e = self.M * self.co * 2
-        work = 8 * self.G * self.co * (1 if plan.training else 0) + 2 * e + (e if r else 0)
+        work = 8 * self.G * self.co * (1 if plan.training and finalize else 0) + 2 * e + (e if r else 0)
 
         def run():
-            if plan.training:
+            if plan.training and not finalize:
+                pass
+            elif plan.training:
                 call("ym_bn_finalize", ssp, sqp, self.G, self.co, float(self.M), _p(bn.weight),
                      _p(bn.bias), _p(bn.running_mean), _p(bn.running_var), _p(bn.num_batches_tracked),
                      float(bn.momentum), float(bn.eps), sc, sh, mu, rs, plan.bn_ws.data_ptr(), st)
@@ -282,6 +309,12 @@ class ConvBN:
         if conv is None:
             conv = self._sc = (ctypes.byref(self.desc), self.x.ptr(), self.wf.data_ptr(), self.z.data_ptr(), None,
                                ss.data_ptr() if plan.training else None, sq.data_ptr() if plan.training else None)
+        if plan.training and self._fused(plan):
+            fold = self._fold(plan)
+            self._timed(plan, "fwd", plan._cur_stream,
+                        lambda: call("ym_conv_fwd_bn", conv[0], conv[1], conv[2], conv[3], conv[5], conv[6], fold, st))
+            self._bn_fwd(plan, st, ss, sq, finalize=False)
+            return
         self._timed(plan, "fwd", plan._cur_stream, lambda: call("ym_conv_fwd", *conv, st))
         self._bn_fwd(plan, st, ss, sq)
 
