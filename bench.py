@@ -13,7 +13,8 @@ directly, in which case this process starts torchrun with N ranks as a child and
 Rank 0 prints ONE JSON line.  `roofline` is the dense 3x3 conv family against the 16-bit MFMA peak
 (the north star's target: every fwd / dgrad / wgrad launch of a k=3 Conv block bracketed with HIP
 events on its launch stream, in a pass that runs all launches on one stream, algorithmic FLOPs
-summed / durations summed); `roofline_families` gives the same for every conv forward, data-gradient,
+summed / durations summed; in that pass the forward BatchNorm finalize is its own launch, not the conv
+launch's tail as in the timed steps); `roofline_families` gives the same for every conv forward, data-gradient,
 weight-gradient launch and the BatchNorm passes (HBM); `roofline_probe` is the heaviest single conv
 launch; `roofline_step` prices the whole step against the MFMA peak.  `traffic` fields are read from
 the committed counter passes (profiles/traffic.json, labelled with their source and commit), not
@@ -314,6 +315,11 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    # the probe and family passes time the conv kernels' own work: there the forward BatchNorm finalize runs as its
+    # own launch (YM_FOLD=0, timed in the 'bn' family) instead of as the conv launch's tail (the timed region above
+    # and the driver's step run it folded)
+    saved_fold = os.environ.get("YM_FOLD")
+    os.environ["YM_FOLD"] = "0"
     plan.probe, plan.probe_events = dom, []
     for i in range(PROBE_STEPS):
         step(args.warmup + args.steps + i)
@@ -340,6 +346,10 @@ def main():
         work = sum(w for _, _, w in evs) / PROBE_STEPS
         fams[kind] = (ms, work, len(evs) // PROBE_STEPS)
     plan.family_events = None
+    if saved_fold is None:
+        os.environ.pop("YM_FOLD", None)
+    else:
+        os.environ["YM_FOLD"] = saved_fold
     # host time to enqueue one step (Python + ctypes launches) vs its wall time: a step whose
     # enqueue time approaches its wall time leaves the GPU waiting on the host
     host = []
@@ -409,7 +419,7 @@ def main():
                          f"fwd + dgrad, "
                          f"wgrad3 + split-K reduce): {c3_n} launches per step, {c3_flop / 1e9:.0f} GFLOP algorithmic "
                          f"in {c3_ms:.3f} ms summed launch time (HIP events on the launch stream, all launches on "
-                         f"one stream, {PROBE_STEPS} steps)",
+                         f"one stream, {PROBE_STEPS} steps, the forward BN finalize as its own launch)",
                "per_direction_frac": {k[:-1]: round(fam_rate(k)[1], 4) for k in ("fwd3", "dgrad3", "wgrad3")}}
     names = {"fwd": "conv forward (pipelined / halo / implicit-GEMM / direct kernels)",
              "dgrad": "conv data gradient (pipelined / halo / implicit-GEMM / direct kernels)",

@@ -461,7 +461,7 @@ def test_conv_fwd_bias_on_every_policy(k, out_f32):
     assert err < (2e-3 if out_f32 == 2 else 1e-2), err
 
 
-# ym_conv_fwd_bn: conv forward + BatchNorm finalize, the finalize folded into the pipelined kernel's tail where
+# ym_conv_fwd_bn: conv forward + BatchNorm finalize, the finalize folded into the pipelined / halo kernel's tail where
 # ym_conv_fwd_bn_fused says so (tickets per channel tile, fixed-order fp64 fold), else conv + ym_bn_finalize.
 # Both against the two-call path (ym_conv_fwd, ym_bn_finalize): z bit-identical, the coefficients and running
 # statistics to 1e-6 (the fold order differs), num_batches_tracked +1 exactly; three calls in a row (the tickets
@@ -470,7 +470,9 @@ FOLD = [
     (16, 64, 64, 128, 128, 3, 1),      # pipe 256x128, one channel tile, fused
     (16, 64, 64, 256, 192, 1, 0),      # pipe 1x1, 2 channel tiles (192 = 128 + 64), fused
     (16, 128, 128, 64, 128, 3, 1),     # stride 1 128-channel: pipe
-    (2, 20, 20, 128, 128, 3, 1),       # small map: halo kernel, not fused (conv + finalize)
+    (2, 20, 20, 128, 128, 3, 1),       # small map: halo-staged kernel (C8), fused
+    (3, 20, 20, 64, 64, 3, 1),         # halo C4 (64-channel tiles), fused
+    (2, 20, 20, 256, 128, 1, 0),       # small 1x1: 2-stage implicit GEMM, not fused (conv + finalize)
 ]
 
 
@@ -491,7 +493,7 @@ def test_conv_fwd_bn_fold_matches_two_calls(shape):
     st = torch.cuda.current_stream().cuda_stream
     rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
     fused = lib().ym_conv_fwd_bn_fused(ctypes.byref(d))
-    assert fused == (0 if h == 20 else 1)
+    assert fused == (0 if k == 1 and h == 20 else 1)
 
     def run(fold):
         z = torch.empty(n, h, w, cout, dtype=torch.float16, device=dev)

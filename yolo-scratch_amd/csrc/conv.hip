@@ -1006,7 +1006,7 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
     }
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) {
-        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream));
+        halo_launch(hp, d, 0, x, w, y, bias, stat_sum, stat_sq, as_stream(stream), fold);
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
@@ -1021,11 +1021,11 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
 }
 
 extern "C" int ym_conv_fwd_bn_fused(const ym_conv_desc* d) {
-    // the pipelined forward (bias-free, with statistics) folds the finalize into its tail; the kernels ahead of it
-    // in the selection (direct, halo-pipelined) and the rest run conv + ym_bn_finalize
+    // the pipelined and halo-staged forwards (bias-free, with statistics) fold the finalize into their tail; the
+    // direct, halo-pipelined and 2-stage GEMM forwards run conv + ym_bn_finalize
     if (!d || g_fold_mode == 0) return 0;
     if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok) return 0;
-    return pipe_plan(d, 0).ok ? 1 : 0;
+    return pipe_plan(d, 0).ok || halo_plan(d, 0).ok ? 1 : 0;
 }
 
 extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, float* stat_sum,

@@ -24,6 +24,7 @@
 #include "common.h"
 #include "conv_epi.h"
 #include "conv_halo.h"
+#include "bn_fold.h"
 #include "tile.h"
 
 namespace ym {
@@ -45,6 +46,7 @@ struct HaloArgs {
     int ntiles;
     int out_mode, accumulate;                 // out_mode: 0 bf16, 1 fp32, 2 fp16
     int ep_lds;                               // 16-bit output via the register-transposed epilogue (conv_epi.h)
+    BnFoldArgs fold;                          // BatchNorm finalize as the tail (ym_conv_fwd_bn); gamma null = off
 };
 
 // 64-B LDS rows (32 channels): row r's 16-B chunk c lives in slot c ^ F(r), F(r) = 2 * ((r >> 2) & 1).
@@ -357,10 +359,11 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WPX; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                a.st_sum[int64_t(blockIdx.x) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(blockIdx.x) * a.Nout + ch] = pq;
+                stat_store(&a.st_sum[int64_t(blockIdx.x) * a.Nout + ch], ps, a.fold.gamma != nullptr);
+                stat_store(&a.st_sq[int64_t(blockIdx.x) * a.Nout + ch], pq, a.fold.gamma != nullptr);
             }
         }
+        if (a.fold.gamma) bn_fold_tail<BN, NT>(a.fold, a.st_sum, a.st_sq, a.Nout, int(blockIdx.y), int(gridDim.x), smem);
     }
 }
 
@@ -431,7 +434,7 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, hipStream_t st) {
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold) {
     HaloArgs a{};
     a.x = x;
     a.w = w;
@@ -455,6 +458,7 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     a.ep_lds = !bias && a.out_mode != 1 && a.y_ld % 8 == 0 && a.y_bs % 8 == 0 &&
                int64_t(d->n) * a.y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
+    if (!dgrad && st_sum) a.fold = bn_fold_args(fold);
     const dim3 grid(p.gx, p.nco);
     if (p.cfg == 0) {
         if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_DGRAD>), grid, dim3(512), 0, st, a);

@@ -32,6 +32,7 @@
 #include "common.h"
 #include "conv_epi.h"
 #include "conv_pipe.h"
+#include "bn_fold.h"
 #include "tile.h"
 
 namespace ym {
@@ -60,13 +61,7 @@ struct PipeArgs {
     int ntiles;                               // channel tiles
     int mt_pre[5];                            // first m-tile of each class (prefix), mt_pre[ncls] = total
     int ncls;
-    // BatchNorm finalize as the tail (ym_conv_fwd_bn): f_gamma null = off
-    const float* f_gamma; const float* f_beta;
-    float* f_rm; float* f_rv; int64_t* f_nbt;
-    float* f_scale; float* f_shift; float* f_mean; float* f_rstd;
-    unsigned* f_cnt;                          // one ticket per channel tile (the BN workspace's counters)
-    double f_count;
-    float f_mom, f_eps;
+    BnFoldArgs fold;                          // BatchNorm finalize as the tail (ym_conv_fwd_bn); gamma null = off
 };
 
 struct Cls {
@@ -138,78 +133,6 @@ __device__ __forceinline__ void step_barrier() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-}
-
-// BatchNorm finalize as the tail of a forward launch (ym_conv_fwd_bn): every workgroup of channel tile nt has
-// published its statistics row write-through; after its stores drained (vmcnt(0)) and a workgroup barrier, one
-// lane takes an agent-scope ticket; the workgroup that takes the last one (rows - 1) folds the tile's rows in
-// fp64 in a fixed order (THREADS / BN row subsets, then in subset order) and writes what ym_bn_finalize
-// writes for those channels, then re-arms the ticket.  The hand-off (the pattern of bn.hip's finalize) costs
-// the launch's tail a few us instead of a second launch.
-template <int BN, int THREADS>
-__device__ __forceinline__ void bn_fold_tail(const PipeArgs& a, int nt, int rows, char* smem) {
-    constexpr int K = THREADS / BN;
-    static_assert(K >= 1 && THREADS % BN == 0, "fold geometry");
-    __shared__ int last_sh;
-    const int tid = threadIdx.x;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned t = __hip_atomic_fetch_add(&a.f_cnt[nt], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last_sh = t == unsigned(rows - 1);
-    }
-    __syncthreads();
-    if (!last_sh) return;
-    double (*part)[2][BN] = reinterpret_cast<double (*)[2][BN]>(smem);      // [K][sum|sq][channel]
-    const int cl = tid % BN, k = tid / BN, ch = nt * BN + cl;
-    double s = 0.0, q = 0.0;
-    if (ch < a.Nout) {
-        // 8 rows' loads in flight per step (the fold is latency-bound: one workgroup, L2 round trips)
-        int r = k;
-        for (; r + 7 * K < rows; r += 8 * K) {
-            float vs[8], vq[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                vs[u] = __hip_atomic_load(&a.st_sum[int64_t(r + u * K) * a.Nout + ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                vq[u] = __hip_atomic_load(&a.st_sq[int64_t(r + u * K) * a.Nout + ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                s += double(vs[u]);
-                q += double(vq[u]);
-            }
-        }
-        for (; r < rows; r += K) {
-            s += double(__hip_atomic_load(&a.st_sum[int64_t(r) * a.Nout + ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            q += double(__hip_atomic_load(&a.st_sq[int64_t(r) * a.Nout + ch], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        }
-    }
-    part[k][0][cl] = s;
-    part[k][1][cl] = q;
-    __syncthreads();
-    if (tid == 0) a.f_cnt[nt] = 0u;                // re-armed for the next launch (same stream)
-    if (k != 0 || ch >= a.Nout) return;
-    s = 0.0;
-    q = 0.0;
-    for (int j = 0; j < K; ++j) {
-        s += part[j][0][cl];
-        q += part[j][1][cl];
-    }
-    if (a.f_nbt && nt == 0 && cl == 0) *a.f_nbt += 1;
-    const double mu = s / a.f_count;
-    double var = q / a.f_count - mu * mu;
-    if (var < 0) var = 0;
-    const double rstd = 1.0 / sqrt(var + double(a.f_eps));
-    const float sc = float(double(a.f_gamma[ch]) * rstd);
-    a.f_scale[ch] = sc;
-    a.f_shift[ch] = float(double(a.f_beta[ch]) - mu * double(sc));
-    a.f_mean[ch] = float(mu);
-    a.f_rstd[ch] = float(rstd);
-    if (a.f_rm) {
-        const double unb = a.f_count > 1 ? var * a.f_count / (a.f_count - 1) : var;
-        a.f_rm[ch] = float((1.0 - a.f_mom) * a.f_rm[ch] + a.f_mom * mu);
-        a.f_rv[ch] = float((1.0 - a.f_mom) * a.f_rv[ch] + a.f_mom * unb);
-    }
 }
 
 // issue side of the stage stream: which tile / tap / 64-channel chunk the next LDS-DMA stage
@@ -534,16 +457,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][cl]; pq += red[1][w][cl]; }
-                if (a.f_gamma) {                // published write-through for the tail's fold
-                    __hip_atomic_store(&a.st_sum[int64_t(row) * a.Nout + ch], ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(&a.st_sq[int64_t(row) * a.Nout + ch], pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    a.st_sum[int64_t(row) * a.Nout + ch] = ps;
-                    a.st_sq[int64_t(row) * a.Nout + ch] = pq;
-                }
+                stat_store(&a.st_sum[int64_t(row) * a.Nout + ch], ps, a.fold.gamma != nullptr);
+                stat_store(&a.st_sq[int64_t(row) * a.Nout + ch], pq, a.fold.gamma != nullptr);
             }
         }
-        if (a.f_gamma) bn_fold_tail<BN, NW * 64>(a, nt, int(gridDim.x) / a.ntiles, smem);
+        if (a.fold.gamma) bn_fold_tail<BN, NW * 64>(a.fold, a.st_sum, a.st_sq, a.Nout, nt, int(gridDim.x) / a.ntiles, smem);
     }
 }
 
@@ -647,13 +565,7 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
         acc += int((int64_t(a.N) * ohc * owc + bm - 1) / bm);
     }
     a.mt_pre[a.ncls] = acc;
-    if (fold && !dgrad && st_sum) {
-        a.f_gamma = fold->gamma; a.f_beta = fold->beta;
-        a.f_rm = fold->running_mean; a.f_rv = fold->running_var; a.f_nbt = fold->num_batches_tracked;
-        a.f_scale = fold->scale; a.f_shift = fold->shift; a.f_mean = fold->mean; a.f_rstd = fold->rstd;
-        a.f_cnt = static_cast<unsigned*>(fold->workspace);
-        a.f_count = fold->count; a.f_mom = fold->momentum; a.f_eps = fold->eps;
-    }
+    if (!dgrad && st_sum) a.fold = bn_fold_args(fold);
     launch_cfg(dgrad ? PD : PF, p.cfg, a, p.grid, st);
     return YM_OK;
 }

@@ -259,10 +259,11 @@ class ConvBN:
     def _fused(self, plan):
         """Whether the training forward runs ym_conv_fwd_bn with the BatchNorm finalize folded into the conv
         launch's tail (the pipelined forward; YM_FOLD=0: conv, then ym_bn_finalize, as for the other kernels)."""
+        if os.environ.get("YM_FOLD", "1") == "0":
+            return False
         f = self.__dict__.get("_fused_c")
         if f is None:
-            f = self._fused_c = (os.environ.get("YM_FOLD", "1") != "0"
-                                 and bool(lib().ym_conv_fwd_bn_fused(ctypes.byref(self.desc))))
+            f = self._fused_c = bool(lib().ym_conv_fwd_bn_fused(ctypes.byref(self.desc)))
         return f
 
     def _fold(self, plan):
