@@ -472,7 +472,8 @@ FOLD = [
     (16, 128, 128, 64, 128, 3, 1),     # stride 1 128-channel: pipe
     (2, 20, 20, 128, 128, 3, 1),       # small map: halo-staged kernel (C8), fused
     (3, 20, 20, 64, 64, 3, 1),         # halo C4 (64-channel tiles), fused
-    (2, 20, 20, 256, 128, 1, 0),       # small 1x1: 2-stage implicit GEMM, not fused (conv + finalize)
+    (2, 20, 20, 256, 128, 1, 0),       # small 1x1: 2-stage implicit GEMM, fused
+    (24, 80, 80, 64, 64, 3, 1),        # halo-pipelined 64 -> 64 (weights resident, >= 512 tiles): not fused
 ]
 
 
@@ -493,7 +494,7 @@ def test_conv_fwd_bn_fold_matches_two_calls(shape):
     st = torch.cuda.current_stream().cuda_stream
     rows = lib().ym_conv_fwd_stat_rows(ctypes.byref(d))
     fused = lib().ym_conv_fwd_bn_fused(ctypes.byref(d))
-    assert fused == (0 if k == 1 and h == 20 else 1)
+    assert fused == (0 if cin == 64 and h == 80 else 1)
 
     def run(fold):
         z = torch.empty(n, h, w, cout, dtype=torch.float16, device=dev)

@@ -33,6 +33,7 @@
 #include "conv_halo.h"
 #include "conv_hpipe.h"
 #include "conv_pipe.h"
+#include "bn_fold.h"
 #include "reduce.h"
 #include "tile.h"
 
@@ -60,6 +61,7 @@ struct GemmArgs {
     int ostep;                               // 2: dgrad of a stride-2 conv, one output parity class per blockIdx.z
     int ntl;                                 // channel tiles interleaved into grid x (0: they are grid y)
     int ep_lds;                              // data gradient: LDS-transposed 16-B epilogue (conv_epi.h)
+    BnFoldArgs fold;                         // BatchNorm finalize as the tail (ym_conv_fwd_bn); gamma null = off
 };
 
 // LDS images are lane-linear (LDS-DMA writes lane l of a wave-instruction at base + 16*l): 128-B
@@ -398,10 +400,11 @@ conv_gemm_kernel(GemmArgs a) {
                 float ps = 0.f, pq = 0.f;
 #pragma unroll
                 for (int w = 0; w < WN; ++w) { ps += red[0][w][c]; pq += red[1][w][c]; }
-                a.st_sum[int64_t(bx) * a.Nout + ch] = ps;
-                a.st_sq[int64_t(bx) * a.Nout + ch] = pq;
+                stat_store(&a.st_sum[int64_t(bx) * a.Nout + ch], ps, a.fold.gamma != nullptr);
+                stat_store(&a.st_sq[int64_t(bx) * a.Nout + ch], pq, a.fold.gamma != nullptr);
             }
         }
+        if (a.fold.gamma) bn_fold_tail<BN, NT>(a.fold, a.st_sum, a.st_sq, a.Nout, nt, gxx, smem);
     }
 }
 
@@ -1010,6 +1013,7 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
         YM_LAUNCH_CHECK("ym_conv_fwd (halo)");
         return YM_OK;
     }
+    if (stat_sum) a.fold = bn_fold_args(fold);
     pick_and_launch(a, MODE_FWD, FWD_STAT_BLOCKS, select_n(d), as_stream(stream));
     YM_LAUNCH_CHECK("ym_conv_fwd");
     return YM_OK;
@@ -1021,11 +1025,11 @@ extern "C" int ym_conv_fwd(const ym_conv_desc* d, const uint16_t* x, const uint1
 }
 
 extern "C" int ym_conv_fwd_bn_fused(const ym_conv_desc* d) {
-    // the pipelined and halo-staged forwards (bias-free, with statistics) fold the finalize into their tail; the
-    // direct, halo-pipelined and 2-stage GEMM forwards run conv + ym_bn_finalize
+    // the pipelined, halo-staged and 2-stage GEMM forwards (bias-free, with statistics) fold the finalize into
+    // their tail; the direct and halo-pipelined forwards run conv + ym_bn_finalize
     if (!d || g_fold_mode == 0) return 0;
     if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok) return 0;
-    return pipe_plan(d, 0).ok || halo_plan(d, 0).ok ? 1 : 0;
+    return 1;
 }
 
 extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, float* stat_sum,
