@@ -31,6 +31,7 @@ PEAK_TF = 2500.0
 CONV = r"conv_(direct|direct_quad|hpipe|pipe|halo|gemm)_kernel"
 EXPECT = {
     "ym_conv_fwd": [CONV],
+    "ym_conv_fwd_bn": [CONV],
     "ym_conv_dgrad": [CONV],
     "ym_conv_wgrad": [r"wgrad(3|1|_generic)_kernel", r"wgrad_reduce_kernel"],
     "ym_bn_finalize": [r"bn_finalize_fused_kernel"],
@@ -70,7 +71,8 @@ def record(out, steps=2, warmup=3):
         opt.step()
     for _ in range(warmup):
         step()
-    os.environ.update(YM_STREAMS="1", YM_SIDE_STREAM="0")
+    # one stream, and the forward BatchNorm finalize as its own launch (as bench.py's family pass times it)
+    os.environ.update(YM_STREAMS="1", YM_SIDE_STREAM="0", YM_FOLD="0")
     for _ in range(steps - 1):
         step()
     plan = model.__dict__["_ym_last_plan"]
@@ -143,7 +145,7 @@ def join(trace, calls_json):
     for c, us, kn in mapped:
         call = c["call"]
         if call.startswith("ym_conv") and c.get("type") == "ConvBN":
-            dr = {"ym_conv_fwd": "fwd", "ym_conv_dgrad": "dgrad", "ym_conv_wgrad": "wgrad"}[call]
+            dr = {"ym_conv_fwd": "fwd", "ym_conv_fwd_bn": "fwd", "ym_conv_dgrad": "dgrad", "ym_conv_wgrad": "wgrad"}[call]
             fl = c["flops"]
             tf = fl / (us * 1e-6) / 1e12
             print(f"{c['op']:4d} {dr:>5} {c['k']} {c['s']} {c['ci']:4d} {c['co']:4d} {c['out'][0]:3d}x{c['out'][1]:<3d} "
