@@ -84,3 +84,57 @@ def test_bn_bwd_finalize_vs_host_fp64(G, C):
         np.testing.assert_allclose(coef[0].double().cpu(), (gamma * rstd).double().cpu(), rtol=1e-6)
         np.testing.assert_allclose(coef[1].double().cpu(), s / count, rtol=1e-5, atol=1e-9)
         np.testing.assert_allclose(coef[2].double().cpu(), q / count, rtol=1e-5, atol=1e-9)
+
+
+# ym_bn_bwd_reduce_fold: the backward statistics and finalize in one launch on the small maps (the last workgroup of
+# each 64-channel group folds its rows) against the two launches it replaces: dgamma / dbeta (overwrite, then
+# accumulate) and the apply coefficients to 1e-6, three calls in a row (tickets re-armed), SiLU on and off,
+# a channel-slice view of dy; a map past the size limit falls back to the two launches.
+@pytest.mark.parametrize("m,c,act,extra", [(25600, 128, 1, 0), (400 * 7, 512, 1, 64), (102400, 64, 0, 0),
+                                           (200000, 128, 1, 0)])
+def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra):
+    import ctypes
+    from yolomi._lib import call, lib
+    dev = torch.device("cuda", 0)
+    g = torch.Generator().manual_seed(c + m)
+    hw = 400 if m % 400 == 0 else m
+    z = torch.randn(m, c, generator=g).half().to(dev)
+    dyb = torch.zeros(m, c + extra, dtype=torch.bfloat16, device=dev)
+    dyb[:, :c] = torch.randn(m, c, generator=g).bfloat16().to(dev)
+    scale = (1 + 0.1 * torch.randn(c, generator=g)).to(dev)
+    shift = (0.1 * torch.randn(c, generator=g)).to(dev)
+    mean = (0.05 * torch.randn(c, generator=g)).to(dev)
+    rstd = (1 + 0.1 * torch.rand(c, generator=g)).to(dev)
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).to(dev)
+    Gb = lib().ym_bn_bwd_blocks(m, c)
+    assert lib().ym_bn_bwd_fold_ok(m, c) == (1 if m <= 25600 else 0)
+    st = torch.cuda.current_stream().cuda_stream
+    d_bs, d_ld = hw * (c + extra), c + extra
+
+    def run(fused):
+        ps, pg = torch.empty(Gb, c, device=dev), torch.empty(Gb, c, device=dev)
+        dg, db = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+        coef = torch.empty(3, c, device=dev)
+        ws = torch.zeros(lib().ym_bn_workspace_size(c), dtype=torch.uint8, device=dev)
+        outs = []
+        for acc in (0, 1, 1):
+            if fused:
+                call("ym_bn_bwd_reduce_fold", dyb.data_ptr(), d_bs, d_ld, z.data_ptr(), m, c, hw, scale.data_ptr(),
+                     shift.data_ptr(), mean.data_ptr(), rstd.data_ptr(), act, ps.data_ptr(), pg.data_ptr(),
+                     gamma.data_ptr(), dg.data_ptr(), db.data_ptr(), acc, coef.data_ptr(), ws.data_ptr(), st)
+            else:
+                call("ym_bn_bwd_reduce", dyb.data_ptr(), d_bs, d_ld, z.data_ptr(), m, c, hw, scale.data_ptr(),
+                     shift.data_ptr(), mean.data_ptr(), rstd.data_ptr(), act, ps.data_ptr(), pg.data_ptr(), st)
+                call("ym_bn_bwd_finalize", ps.data_ptr(), pg.data_ptr(), Gb, c, float(m), gamma.data_ptr(),
+                     rstd.data_ptr(), dg.data_ptr(), db.data_ptr(), acc, coef.data_ptr(), ws.data_ptr(), st)
+            torch.cuda.synchronize()
+            outs.append((dg.clone(), db.clone(), coef.clone()))
+        assert int(ws[:256].view(torch.int32).abs().sum()) == 0
+        return outs
+    ref, got = run(False), run(True)
+    for (a1, b1, c1), (a2, b2, c2) in zip(ref, got):
+        for x, y in ((a1, a2), (b1, b2), (c1, c2)):
+            # different fp32 partial groupings of the same sums: relative to the sum's magnitude (a channel's
+            # sum can cancel to ~0, so the floor is 1 % of the largest channel's)
+            err = float(((x - y).abs() / (y.abs() + 1e-2 * y.abs().max())).max())
+            assert err < 1e-4, err

@@ -371,6 +371,121 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     }
 }
 
+// BatchNorm backward statistics AND finalize in one launch for the small maps (ym_bn_bwd_reduce_fold): grid
+// (FOLD_GP pixel blocks, C / 64 channel groups), 256 threads = 8 lanes of 8 channels x 32 pixel rows.  Each
+// workgroup reduces its rows for its 64 channels, publishes one partial row write-through, takes an agent-scope
+// ticket of its channel group; the last workgroup of the group folds the group's FOLD_GP rows in fp64 in a fixed
+// order (4 row subsets, 8 rows' loads in flight) and writes what ym_bn_bwd_finalize writes (dgamma, dbeta,
+// the apply coefficients) for those channels, then re-arms the ticket.  The partial rows of a group are few
+// (FOLD_GP = 64): the fold is 8 K loads, where one folding workgroup over the streaming kernel's 512 full-width
+// rows would be latency-bound for tens of us.
+constexpr int FOLD_GP = 64;
+
+__global__ void __launch_bounds__(256) bn_bwd_reduce_fold_kernel(
+    const bf16_t* __restrict__ dy, int64_t d_ld, const bf16_t* __restrict__ z, int64_t M, int C,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ mean,
+    const float* __restrict__ rstd, int act, float* ps, float* pg, const float* __restrict__ gamma, float* dgamma,
+    float* dbeta, int accumulate, float* coef, unsigned* cnt, double count) {
+    __shared__ float red[2][32][64];
+    __shared__ double part[4][2][64];
+    __shared__ int last_sh;
+    const int tid = threadIdx.x, lg = tid & 7, r = tid >> 3;
+    const int cg = blockIdx.y, c0 = cg * 64 + lg * 8;
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    {
+        float sc[8], sf[8], mu[8], rs[8];
+        load8(scale + c0, sc);
+        load8(shift + c0, sf);
+        load8(mean + c0, mu);
+        load8(rstd + c0, rs);
+        const int64_t step = int64_t(gridDim.x) * 32;
+        for (int64_t m = int64_t(blockIdx.x) * 32 + r; m < M; m += 2 * step) {
+            const int64_t m2 = m + step;
+            const bool two = m2 < M;
+            uint4 zr[2], dr[2];
+            zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
+            dr[0] = *reinterpret_cast<const uint4*>(dy + m * d_ld + c0);
+            if (two) {
+                zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
+                dr[1] = *reinterpret_cast<const uint4*>(dy + m2 * d_ld + c0);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (u == 1 && !two) break;
+                float zv[8], dv[8];
+                unpack8h(zr[u], zv);
+                unpack8(dr[u], dv);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float gg = act ? dv[k] * dsilu(zv[k] * sc[k] + sf[k]) : dv[k];
+                    s[k] += gg;
+                    sx[k] += gg * ((zv[k] - mu[k]) * rs[k]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        red[0][r][lg * 8 + k] = s[k];
+        red[1][r][lg * 8 + k] = sx[k];
+    }
+    __syncthreads();
+    if (tid < 64) {
+        float a = 0.f, b = 0.f;
+        for (int j = 0; j < 32; ++j) {
+            a += red[0][j][tid];
+            b += red[1][j][tid];
+        }
+        __hip_atomic_store(&ps[int64_t(blockIdx.x) * C + cg * 64 + tid], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&pg[int64_t(blockIdx.x) * C + cg * 64 + tid], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned t = __hip_atomic_fetch_add(&cnt[cg], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last_sh = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last_sh) return;
+    // fold: thread (k = tid / 64, cl = tid % 64) sums rows k, k + 4, ... with 8 rows' loads in flight
+    const int cl = tid & 63, k = tid >> 6, ch = cg * 64 + cl;
+    const int rows = int(gridDim.x);
+    auto ld = [&](const float* p, int row) {
+        return __hip_atomic_load(const_cast<float*>(p) + int64_t(row) * C + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    double fs = 0.0, fq = 0.0;
+    int row = k;
+    for (; row + 28 < rows; row += 32) {
+        float vs[8], vq[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            vs[u] = ld(ps, row + 4 * u);
+            vq[u] = ld(pg, row + 4 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            fs += double(vs[u]);
+            fq += double(vq[u]);
+        }
+    }
+    for (; row < rows; row += 4) {
+        fs += double(ld(ps, row));
+        fq += double(ld(pg, row));
+    }
+    part[k][0][cl] = fs;
+    part[k][1][cl] = fq;
+    __syncthreads();
+    if (tid == 0) cnt[cg] = 0u;                    // re-armed for the next launch (same stream)
+    if (k != 0) return;
+    const double sum = (part[0][0][cl] + part[1][0][cl]) + (part[2][0][cl] + part[3][0][cl]);
+    const double dot = (part[0][1][cl] + part[1][1][cl]) + (part[2][1][cl] + part[3][1][cl]);
+    if (dgamma) dgamma[ch] = float(accumulate ? dgamma[ch] + dot : dot);
+    if (dbeta) dbeta[ch] = float(accumulate ? dbeta[ch] + sum : sum);
+    coef[ch] = gamma[ch] * rstd[ch];
+    coef[C + ch] = float(sum / count);
+    coef[2 * C + ch] = float(dot / count);
+}
+
 constexpr int RED_R = 32;   // level-1 row splits of the partials reduction
 
 // grid caps of the streaming kernels (measured in the training step: 2048 / 512 with the conv forward's
@@ -469,6 +584,47 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
                        part_dot, parts, c, RED_R, count, p2, cnt, gamma, nullptr, nullptr, nullptr, nullptr, 0.f,
                        0.f, nullptr, nullptr, nullptr, nullptr, rstd, dgamma, dbeta, accumulate, coef);
     YM_LAUNCH_CHECK("ym_bn_bwd_finalize");
+    return YM_OK;
+}
+
+// fused backward statistics + finalize policy (ym_bn_set_bwd_fold): -1 default (on), 0 off, 1 on
+static int g_bwd_fold = -1;
+// the maps it takes: whole 64-channel groups and at most 40x40 x 64 images of pixels (FOLD_GP workgroups per
+// group stream the tensor; on the larger maps the streaming kernel's 512 full-width workgroups win)
+static constexpr int64_t FOLD_MAX_M = 25600;
+
+extern "C" int ym_bn_bwd_fold_ok(int64_t m, int c) {
+    if (g_bwd_fold == 0) return 0;
+    return m > 0 && m <= FOLD_MAX_M && c % 64 == 0 && c <= 2048 && ym_bn_bwd_blocks(m, c) >= FOLD_GP ? 1 : 0;
+}
+
+extern "C" int ym_bn_set_bwd_fold(int mode) {
+    // fused backward statistics + finalize: -1 default (on), 0 off, 1 on; returns the previous setting
+    const int prev = g_bwd_fold;
+    g_bwd_fold = mode < -1 || mode > 1 ? -1 : mode;
+    return prev;
+}
+
+extern "C" int ym_bn_bwd_reduce_fold(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
+                                     int hw, const float* scale, const float* shift, const float* mean,
+                                     const float* rstd, int act, float* part_sum, float* part_dot, const float* gamma,
+                                     float* dgamma, float* dbeta, int accumulate, float* coef, void* workspace,
+                                     void* stream) {
+    CHECK_C(c);
+    CHECK_VIEW(d_bs, d_ld, hw);
+    YM_CHECK_ARG(workspace && gamma && coef, "ym_bn_bwd_reduce_fold: null argument");
+    if (!ym_bn_bwd_fold_ok(m, c)) {
+        // the streaming statistics kernel + the finalize launch (the same outputs)
+        const int r = ym_bn_bwd_reduce(dy, d_bs, d_ld, z, m, c, hw, scale, shift, mean, rstd, act, part_sum, part_dot,
+                                       stream);
+        if (r != YM_OK) return r;
+        return ym_bn_bwd_finalize(part_sum, part_dot, ym_bn_bwd_blocks(m, c), c, double(m), gamma, rstd, dgamma,
+                                  dbeta, accumulate, coef, workspace, stream);
+    }
+    hipLaunchKernelGGL(bn_bwd_reduce_fold_kernel, dim3(FOLD_GP, c / 64), dim3(256), 0, as_stream(stream), dy, d_ld, z,
+                       m, c, scale, shift, mean, rstd, act, part_sum, part_dot, gamma, dgamma, dbeta, accumulate, coef,
+                       static_cast<unsigned*>(workspace), double(m));
+    YM_LAUNCH_CHECK("ym_bn_bwd_reduce_fold");
     return YM_OK;
 }
 

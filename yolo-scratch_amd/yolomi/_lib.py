@@ -93,6 +93,9 @@ SIGNATURES = {
     "ym_bn_bwd_blocks": (R, [I64, INT]),
     "ym_bn_bwd_reduce": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, INT, P, P, P]),
+    "ym_bn_bwd_fold_ok": (R, [I64, INT]),
+    "ym_bn_bwd_reduce_fold": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, P, P, INT, P, P, P]),
+    "ym_bn_set_bwd_fold": (R, [INT]),
     "ym_bn_bwd_apply": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P]),
     "ym_bn_bwd_apply_res": (R, [P, I64, I64, P, I64, INT, INT, P, P, P, P, INT, P, P, P, I64, I64, INT, P]),
     "ym_sppf_supported": (R, [INT, INT, INT]),

@@ -332,12 +332,23 @@ class ConvBN:
         e = self.M * self.co * 2
         work = 5 * e + 16 * Gb * self.co + ((2 + racc) * e if r is not None else 0)
 
+        fold = self.__dict__.get("_bwd_fold")
+        if fold is None:
+            fold = self._bwd_fold = bool(lib().ym_bn_bwd_fold_ok(self.M, self.co))
+        fold = fold and os.environ.get("YM_BWD_FOLD", "1") != "0"
+
         def run():
-            call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc, sh,
-                 mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
-            call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
-                 _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
-                 plan.bn_ws.data_ptr(), st)
+            if fold:
+                # small maps: statistics + finalize in one launch (the last workgroup of each 64-channel group folds)
+                call("ym_bn_bwd_reduce_fold", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW,
+                     sc, sh, mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), _p(bn.weight),
+                     plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(), plan.bn_ws.data_ptr(), st)
+            else:
+                call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc,
+                     sh, mu, rs, self.act, self.ps[0].data_ptr(), self.ps[1].data_ptr(), st)
+                call("ym_bn_bwd_finalize", self.ps[0].data_ptr(), self.ps[1].data_ptr(), Gb, self.co, float(self.M),
+                     _p(bn.weight), rs, plan.gptr(bn.weight), plan.gptr(bn.bias), 0, self.coef.data_ptr(),
+                     plan.bn_ws.data_ptr(), st)
             if r is not None:
                 call("ym_bn_bwd_apply_res", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, self.co, self.HW, sc,
                      sh, mu, rs, self.act, self.coef.data_ptr(), self.z.data_ptr(), r.gptr(), r.bs, r.ld, racc, st)
