@@ -91,7 +91,8 @@ def test_bn_bwd_finalize_vs_host_fp64(G, C):
 # accumulate) and the apply coefficients to 1e-6, three calls in a row (tickets re-armed), SiLU on and off,
 # a channel-slice view of dy; a map past the size limit falls back to the two launches.
 @pytest.mark.parametrize("m,c,act,extra", [(25600, 128, 1, 0), (400 * 7, 512, 1, 64), (102400, 64, 0, 0),
-                                           (200000, 128, 1, 0)])
+                                           (200000, 128, 1, 0), (25600, 256, 0, 0), (25600, 256, 1, 256),
+                                           (25600, 64, 0, 64), (25600, 512, 0, 0)])
 def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra):
     import ctypes
     from yolomi._lib import call, lib

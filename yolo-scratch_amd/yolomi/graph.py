@@ -335,7 +335,7 @@ class ConvBN:
         fold = self.__dict__.get("_bwd_fold")
         if fold is None:
             fold = self._bwd_fold = bool(lib().ym_bn_bwd_fold_ok(self.M, self.co))
-        fold = fold and os.environ.get("YM_BWD_FOLD", "0") == "1"
+        fold = fold and os.environ.get("YM_BWD_FOLD", "1") == "1"
 
         def run():
             if fold:
