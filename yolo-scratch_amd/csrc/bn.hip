@@ -183,6 +183,10 @@ __global__ void bn_eval_coeff_batch_kernel(const ym_bn_eval_entry* __restrict__ 
 }
 
 // ---------------------------------------------------------------- streaming kernels
+// rows of one thread whose loads are in flight together in the streaming kernels
+#ifndef BN_ROWS
+#define BN_ROWS 2
+#endif
 struct Lanes {
     int g, r, rows;
     bool on;
@@ -209,21 +213,21 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
     load8(scale + c0, sc);
     load8(shift + c0, sf);
     const int64_t step = int64_t(gridDim.x) * L.rows;
-    // two rows per iteration: both rows' loads are in flight before either is used
-    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
-        const int64_t m2 = m + step;
-        const bool two = m2 < M;
-        uint4 zr[2], rr[2];
-        zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
-        if (two) zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
-        if (res) {
-            rr[0] = *reinterpret_cast<const uint4*>(res + m * r_ld + c0);
-            if (two) rr[1] = *reinterpret_cast<const uint4*>(res + m2 * r_ld + c0);
+    // BN_ROWS rows per iteration: every row's loads are in flight before any is used
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += BN_ROWS * step) {
+        uint4 zr[BN_ROWS], rr[BN_ROWS];
+#pragma unroll
+        for (int u = 0; u < BN_ROWS; ++u) {
+            const int64_t mm = m + u * step;
+            if (mm < M) {
+                zr[u] = *reinterpret_cast<const uint4*>(z + mm * C + c0);
+                if (res) rr[u] = *reinterpret_cast<const uint4*>(res + mm * r_ld + c0);
+            }
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (u == 1 && !two) break;
-            const int64_t mm = u ? m2 : m;
+        for (int u = 0; u < BN_ROWS; ++u) {
+            const int64_t mm = m + u * step;
+            if (mm >= M) break;
             float v[8];
             unpack8h(zr[u], v);
 #pragma unroll
@@ -266,19 +270,19 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(const bf16_t* __rest
         load8(mean + c0, mu);
         load8(rstd + c0, rs);
         const int64_t step = int64_t(gridDim.x) * L.rows;
-        for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
-            const int64_t m2 = m + step;
-            const bool two = m2 < M;
-            uint4 zr[2], dr[2];
-            zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
-            dr[0] = *reinterpret_cast<const uint4*>(dy + m * d_ld + c0);
-            if (two) {
-                zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
-                dr[1] = *reinterpret_cast<const uint4*>(dy + m2 * d_ld + c0);
+        for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += BN_ROWS * step) {
+            uint4 zr[BN_ROWS], dr[BN_ROWS];
+#pragma unroll
+            for (int u = 0; u < BN_ROWS; ++u) {
+                const int64_t mm = m + u * step;
+                if (mm < M) {
+                    zr[u] = *reinterpret_cast<const uint4*>(z + mm * C + c0);
+                    dr[u] = *reinterpret_cast<const uint4*>(dy + mm * d_ld + c0);
+                }
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (u == 1 && !two) break;
+            for (int u = 0; u < BN_ROWS; ++u) {
+                if (m + u * step >= M) break;
                 float zv[8], dv[8];
                 unpack8h(zr[u], zv);
                 unpack8(dr[u], dv);
@@ -332,19 +336,20 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
     load8(coef + C + c0, k2);
     load8(coef + 2 * C + c0, k3);
     const int64_t step = int64_t(gridDim.x) * L.rows;
-    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += 2 * step) {
-        const int64_t m2 = m + step;
-        const bool two = m2 < M;
-        uint4 zr[2], dr[2];
-        zr[0] = *reinterpret_cast<const uint4*>(z + m * C + c0);
-        dr[0] = *reinterpret_cast<const uint4*>(dy + m * d_ld + c0);
-        if (two) {
-            zr[1] = *reinterpret_cast<const uint4*>(z + m2 * C + c0);
-            dr[1] = *reinterpret_cast<const uint4*>(dy + m2 * d_ld + c0);
+    for (int64_t m = int64_t(blockIdx.x) * L.rows + L.r; m < M; m += BN_ROWS * step) {
+        uint4 zr[BN_ROWS], dr[BN_ROWS];
+#pragma unroll
+        for (int u = 0; u < BN_ROWS; ++u) {
+            const int64_t mm = m + u * step;
+            if (mm < M) {
+                zr[u] = *reinterpret_cast<const uint4*>(z + mm * C + c0);
+                dr[u] = *reinterpret_cast<const uint4*>(dy + mm * d_ld + c0);
+            }
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            if (u == 1 && !two) break;
+        for (int u = 0; u < BN_ROWS; ++u) {
+            const int64_t mm = m + u * step;
+            if (mm >= M) break;
             float zv[8], dv[8], o[8];
             unpack8h(zr[u], zv);
             unpack8(dr[u], dv);
@@ -354,9 +359,9 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
                 const float xh = (zv[k] - mu[k]) * rs[k];
                 o[k] = k1[k] * (gg - k2[k] - xh * k3[k]);
             }
-            *reinterpret_cast<uint4*>(dz + (u ? m2 : m) * C + c0) = pack8(o);
+            *reinterpret_cast<uint4*>(dz + mm * C + c0) = pack8(o);
             if constexpr (RES) {
-                uint4* rp = reinterpret_cast<uint4*>(dres + (u ? m2 : m) * r_ld + c0);
+                uint4* rp = reinterpret_cast<uint4*>(dres + mm * r_ld + c0);
                 if (r_acc) {
                     float rv[8];
                     unpack8(*rp, rv);
