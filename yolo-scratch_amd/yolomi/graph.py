@@ -398,7 +398,7 @@ class StemConvBN(ConvBN):
         assert (oh, ow) == (y.H, y.W)
         self.M, self.HW, self.oh, self.ow = B * oh * ow, oh * ow, oh, ow
         self.z = torch.empty(self.M, co, dtype=BF16, device=plan.dev)
-        self.G = 1024
+        self.G = 2048           # statistics rows = workgroups (2048 vs 1024: -22 us alone, +0.06-0.1 % step)
         self.ps = torch.empty(2, max(self.G, lib().ym_bn_bwd_blocks(self.M, co)), co, dtype=F32, device=plan.dev)
         self.bnv = torch.empty(4, co, dtype=F32, device=plan.dev)
         self.coef = torch.empty(3, co, dtype=F32, device=plan.dev)
