@@ -563,7 +563,11 @@ extern "C" int ym_bn_apply(const uint16_t* z, int64_t m, int c, int hw, const fl
     return YM_OK;
 }
 
-extern "C" int ym_bn_bwd_blocks(int64_t m, int c) { return stream_blocks(m, c, REDUCE_CAP); }
+// the largest maps (m * c >= 2^26: the stem, the 160x160 >= 64-channel and 80x80 256-channel layers) take twice the
+// workgroups: the stem's statistics sit on the serial tail of the backward (+0.5-0.6 % step, bn_reduce_cap_ab.txt)
+extern "C" int ym_bn_bwd_blocks(int64_t m, int c) {
+    return stream_blocks(m, c, m * c >= (int64_t(1) << 26) ? 2 * REDUCE_CAP : REDUCE_CAP);
+}
 
 extern "C" int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,
                                 int hw, const float* scale, const float* shift, const float* mean, const float* rstd,
