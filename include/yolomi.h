@@ -275,7 +275,8 @@ int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint1
 int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                        const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
                        float* coef, void* workspace, void* stream);
-/* Backward statistics AND finalize in one launch on the small maps (m <= 40x40x64 pixels, c % 64 == 0):
+/* Backward statistics AND finalize in one launch on the small maps (m <= 25600 pixels = 20x20 x 64
+ * images, c % 64 == 0):
  * ym_bn_bwd_reduce followed by ym_bn_bwd_finalize over its rows, with the same outputs (dgamma / dbeta /
  * coef; part_sum / part_dot as scratch rows, ym_bn_bwd_blocks(m, c) x c floats each).  Where
  * ym_bn_bwd_fold_ok(m, c) is 0 it runs those two launches. */

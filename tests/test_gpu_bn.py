@@ -139,3 +139,174 @@ def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra):
             # sum can cancel to ~0, so the floor is 1 % of the largest channel's)
             err = float(((x - y).abs() / (y.abs() + 1e-2 * y.abs().max())).max())
             assert err < 1e-4, err
+
+
+# ym_bn_bwd_reduce + ym_bn_bwd_finalize at the sizes where ym_bn_bwd_blocks takes 1024 workgroups (m * c >= 2^26:
+# the stem and the 160x160 maps at bs >= 21; round-4 commit 0f64fef), against a host fp64 reduction of the same
+# bf16 dy / fp16 z (the Conv block's BatchNorm2d + SiLU backward, models/yolo11_modules.py:29-33; eps / momentum
+# yolo11_model.py:183-185), plus the apply pass dz = k1 (g - k2 - xhat k3) on every row.
+@pytest.mark.parametrize("m,c,act", [(640000, 128, 1), (1638400, 64, 1), (524288, 128, 0)])
+def test_bn_bwd_reduce_finalize_large_vs_host_fp64(m, c, act):
+    from yolomi._lib import call, lib, stream_ptr
+    dev = torch.device("cuda", 0)
+    st = stream_ptr(dev)
+    assert m * c >= 1 << 26
+    Gb = lib().ym_bn_bwd_blocks(m, c)
+    assert Gb == 1024, Gb
+    g = torch.Generator().manual_seed(m + c)
+    z_h = torch.randn(m, c, generator=g).half()
+    dy_b = torch.randn(m, c, generator=g).bfloat16()
+    scale = 1 + 0.1 * torch.randn(c, generator=g)
+    shift = 0.1 * torch.randn(c, generator=g)
+    mean = 0.05 * torch.randn(c, generator=g)
+    rstd = 1 + 0.1 * torch.rand(c, generator=g)
+    gamma = 1 + 0.1 * torch.randn(c, generator=g)
+    z, dy = z_h.to(dev), dy_b.to(dev)
+    scd, shd, mud, rsd, gmd = (t.to(dev) for t in (scale, shift, mean, rstd, gamma))
+    ps, pg = torch.empty(Gb, c, device=dev), torch.empty(Gb, c, device=dev)
+    dg, db = torch.zeros(c, device=dev), torch.zeros(c, device=dev)
+    coef = torch.empty(3, c, device=dev)
+    ws = torch.zeros(lib().ym_bn_workspace_size(c), dtype=torch.uint8, device=dev)
+    dz = torch.empty(m, c, dtype=torch.bfloat16, device=dev)
+    hw = 6400
+    call("ym_bn_bwd_reduce", dy.data_ptr(), hw * c, c, z.data_ptr(), m, c, hw, scd.data_ptr(), shd.data_ptr(),
+         mud.data_ptr(), rsd.data_ptr(), act, ps.data_ptr(), pg.data_ptr(), st)
+    call("ym_bn_bwd_finalize", ps.data_ptr(), pg.data_ptr(), Gb, c, float(m), gmd.data_ptr(), rsd.data_ptr(),
+         dg.data_ptr(), db.data_ptr(), 0, coef.data_ptr(), ws.data_ptr(), st)
+    call("ym_bn_bwd_apply", dy.data_ptr(), hw * c, c, z.data_ptr(), m, c, hw, scd.data_ptr(), shd.data_ptr(),
+         mud.data_ptr(), rsd.data_ptr(), act, coef.data_ptr(), dz.data_ptr(), st)
+    torch.cuda.synchronize()
+    # host fp64 in row chunks (the whole map in fp64 would be ~1.3 GB per operand)
+    s = torch.zeros(c, dtype=torch.float64)
+    sx = torch.zeros(c, dtype=torch.float64)
+    sc64, sh64, mu64, rs64 = scale.double(), shift.double(), mean.double(), rstd.double()
+    for r0 in range(0, m, 131072):
+        zz = z_h[r0:r0 + 131072].double()
+        gg = dy_b[r0:r0 + 131072].double()
+        if act:
+            t = zz * sc64 + sh64
+            sg = torch.sigmoid(t)
+            gg = gg * sg * (1 + t * (1 - sg))
+        s += gg.sum(0)
+        sx += (gg * ((zz - mu64) * rs64)).sum(0)
+    # a channel's sum can cancel towards 0: relative to 1 % of the largest channel's magnitude
+    for got, ref in ((db.double().cpu(), s), (dg.double().cpu(), sx)):
+        err = float(((got - ref).abs() / (ref.abs() + 1e-2 * ref.abs().max())).max())
+        assert err < 1e-4, err
+    k1, k2, k3 = (gamma.double() * rs64), s / m, sx / m
+    np.testing.assert_allclose(coef[0].double().cpu(), k1, rtol=1e-6)
+    for got, ref in ((coef[1].double().cpu(), k2), (coef[2].double().cpu(), k3)):
+        err = float(((got - ref).abs() / (ref.abs() + 1e-2 * ref.abs().max())).max())
+        assert err < 1e-4, err
+    assert int(ws[:256].view(torch.int32).abs().sum()) == 0        # tickets re-armed
+    # the apply pass on every row vs fp64 with the kernel's own coefficients (bf16 output: 2^-8 relative)
+    kc = coef.double().cpu()
+    worst = 0.0
+    for r0 in range(0, m, 131072):
+        zz = z_h[r0:r0 + 131072].double()
+        gg = dy_b[r0:r0 + 131072].double()
+        if act:
+            t = zz * sc64 + sh64
+            sg = torch.sigmoid(t)
+            gg = gg * sg * (1 + t * (1 - sg))
+        ref = kc[0] * (gg - kc[1] - (zz - mu64) * rs64 * kc[2])
+        got = dz[r0:r0 + 131072].double().cpu()
+        worst = max(worst, float(((got - ref).abs() / (ref.abs() + 1e-2)).max()))
+    assert worst < 1.2e-2, worst
+
+
+# the fused backward statistics + finalize (ym_bn_bwd_reduce_fold, on by default for the 20x20 maps)
+# against the two launches it replaces, on the ACTUAL in-model inputs of one s@640 bs64 training step: every
+# fold-eligible BatchNorm backward (Conv blocks, the Bottleneck shortcuts, the strided dy views of concat slices and
+# the C2PSA's depthwise pe block) is intercepted, both paths run on the same dy / z / BN vectors before the plan's own
+# call, and dgamma / dbeta / the apply coefficients of BOTH are checked against a host fp64 reduction of the same
+# inputs.  The bound is relative to the sum of the terms' magnitudes (sum |g|, sum |g xhat|): these sums cancel
+# (dbeta of a layer is often 1e-2..1e-3 of sum |g|), so two fp32 groupings of the same terms can differ by 1e-3 of the
+# SUM while each is within ~1e-7 of the terms' scale — that, not the sum, is what fp32 reordering moves.
+def test_bn_bwd_fold_matches_two_launches_in_model():
+    import yaml
+    from pathlib import Path
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets import prepare_batch
+    from datasets.synthetic import synth_batch
+    from yolomi import graph as G
+    from yolomi._lib import call, lib
+    root = Path(__file__).resolve().parents[1] / "yolo-scratch_amd"
+    cfg = yaml.safe_load((root / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = "s"
+    torch.manual_seed(0)
+    m = build_yolo11(cfg, ch=1, nc=5).cuda().train()
+    crit = v8DetectionLoss(m, tal_topk=10)
+    b = prepare_batch(synth_batch(64, 640, seed=5), torch.device("cuda"))
+    dev = torch.device("cuda", 0)
+    results = []
+    orig = G.ConvBN._bn_bwd
+
+    def patched(self, plan, st, dy):
+        if lib().ym_bn_bwd_fold_ok(self.M, self.co):
+            c = self.co
+            Gb = lib().ym_bn_bwd_blocks(self.M, c)
+            sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
+            gamma = self.m.bn.weight
+            outs = []
+            bufs = [(torch.empty(Gb, c, device=dev), torch.empty(Gb, c, device=dev), torch.zeros(c, device=dev),
+                     torch.zeros(c, device=dev), torch.empty(3, c, device=dev),
+                     torch.zeros(lib().ym_bn_workspace_size(c), dtype=torch.uint8, device=dev)) for _ in range(2)]
+            # the fills above run on torch's current stream, the kernels below on the plan's stream `st`: without
+            # this wait a late zero-fill of the workspace re-arms the finalize's tickets mid-launch (nothing written)
+            torch.cuda.synchronize()
+            for fused, (ps, pg, dg, db, coef, ws) in zip((True, False), bufs):
+                if fused:
+                    call("ym_bn_bwd_reduce_fold", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, c, self.HW,
+                         sc, sh, mu, rs, self.act, ps.data_ptr(), pg.data_ptr(), gamma.data_ptr(), dg.data_ptr(),
+                         db.data_ptr(), 0, coef.data_ptr(), ws.data_ptr(), st)
+                else:
+                    call("ym_bn_bwd_reduce", dy, self.y.bs, self.y.ld, self.z.data_ptr(), self.M, c, self.HW, sc, sh,
+                         mu, rs, self.act, ps.data_ptr(), pg.data_ptr(), st)
+                    call("ym_bn_bwd_finalize", ps.data_ptr(), pg.data_ptr(), Gb, c, float(self.M), gamma.data_ptr(),
+                         rs, dg.data_ptr(), db.data_ptr(), 0, coef.data_ptr(), ws.data_ptr(), st)
+                outs.append((dg, db, coef))
+            torch.cuda.synchronize()
+            g = self.y.act.grad()[..., self.y.c0:self.y.c0 + c].reshape(self.M, c).double().cpu()
+            z = self.z.view(torch.float16).double().cpu()
+            sc_, sh_, mu_, rs_ = (self.bnv[i].double().cpu() for i in range(4))
+            if self.act:
+                t = z * sc_ + sh_
+                sg = torch.sigmoid(t)
+                g = g * sg * (1 + t * (1 - sg))
+            gx = g * ((z - mu_) * rs_)
+            ref = (g.sum(0), gx.sum(0), g.abs().sum(0), gx.abs().sum(0))
+            results.append((type(self).__name__, self.M, c, self.y.ld, outs, ref))
+        return orig(self, plan, st, dy)
+
+    G.ConvBN._bn_bwd = patched
+    try:
+        m.zero_grad(set_to_none=True)
+        loss, _ = crit(m(b["img"]), b)
+        loss.backward()
+        torch.cuda.synchronize()
+    finally:
+        G.ConvBN._bn_bwd = orig
+    assert len(results) >= 20, len(results)
+    kinds = {r[0] for r in results}
+    assert "DWConvBN" in kinds and any(r[3] != r[2] for r in results), (kinds, [(r[2], r[3]) for r in results])
+    worst = {True: 0.0, False: 0.0}
+    bad = []
+    for name, M, c, ld, outs, (s, sx, sa, sxa) in results:
+        for fused, (dg, db, coef) in zip((True, False), outs):
+            dg, db, coef = dg.double().cpu(), db.double().cpu(), coef.double().cpu()
+            for q, (got, want, scale) in enumerate(((db, s, sa), (dg, sx, sxa), (coef[1] * M, s, sa),
+                                                    (coef[2] * M, sx, sxa))):
+                e = (got - want).abs() / scale.clamp_min(1e-30)
+                err = float(e.max())
+                worst[fused] = max(worst[fused], err)
+                if err >= 2e-5:
+                    k = int(e.argmax())
+                    bad.append((name, M, c, ld, "fold" if fused else "two", q, err, k, float(got[k]), float(want[k]),
+                                float(scale[k]), int((e >= 2e-5).sum())))
+    for r in bad:
+        print("BAD", r)
+    assert not bad, bad[:4]
+    print(f"{len(results)} in-model BatchNorm backwards vs host fp64, error / sum of |terms|: "
+          f"fold {worst[True]:.2e}, two launches {worst[False]:.2e}")

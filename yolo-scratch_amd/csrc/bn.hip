@@ -598,8 +598,9 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
 
 // fused backward statistics + finalize policy (ym_bn_set_bwd_fold): -1 default (on), 0 off, 1 on
 static int g_bwd_fold = -1;
-// the maps it takes: whole 64-channel groups and at most 40x40 x 64 images of pixels (FOLD_GP workgroups per
-// group stream the tensor; on the larger maps the streaming kernel's 512 full-width workgroups win)
+// the maps it takes: whole 64-channel groups and at most 25600 pixels = 20x20 x 64 images (FOLD_GP workgroups per
+// group stream the tensor; on the larger maps, 40x40 included, the streaming kernel's 512 full-width workgroups win:
+// profiles/r04/bn_bwd_fold_ab.txt)
 static constexpr int64_t FOLD_MAX_M = 25600;
 
 extern "C" int ym_bn_bwd_fold_ok(int64_t m, int c) {

@@ -180,7 +180,7 @@ class GradSync:
         self.buckets[id(plan)] = b
 
         def hook(params, writes=None, _b=b, _plan=plan):
-            if getattr(_plan, "pooled", False):
+            if self.model.__dict__.get("_ym_pooled_step"):
                 return                    # reduced after the backwards (sync), not bucket by bucket
             if not _b.remaining:
                 _b.begin()
@@ -189,10 +189,16 @@ class GradSync:
 
     def sync(self):
         plan = self.model.__dict__.get("_ym_last_plan")
-        if plan is not None and getattr(plan, "pooled", False):
-            # several forwards were in flight before the backward (yolomi.graph.run_model): their plans'
-            # gradients were added together into .grad, which is reduced below as one buffer
+        if self.model.__dict__.pop("_ym_pooled_step", False):
+            # several forwards were in flight before this step's backwards (yolomi.graph.run_model): their
+            # plans' gradients were added together into .grad, which is reduced below as one buffer; the
+            # flag is per step, so the next ordinary step overlaps its buckets with the backward again.
+            # The decision is rank-local: a data-parallel loop must take the same forwards on every rank
+            # (SPMD), as DDP requires of its own bucket hooks.
             plan = None
+            for b in self.buckets.values():
+                if b is not None:
+                    b.remaining = []
         if plan is not None:
             b = self.buckets.get(id(plan))
             if b is not None and b.remaining:

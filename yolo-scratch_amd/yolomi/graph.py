@@ -423,6 +423,7 @@ class StemConvBN(ConvBN):
             ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
             call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight),
                  plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
+            plan.note_grad_write(plan._cur_stream)      # conv.weight: after the BN event _bn_bwd noted
             return
         bn = self.m.bn
         sc, sh, mu, rs = (self.bnv[i].data_ptr() for i in range(4))
@@ -440,6 +441,7 @@ class StemConvBN(ConvBN):
                  self.bnv.data_ptr(), self.coef.data_ptr(), plan.gptr(self.m.conv.weight), ws.data_ptr(),
                  ws.numel() * 4, *self._geo(plan), st)
         self._timed(plan, "bn", plan._cur_stream, run, 4 * e + 16 * Gb * self.co + 4 * plan.B * self.H * self.W)
+        plan.note_grad_write(plan._cur_stream)          # dgamma / dbeta and conv.weight are in the stream now
 
 
 class DWConvBN(ConvBN):
@@ -484,6 +486,7 @@ class DWConvBN(ConvBN):
         call("ym_dw3x3_bwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
              self.z.data_ptr(), self.x.gptr(), self.x.bs, self.x.ld, plan.gptr(self.m.conv.weight), plan.B, self.y.H,
              self.y.W, self.C, acc, ws.data_ptr(), ws.numel() * 4, st)
+        plan.note_grad_write(plan._cur_stream)          # conv.weight: after the BN event _bn_bwd noted
         self.x.act.written[vch] = True
 
 
@@ -1069,21 +1072,28 @@ class Plan:
         self._replay("fwd", body, [("img", self.img)] if self.img is not None else [])
 
     def backward(self):
+        # gradient accumulation without zero_grad(): the parameters' .grad still alias this plan's flat
+        # buffer (install_grads) and hold the previous backward's sum, which the zero fill of the backward
+        # would drop — keep it and add it back after this backward (single-process; under DP the buffer is
+        # on the wire during the backward, and the reference's loop zeroes its gradients every step).
+        # Decided and done eagerly, OUTSIDE the body a HIP graph captures and replays (YM_GRAPH=1): a
+        # captured decision would replay a stale keep buffer, or none, on every later step.
+        keep = self._accumulation_keep()
         self._replay("bwd", lambda: self._backward_ops(self.ops),
                      [("dhead", self.dhead)] if self.dhead is not None else [])
+        if keep is not None:
+            self.grad_flat.add_(keep)
+
+    def _accumulation_keep(self):
+        if self.grad_hook is None and self.params:
+            p0 = self.params[0]
+            if p0.grad is not None and p0.grad.data_ptr() == self.grad_views[id(p0)].data_ptr():
+                return self.grad_flat.clone()
+        return None
 
     def _backward_ops(self, ops):
         for a in self.acts:
             a.written[:] = False
-        # gradient accumulation without zero_grad(): the parameters' .grad still alias this plan's flat
-        # buffer (install_grads) and hold the previous backward's sum, which the zero fill below would
-        # drop — keep it and add it back after this backward (single-process; under DP the buffer is
-        # on the wire during the backward, and the reference's loop zeroes its gradients every step)
-        keep = None
-        if self.grad_hook is None and self.params:
-            p0 = self.params[0]
-            if p0.grad is not None and p0.grad.data_ptr() == self.grad_views[id(p0)].data_ptr():
-                keep = self.grad_flat.clone()
         self.grad_flat.zero_()
         for t in self._scratch:
             t.zero_()
@@ -1093,8 +1103,6 @@ class Plan:
         self._run(list(reversed(ops)), "bwd",
                   (lambda op: hook(op_params(op), self.take_grad_writes(op))) if hook is not None else None)
         self._join_side()
-        if keep is not None:
-            self.grad_flat.add_(keep)
 
     # --------------------------------------------------------------- forwards in flight
     # A plan owns ONE set of activation buffers.  While a training forward's autograd graph is alive
@@ -1466,7 +1474,10 @@ def run_detect(det, xs):
         plan.level_hw = [(x.shape[2], x.shape[3]) for x in xs]
 
         def backward_from_head():
+            keep = plan._accumulation_keep()
             plan._backward_ops(plan.ops)
+            if keep is not None:
+                plan.grad_flat.add_(keep)
         plan.backward_from_head = backward_from_head
         cache[key] = plan
     # every level input takes part in the backward (needs_grad checks plan.input only)
@@ -1502,11 +1513,11 @@ def run_model(model, img: torch.Tensor):
         plan.is_model = True
         lower_model(plan, model, (B, H, W))
         pool.append(plan)
-        if len(pool) > 1:
-            # several forwards in flight: their gradients meet in .grad (install_grads adds), so data
-            # parallelism all-reduces .grad after the backwards instead of each plan's buffer during its own
-            for p_ in pool:
-                p_.pooled = True
+    if model.training and torch.is_grad_enabled() and any(p_.pending for p_ in pool if p_ is not plan):
+        # several forwards in flight THIS step: their gradients meet in .grad (install_grads adds), so data
+        # parallelism all-reduces .grad after the backwards instead of each plan's buffer during its own.
+        # A per-step flag (GradSync.sync clears it): the next ordinary step buckets again.
+        model.__dict__["_ym_pooled_step"] = True
     if model.training:
         model.__dict__["_ym_last_plan"] = plan
     anchor = model.__dict__.setdefault("_ym_anchor", torch.zeros(1, device=img.device, requires_grad=True))
