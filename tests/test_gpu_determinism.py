@@ -97,3 +97,50 @@ def test_eval_coefficients_follow_replaced_buffers():
     y2 = run(m2)
     assert not torch.equal(y1, y0)
     assert torch.equal(y1, y2)
+
+
+def test_graph_replay_gradient_accumulation():
+    """gradient accumulation (two backwards without zero_grad in between) under HIP-graph
+    replay (YM_GRAPH=1), mixing zero_grad(set_to_none=True) and in-place zero_grad(set_to_none=False) across the
+    eager, capture and replay steps.  The keep-and-add-back of the previous sum runs eagerly around the replayed
+    backward, so every step's .grad equals (number of backwards since the last zeroing) x the single-step
+    gradient of the same inputs — never a stale sum from the captured step, never a dropped one."""
+    from oracle import model as om
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    cfg = om.load_cfg("n")
+    _, _, P = om.build(cfg)
+    b = {k: v.cuda() for k, v in synth_batch(2, 256, seed=21).items()}
+    os.environ["YM_GRAPH"] = "0"
+    m0 = build_yolo11(cfg, ch=1, nc=5)
+    m0.load_state_dict(P)
+    m0 = m0.cuda().train()
+    bufs = {k: v.clone() for k, v in m0.state_dict().items()}
+    single = _step(m0, v8DetectionLoss(m0), b)[3]
+    os.environ["YM_GRAPH"] = "1"
+    try:
+        m = build_yolo11(cfg, ch=1, nc=5)
+        m.load_state_dict(P)
+        m = m.cuda().train()
+        crit = v8DetectionLoss(m)
+        # (zeroing before the step: None = none, True = set_to_none, False = in-place; backwards in the step)
+        plan = [(True, 1), (False, 2), (True, 2), (None, 1), (False, 1), (True, 3)]
+        count = 0
+        for zero, nb in plan:
+            if zero is not None:
+                m.zero_grad(set_to_none=zero)
+                count = 0
+            for _ in range(nb):
+                m.load_state_dict(bufs)
+                loss, _ = crit(m(b["img"].clone()), b)
+                loss.backward()
+                count += 1
+            torch.cuda.synchronize()
+            grads = [p.grad for p in m.parameters() if p.grad is not None]
+            assert len(grads) == len(single)
+            for i, (g, s) in enumerate(zip(grads, single)):
+                torch.testing.assert_close(g, s * count, rtol=1e-5, atol=1e-6 * float(s.abs().max()) * count,
+                                           msg=f"step {zero, nb} (count {count}) parameter {i}")
+    finally:
+        os.environ.pop("YM_GRAPH", None)

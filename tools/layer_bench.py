@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--pipe", type=int, default=-1, help="ym_conv_set_pipe policy for this run (A/B)")
     ap.add_argument("--halo", type=int, default=-1, help="ym_conv_set_halo policy for this run (A/B)")
     ap.add_argument("--direct", type=int, default=-1, help="ym_conv_set_direct policy for this run (A/B)")
+    ap.add_argument("--set", nargs="*", default=[], help="other library setters for this run, NAME=VALUE "
+                                                        "(e.g. ym_pipe_set_exp=1)")
     ap.add_argument("--names", action="store_true", help="append each launch's kernel instance (ym_conv_kernel)")
     ap.add_argument("--seq-out", help="counter-pass mode: write the (op, kind, k, flops, launches) order of the "
                                       "timed groups here and separate the groups with a marker kernel "
@@ -43,6 +45,9 @@ def main():
     from yolomi._lib import lib
     lib().ym_conv_set_hpipe(args.hpipe)
     lib().ym_conv_set_pipe(args.pipe)
+    for kv in args.set:
+        name, val = kv.split("=")
+        getattr(lib(), name)(int(val))
     lib().ym_conv_set_halo(args.halo)
     lib().ym_conv_set_direct(args.direct)
     dev = torch.device("cuda", 0)

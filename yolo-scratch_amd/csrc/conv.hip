@@ -925,7 +925,8 @@ extern "C" int ym_conv_kernel(const ym_conv_desc* d, int dir, char* name, int na
             snprintf(buf, sizeof buf, "hpipe %s", hq.cfg == 0 ? "16x16px x 128" : hq.cfg == 1 ? "16x16px x 64" : "16x16px x 64 wres");
         } else if (pp.ok) {
             id = 2000 + pp.cfg;
-            snprintf(buf, sizeof buf, "pipe %s", pp.cfg == 0 ? "256x128" : "256x64");
+            static const char* const pipe_names[] = {"256x128", "256x64", "256x128 8w"};
+            snprintf(buf, sizeof buf, "pipe %s", pipe_names[pp.cfg]);
         } else if (hp.ok) {
             id = 1000 + 100 * hp.cfg + std::min(hp.TW, 99);
             snprintf(buf, sizeof buf, "halo %s %dx%d", hp.cfg == 0 ? "C8" : "C4", hp.TH, hp.TW);

@@ -41,6 +41,9 @@ namespace ym {
 // output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
 // wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
 int g_pipe_force = -1;
+// experiments (ym_pipe_set_exp, not in the header; tools/pipe_ab.py): 0 shipped; 1 the 8-wave 256 x 128 tile;
+// 10-13 ablations of the 16-wave tile (conv_pipe_kernel ABL 1, 2, 4, 8); 20 the generic (class-search) control path
+int g_pipe_exp = 0;
 
 namespace {
 
@@ -139,7 +142,12 @@ __device__ __forceinline__ void step_barrier() {
 // stages, and the per-lane gather offsets of the current tile and tap.  All control state is
 // wave-uniform (scalar registers); per stage the DMAs cost one M0 write each, per tap one
 // bounds select per gather row, per tile one pixel decomposition.
-template <int BM, int BN, int NW, int MODE>
+// C1 (every launch pipe_plan makes by default: one output class, maps of >= BM pixels): no class search, no
+// per-tile divisions — the tile's (image, in-image offset) advance by a constant step with one wrap, the
+// buffer resource over the tile's images is built once per tile.  (Round 5: the generic form spent ~3.8 SALU
+// and ~3.5 VALU per MFMA, SQ_INSTS_* over op 73, much of it the per-tile class search and 32-bit divisions of
+// both the issue and the compute side; its no-MFMA ablation alone ran 107 of the layer's 145 us.)
+template <int BM, int BN, int NW, int MODE, int ABL = 0, bool C1 = false>
 struct Issuer {
     static constexpr int AI = BN / 8 / NW, BI = BM / 8 / NW, RB = 128;
     const PipeArgs& a;
@@ -155,12 +163,67 @@ struct Issuer {
     int bh[BI], bw[BI];
     uint32_t bc[BI], b_off[BI];
     uint32_t a_tap = 0;
+    // C1: the staged tile's first pixel (image, in-image offset, flat index) and the per-tile step
+    int tn = 0, m0 = 0, step_n = 0, m_step = 0;
+    uint32_t tp = 0, step_p = 0, ohw = 1;
+    float inv_w = 1.f;
+    __amdgpu_buffer_rsrc_t xres_t;
 
     __device__ Issuer(const PipeArgs& a_, int wave_, int lane, int mt_lo_, int qstride_, int ntile_)
         : a(a_), wave(wave_), lrow(lane >> 3), lslot(lane & 7), kc(a_.Kin >> 6), xld_b(uint32_t(a_.x_ld) * 2u),
-          mt_lo(mt_lo_), qstride(qstride_), ntile(ntile_) {}
+          mt_lo(mt_lo_), qstride(qstride_), ntile(ntile_) {
+        if constexpr (C1) {
+            ohw = uint32_t(a.OH) * uint32_t(a.OW);
+            m0 = mt_lo * BM;
+            tn = int(uint32_t(m0) / ohw);
+            tp = uint32_t(m0) - uint32_t(tn) * ohw;
+            m_step = qstride * BM;
+            step_n = int(uint32_t(m_step) / ohw);
+            step_p = uint32_t(m_step) - uint32_t(step_n) * ohw;
+            inv_w = 1.0f / float(a.OW);
+            nkw = a.KW;
+            nrows = a.KH;
+        }
+    }
 
     __device__ __forceinline__ void tile_setup() {
+        if constexpr (C1) {
+            x_tile = a.x + int64_t(tn) * a.x_bs;
+            const int64_t xb = (int64_t(a.N) - tn) * a.x_bs * 2;
+            x_bytes = int(xb < 0x7fffffff ? xb : 0x7fffffff);
+            const uint64_t xp = reinterpret_cast<uint64_t>(x_tile);
+            const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xp))));
+            const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xp >> 32))));
+            xres_t = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
+                               __builtin_amdgcn_readfirstlane(x_bytes));
+            const int M = a.N * int(ohw);
+#pragma unroll
+            for (int j = 0; j < BI; ++j) {
+                const int r = (wave * BI + j) * 8 + lrow;
+                if (m0 + r < M) {
+                    uint32_t pix = tp + uint32_t(r), n = 0;
+                    if (pix >= ohw) { pix -= ohw; n = 1; }              // ohw >= BM: at most one wrap
+                    uint32_t q = uint32_t(float(pix) * inv_w);
+                    const int rem = int(pix) - int(q * uint32_t(a.OW));
+                    q = rem < 0 ? q - 1 : (rem >= a.OW ? q + 1 : q);
+                    const int oh = int(q), ow = int(pix - q * uint32_t(a.OW));
+                    if (MODE == PF) {
+                        bh[j] = oh * a.stride - a.pad;
+                        bw[j] = ow * a.stride - a.pad;
+                    } else {                        // stride-1 data gradient
+                        bh[j] = oh + a.pad;
+                        bw[j] = ow + a.pad;
+                    }
+                    bc[j] = n * uint32_t(a.x_bs) * 2u + uint32_t(bh[j] * a.GW + bw[j]) * xld_b +
+                            uint32_t(lslot ^ fsw128(r)) * 16u;
+                } else {
+                    bh[j] = -(1 << 20);             // no tap is in range
+                    bw[j] = 0;
+                    bc[j] = 0;
+                }
+            }
+            return;
+        }
         const int mt = mt_lo + i * qstride;
         const int c = cls_find(a, mt);
         const Cls k = cls_of(a, c);
@@ -168,19 +231,19 @@ struct Issuer {
         nrows = k.ntap / k.nkw;
         kh0 = k.kh0;
         kw0 = k.kw0;
-        const int64_t m0 = int64_t(mt - a.mt_pre[c]) * BM;
-        const uint32_t nfirst = uint32_t(m0) / k.OHW, tp = uint32_t(m0) - nfirst * k.OHW;
-        const float inv_w = 1.0f / float(k.OWc);
+        const int64_t m0l = int64_t(mt - a.mt_pre[c]) * BM;
+        const uint32_t nfirst = uint32_t(m0l) / k.OHW, tpl = uint32_t(m0l) - nfirst * k.OHW;
+        const float inv_wl = 1.0f / float(k.OWc);
         x_tile = a.x + int64_t(nfirst) * a.x_bs;
         const int64_t xb = (int64_t(a.N) - nfirst) * a.x_bs * 2;
         x_bytes = int(xb < 0x7fffffff ? xb : 0x7fffffff);
 #pragma unroll
         for (int j = 0; j < BI; ++j) {
             const int r = (wave * BI + j) * 8 + lrow;
-            const int64_t m = m0 + r;
+            const int64_t m = m0l + r;
             if (m < k.Mc) {
                 uint32_t n, pix, ii;
-                split_pix(nfirst, tp, uint32_t(r), k.OHW, uint32_t(k.OWc), inv_w, n, pix, ii);
+                split_pix(nfirst, tpl, uint32_t(r), k.OHW, uint32_t(k.OWc), inv_wl, n, pix, ii);
                 const int oh = int(ii) * a.os + k.py, ow = int(pix - ii * uint32_t(k.OWc)) * a.os + k.px;
                 if (MODE == PF) {
                     bh[j] = oh * a.stride - a.pad;
@@ -209,7 +272,8 @@ struct Issuer {
             const bool ok = uint32_t(gh) < uint32_t(a.GH) && uint32_t(gw) < uint32_t(a.GW);
             b_off[j] = ok ? bc[j] + delta : OOB;
         }
-        a_tap = uint32_t(((kh0 + ti * ost) * a.KW + (kw0 + tj * ost)) * a.Kin) * 2u;
+        a_tap = C1 ? uint32_t((ti * a.KW + tj) * a.Kin) * 2u
+                   : uint32_t(((kh0 + ti * ost) * a.KW + (kw0 + tj * ost)) * a.Kin) * 2u;
     }
 
     __device__ __forceinline__ void start() {
@@ -224,16 +288,23 @@ struct Issuer {
     // every step keeps the same DMA count (the counted vmcnt waits stay constant)
     __device__ __forceinline__ void issue_dma(char* st, __amdgpu_buffer_rsrc_t wres, const uint32_t* a_off, bool live) {
         const uint32_t kb = uint32_t(kci) * 128u;
-        // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
-        const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
-        const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
-        const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
-        const __amdgpu_buffer_rsrc_t xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
-                                                      __builtin_amdgcn_readfirstlane(x_bytes));
+        __amdgpu_buffer_rsrc_t xres;
+        if constexpr (C1) {
+            xres = xres_t;
+        } else {
+            // wave-uniform base / size (readfirstlane: else hipcc waterfalls every DMA over the resource)
+            const uint64_t xb = reinterpret_cast<uint64_t>(x_tile);
+            const uint32_t xlo = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb))));
+            const uint32_t xhi = uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(xb >> 32))));
+            xres = make_rsrc(reinterpret_cast<const void*>((uint64_t(xhi) << 32) | xlo),
+                             __builtin_amdgcn_readfirstlane(x_bytes));
+        }
 #pragma unroll
-        for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, live ? a_off[j] : OOB, a_tap + kb);
+        for (int j = 0; j < AI; ++j)
+            dma16(wres, st + (wave * AI + j) * 1024, live && !(ABL & 9) ? a_off[j] : OOB, a_tap + kb);
 #pragma unroll
-        for (int j = 0; j < BI; ++j) dma16(xres, st + BN * RB + (wave * BI + j) * 1024, live ? b_off[j] : OOB, kb);
+        for (int j = 0; j < BI; ++j)
+            dma16(xres, st + BN * RB + (wave * BI + j) * 1024, live && !(ABL & 5) ? b_off[j] : OOB, kb);
     }
 
     // advance the stream position by one stage (new tap: its gather offsets; new tile: its pixels)
@@ -244,7 +315,15 @@ struct Issuer {
                 tj = 0;
                 if (++ti == nrows) {
                     ti = 0;
-                    if (++i < ntile) tile_setup();
+                    if (++i < ntile) {
+                        if constexpr (C1) {
+                            m0 += m_step;
+                            tn += step_n;
+                            tp += step_p;
+                            if (tp >= ohw) { tp -= ohw; ++tn; }
+                        }
+                        tile_setup();
+                    }
                 }
             }
             tap_setup();
@@ -255,9 +334,15 @@ struct Issuer {
 // EPI 2: the register-only epilogue (epilogue_regs: no LDS, so hipcc does not drain the in-flight stages in front of
 // it) whose stores the next step's wait leaves in flight — both directions since round 4 (the LDS-transposed form
 // measured 2-7 % slower on every forward, profiles/r04/pipe_fwd_reg_epilogue_ab.txt)
-template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2>
+// ABL (ablations for measurement only, never selected by pipe_plan): 1 every stage DMA out of range (issued, nothing
+// fetched), 2 no MFMAs (fragments still read), 4 only the gathered input's DMAs out of range, 8 only the weights'
+// C1: one output class on maps of >= BM pixels (Issuer's fast path; the stride-2 data gradient's four classes and tiny
+// maps take the generic one)
+template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
-    constexpr int NS = 3;                     // LDS ring: stage g computing, g+1 and g+2 in flight
+    // NS: LDS ring of K stages — stage g computing, g+1 .. g+NS-1 in flight (3; 2 for the 64-KB+ stages of the
+    // 256-channel / 512-pixel tiles)
+    static_assert(NS == 2 || NS == 3, "ring depth");
     constexpr int RB = 128;                   // 64 K x 2 B per LDS row
     constexpr int NW = WM * WN;
     constexpr int AI = BN / 8 / NW;           // weight DMA instructions per wave per stage
@@ -290,7 +375,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     const int ntile = mt_lo < mt_hi ? (mt_hi - mt_lo + qstride - 1) / qstride : 0;
     const int n0 = nt * BN;
     int total = 0;                            // K steps of this workgroup's whole stream
-    if (a.ncls == 1) total = ntile * cls_of(a, 0).ntap * kc;
+    if (C1) total = ntile * a.KH * a.KW * kc;
+    else if (a.ncls == 1) total = ntile * cls_of(a, 0).ntap * kc;
     else
         for (int t = 0; t < ntile; ++t) total += cls_of(a, cls_find(a, mt_lo + t * qstride)).ntap * kc;
 
@@ -324,6 +410,13 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     };
     f32x4 acc[TM][TN];
     auto mma = [&](const bf16x8* fa, const bf16x8* fb) {
+        if constexpr ((ABL & 2) != 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -343,7 +436,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
 
-    Issuer<BM, BN, NW, MODE> is(a, wave, lane, mt_lo, qstride, ntile);
+    Issuer<BM, BN, NW, MODE, ABL, C1> is(a, wave, lane, mt_lo, qstride, ntile);
     is.start();
 
     // prologue: stages 0..2 in flight (stages past the stream's end fetch nothing); stage 0 landed
@@ -353,18 +446,38 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         is.issue_dma(smem + s * STAGE, wres, a_off, s < total);
         is.advance();
     }
-    vm_wait<2 * DPS>();
+    vm_wait<(NS - 1) * DPS>();
     step_barrier();
     if (total > 0) read_frags(f0a, f0b, 0, 0);
 
     // compute side: one K step per iteration; tiles end inside the stream
-    int ct = 0, ck = 0, cnk = 0, buf = 0;
+    int ct = 0, ck = 0, cnk = C1 ? a.KH * a.KW * kc : 0, buf = 0;
     int64_t m0 = 0;
     Cls cc{};
     uint32_t t_n = 0, t_p = 0;                // divmod(m0, OHW) of the computing tile
     float inv_owc = 1.f;
+    // C1: the computing tile's first pixel, advanced per tile as the issuer's
+    int c_m0 = 0, c_tn = 0;
+    uint32_t c_tp = 0;
+    if constexpr (C1) {
+        c_m0 = mt_lo * BM;
+        c_tn = int(uint32_t(c_m0) / is.ohw);
+        c_tp = uint32_t(c_m0) - uint32_t(c_tn) * is.ohw;
+    }
+    const int Mtot = a.N * int(is.ohw);
     for (int g = 0; g < total; ++g) {
-        if (ck == 0) {
+        if (C1 && ck == 0) {
+            if (ct > 0) {
+                c_m0 += is.m_step;
+                c_tn += is.step_n;
+                c_tp += is.step_p;
+                if (c_tp >= is.ohw) { c_tp -= is.ohw; ++c_tn; }
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        } else if (ck == 0) {
             const int mt = mt_lo + ct * qstride;
             const int c = cls_find(a, mt);
             cc = cls_of(a, c);
@@ -383,14 +496,14 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
         // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight (every step issues DPS DMAs,
         // live or not, so the count is constant); in a tile's first step the previous tile's epilogue stores,
         // issued after stage g+2's pieces, may stay in flight too
-        if (EPI == 2 && ck == 0 && ct > 0) vm_wait<DPS + EPS>();
-        else vm_wait<DPS>();
+        if (EPI == 2 && ck == 0 && ct > 0) vm_wait<(NS - 2) * DPS + EPS>();
+        else vm_wait<(NS - 2) * DPS>();
         step_barrier();
         // the slot of stage g is free again (every wave's reads of it returned before the barrier): stage
         // g+3's DMAs go out one at a time between the second half's MFMAs (issued in a burst they held both
         // waves of a SIMD off the MFMA pipe for the whole burst), then the next stage's first-half reads
         const int nbuf = buf == NS - 1 ? 0 : buf + 1;
-        is.issue_dma(smem + buf * STAGE, wres, a_off, g + 3 < total);
+        is.issue_dma(smem + buf * STAGE, wres, a_off, g + NS < total);
         read_frags(f0a, f0b, nbuf, 0);
         mma(f1a, f1b);
 #pragma unroll
@@ -415,6 +528,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
             const int64_t ybytes = (int64_t(a.N - 1) * a.y_bs + int64_t(a.OH) * a.OW * a.y_ld) * 2;
             const __amdgpu_buffer_rsrc_t yres = make_rsrc(a.y, ybytes);
             auto pix_off = [&](int qp) -> uint32_t {
+                if constexpr (C1) {
+                    // one class, stride-1 output: the output pixel IS the in-image offset (one wrap: ohw >= BM)
+                    const int q = wc * (BM / WN) + qp;
+                    if (c_m0 + q >= Mtot) return OOB;
+                    uint32_t pix = c_tp + uint32_t(q);
+                    int n = c_tn;
+                    if (pix >= is.ohw) { pix -= is.ohw; ++n; }
+                    return uint32_t((int64_t(n) * a.y_bs + int64_t(pix) * a.y_ld + wch0) * 2);
+                }
                 const int64_t m = m0 + wc * (BM / WN) + qp;
                 if (m >= cc.Mc) return OOB;
                 uint32_t n, pix, ci_;
@@ -422,7 +544,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 const int64_t opix = int64_t(ci_ * a.os + cc.py) * a.OW + int64_t(pix - ci_ * uint32_t(cc.OWc)) * a.os + cc.px;
                 return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
             };
-            auto pix_ok = [&](int qp) -> bool { return m0 + wc * (BM / WN) + qp < cc.Mc; };
+            auto pix_ok = [&](int qp) -> bool {
+                if constexpr (C1) return c_m0 + wc * (BM / WN) + qp < Mtot;
+                return m0 + wc * (BM / WN) + qp < cc.Mc;
+            };
             epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
                                   a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
         }
@@ -465,27 +590,51 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
     }
 }
 
-// tile configurations
+// tile configurations: 0 / 1 the shipped 16-wave 256 x 128 and 8-wave 256 x 64 tiles; 2 experimental
+// (ym_pipe_set_exp 1): 256 x 128 on 8 waves of 64 x 64 — round 5, same process: within +-3.5 % of the 16-wave tile
+// on every layer with 31 % fewer LDS-array cycles (profiles/r05/pipe_wave_tile_ab.txt), so the LDS array does not
+// bound it.  (256 x 256 / 512 x 128 tiles on 8 waves of 128 x 64 need 128 accumulator registers per lane and
+// spilled 213-439 VGPRs at the 256-register cap of two waves per SIMD: not kept.)
 struct Cfg {
     int bm, bn;
 };
-constexpr Cfg kCfg[] = {{256, 128}, {256, 64}};
+constexpr Cfg kCfg[] = {{256, 128}, {256, 64}, {256, 128}};
 
 // 256 x 128 tiles run on 16 waves of 32 x 64 (four per SIMD, 127 VGPRs): same staging and LDS as 8 waves
 // of 64 x 64, 1.5x the fragment reads, but while some waves of a SIMD issue their DMA pieces or wait at
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
+template <int MODE>
+void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
+    const bool c1 = a.ncls == 1 && int64_t(a.OH) * a.OW >= kCfg[cfg].bm && g_pipe_exp != 20;
+    if (cfg == 0 && g_pipe_exp >= 10 && g_pipe_exp < 20) {
+        switch (g_pipe_exp) {
+            case 10: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 1, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
+            case 11: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 2, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
+            case 12: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 4, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
+            default: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 8, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
+        }
+    }
+    if (c1) {
+        switch (cfg) {
+            case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(1024), 0, st>>>(a); break;
+            case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+            default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+        }
+        return;
+    }
+    switch (cfg) {
+        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2><<<dim3(grid), dim3(1024), 0, st>>>(a); break;
+        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+    }
+}
+
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     // both directions: the register-only epilogue (round 4 for the forward, with the statistics masked by a compare:
     // same-process A/B 2-7 % faster on every pipelined forward, profiles/r04/pipe_fwd_reg_epilogue_ab.txt)
-    if (mode == PF) {
-        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PF, 2><<<dim3(grid), dim3(1024), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PF, 2><<<dim3(grid), dim3(512), 0, st>>>(a);
-    } else {
-        // data gradient: register-only epilogue (same-process A/B, s@640 bs64: 1-8 % faster on 9 of 10 layers)
-        if (cfg == 0) conv_pipe_kernel<256, 128, 4, 4, PD, 2><<<dim3(grid), dim3(1024), 0, st>>>(a);
-        else conv_pipe_kernel<256, 64, 1, 8, PD, 2><<<dim3(grid), dim3(512), 0, st>>>(a);
-    }
+    if (mode == PF) launch_mode<PF>(cfg, a, grid, st);
+    else launch_mode<PD>(cfg, a, grid, st);
 }
 
 }  // namespace
@@ -515,6 +664,7 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     if (int64_t(OH) * OW >= (int64_t(1) << 24) || OH >= (1 << 16)) return p;
     const int64_t M = select_n(d) * ((OH + os - 1) / os) * ((OW + os - 1) / os) * os * os;
     p.cfg = nout >= 128 ? 0 : 1;
+    if (g_pipe_exp == 1 && nout >= 128) p.cfg = 2;
     const int bm = kCfg[p.cfg].bm, bn = kCfg[p.cfg].bn;
     const int ntiles = (nout + bn - 1) / bn;
     const int64_t tiles = (M / bm) * ntiles;
@@ -530,6 +680,12 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     p.rows = grid / ntiles;
     p.ok = 1;
     return p;
+}
+
+extern "C" int ym_pipe_set_exp(int v) {
+    const int prev = g_pipe_exp;
+    g_pipe_exp = v;
+    return prev;
 }
 
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
