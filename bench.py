@@ -39,6 +39,7 @@ for p in (str(ROOT), str(PKG)):
 METRIC = "images/sec at 640×640 bs=64/GPU, YOLOv11-s, 1/2/4/8 MI355X; mAP50 parity"
 PEAK_BF16_TFLOPS = 2500.0          # dense bf16 MFMA, MI355X_MICROARCH.md chip table
 HBM_PEAK_GBS = 8000.0
+DP_TRACE_STEPS = 3
 PROBE_STEPS = 3
 
 
@@ -134,6 +135,53 @@ def cpu_baseline(batch: int = 16, imgsz: int = 640, warmup: int = 1, steps: int 
     return {"value": round(batch / t, 3), "unit": "images/sec", "cores": threads, "kind": "port", **host,
             "sample": f"YOLOv11-s {imgsz}x{imgsz} bs={batch} full train step (fwd+loss+bwd+clip+AdamW), "
                       f"oracle fp32 restatement, median of {steps} steps after {warmup} warm-up"}
+
+
+def dp_overlap_probe(step_parts, dp, dev, first: int, steps: int) -> dict:
+    """Per-bucket collective start / end and the backward's end, in ms from the step's start (events on the
+    device; the median over `steps` steps), on THIS rank (rank 0's line).  Labelled unmeasured-on-hardware when
+    the collectives ran over gloo (a one-GPU rehearsal)."""
+    import statistics
+    import torch
+    import torch.distributed as dist
+    recs = []
+    dp.set_trace(True)
+    try:
+        for k in range(steps):
+            evs = {}
+
+            def mark(name):
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(torch.cuda.current_stream(dev))
+                evs[name] = e
+            step_parts(first + k, mark)
+            torch.cuda.synchronize(dev)
+            t0 = evs["start"]
+            tr = dp.last_trace()
+            recs.append({"backward_end": t0.elapsed_time(evs["backward_end"]),
+                         "sync_end": t0.elapsed_time(evs["sync_end"]),
+                         "buckets": [(r["bucket"], r["bytes"], t0.elapsed_time(r["start"]), t0.elapsed_time(r["end"]))
+                                     for r in tr if "start" in r]})
+    finally:
+        dp.set_trace(False)
+    med = lambda xs: round(statistics.median(xs), 3) if xs else None
+    nb = min(len(r["buckets"]) for r in recs) if recs else 0
+    buckets = []
+    for j in range(nb):
+        buckets.append({"bucket": recs[0]["buckets"][j][0], "mb": round(recs[0]["buckets"][j][1] / 2 ** 20, 2),
+                        "start_ms": med([r["buckets"][j][2] for r in recs]),
+                        "end_ms": med([r["buckets"][j][3] for r in recs])})
+    bwd = med([r["backward_end"] for r in recs])
+    sync_end = med([r["sync_end"] for r in recs])
+    coll = sum(b["end_ms"] - b["start_ms"] for b in buckets)
+    hidden = sum(max(0.0, min(b["end_ms"], bwd) - b["start_ms"]) for b in buckets) if bwd is not None else 0.0
+    backend = dist.get_backend()
+    return {"steps": steps, "backend": backend, "buckets": buckets, "backward_end_ms": bwd, "sync_end_ms": sync_end,
+            "exposed_ms": round(sync_end - bwd, 3) if bwd is not None else None,
+            "collective_ms": round(coll, 3), "collective_before_backward_end_frac": round(hidden / coll, 3) if coll else None,
+            "note": ("collectives bracketed by events on the comm stream (each waits for its collective: buckets serialized, "
+                     "as one process group's collectives are); times from the step's start on rank 0") +
+                    ("" if backend == "nccl" else "; gloo rehearsal, NOT an RCCL / xGMI measurement")}
 
 
 def needs_launch(gpus: int, env=None) -> bool:
@@ -255,18 +303,28 @@ def main():
         b = prepare_batch(b, dev)                  # the data path's H2D (records max_gt on the host)
         batches.append(b)
 
-    def step(i):
+    def step_parts(i, mark=None):
+        """One training step; mark(name) (optional) is called at its phase boundaries (dp_overlap_probe)."""
         b = batches[i % n_batches]
         opt.zero_grad(set_to_none=True)
+        if mark:
+            mark("start")
         preds = model(b["img"])
         loss, items = crit(preds, b)
         loss.backward()
+        if mark:
+            mark("backward_end")
         if dp:
             dp.sync()
+        if mark:
+            mark("sync_end")
         if not fuses_clip:
             torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=10.0)
         opt.step()
         return loss
+
+    def step(i):
+        return step_parts(i)
 
     # model setup: the plan's first forward/backward allocate its workspaces (and with YM_GRAPH=1
     # the second captures them as HIP graphs) — done here, untimed, whatever --warmup is
@@ -315,6 +373,10 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    # N > 1: where the bucket collectives ran against the backward (dp_overlap in the JSON line), over a few extra steps
+    # after the timed region with every collective bracketed by events on the comm stream (Buckets.trace); the
+    # exposed communication is what the step waits for after the backward's last kernel
+    dp_overlap = dp_overlap_probe(step_parts, dp, dev, args.warmup + args.steps, DP_TRACE_STEPS) if dp else None
     # the probe and family passes time the conv kernels' own work: there the forward BatchNorm finalize runs as its
     # own launch (YM_FOLD=0, timed in the 'bn' family) instead of as the conv launch's tail (the timed region above
     # and the driver's step run it folded)
@@ -467,6 +529,8 @@ def main():
         "probe": {"key": probe_key, "rank": probe_rank, "count": probe_count},
         "host_enqueue_ms_per_step": round(host_ms, 3),
     }
+    if dp_overlap is not None:
+        out["dp_overlap"] = dp_overlap
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline()

@@ -111,6 +111,47 @@ def _bucket_worker(rank, world, port, q):
         q.put((rank, "error", repr(e)))
 
 
+def _trace_worker(rank, world, port, q):
+    """Measurement mode (GradSync.set_trace, bench.py's dp_overlap at N > 1): every bucket's collective is recorded
+    once per step, the results are unchanged, and switching it off restores the untraced launches."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        from yolomi import dist as ydist
+        ctx = ydist.init_from_env("gloo")
+        m = torch.nn.Sequential(*[torch.nn.Linear(64, 64) for _ in range(6)])
+        plan = _FakePlan(m)
+        m.__dict__["_ym_last_plan"] = plan
+        sync = ydist.GradSync(m, ctx, bucket_mb=0.02)
+        res, traces = [], []
+        for step in range(4):
+            sync.set_trace(step in (1, 2))
+            plan.backward(rank, step)
+            sync.sync()
+            traces.append([(r["bucket"], r["bytes"], r["host_done"] >= r["host_issue"]) for r in sync.last_trace()]
+                          if step in (1, 2) else None)
+            res.append([float(plan.grad_views[id(p)].mean()) for p in plan.params])
+        b = sync.buckets[id(plan)]
+        q.put((rank, res, traces, len(b.ranges), [(e - s) * 4 for s, e in b.ranges], b.trace is None))
+        ydist.shutdown()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e)))
+
+
+def test_bucket_trace_world2_gloo():
+    res = _spawn(_trace_worker)
+    for r in range(2):
+        _, means, traces, nb, sizes, off = res[r]
+        for step, ms in enumerate(means):
+            for i, g in enumerate(ms):
+                assert g == pytest.approx(1.5 * (i + 1) * (step + 1)), (r, step, i)
+        for t in traces[1:3]:
+            assert sorted(x[0] for x in t) == list(range(nb))           # every bucket once per step
+            assert all(x[2] for x in t)
+            assert sorted(x[1] for x in t) == sorted(sizes)
+        assert traces[0] is None and traces[3] is None and off
+
+
 def test_bucketed_overlap_world2_gloo():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")

@@ -90,6 +90,10 @@ class Buckets:
         self.remaining = []
         self.streams = None        # callable -> the producing plan's streams (yolomi.graph.Plan.comm_streams)
         self.comm = None           # the stream the bucket collectives are issued from (created on first use)
+        # measurement mode (GradSync.trace; bench.py's dp_overlap at N > 1): per launched bucket, where its
+        # collective starts and ends on the device (events on the comm stream, the end after the collective's
+        # own stream has finished it) or on the host (gloo on CPU tensors)
+        self.trace = None
 
     def _close(self, start, size, members):
         b = len(self.ranges)
@@ -118,6 +122,8 @@ class Buckets:
                 self._launch(b)
 
     def _launch(self, b):
+        if self.trace is not None:
+            return self._launch_traced(b)
         s, e = self.ranges[b]
         writes = self.writes[b] if getattr(self, "writes", None) else {}
         streams = self.streams() if self.streams else []
@@ -142,6 +148,40 @@ class Buckets:
                 comm.wait_stream(o)
             with torch.cuda.stream(comm):
                 self.handles.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True))
+        self.launched[b] = True
+
+    def _launch_traced(self, b):
+        """_launch with each collective bracketed: the start event after the bucket's write events (where the
+        comm stream can start it), the end event after the comm stream has waited for the collective (on RCCL's
+        internal stream), so end - start is the collective's wall time on the device.  The extra waits serialize
+        the buckets on the comm stream, as RCCL serializes one process group's collectives anyway."""
+        import time
+        s, e = self.ranges[b]
+        rec = {"bucket": b, "bytes": (e - s) * self.flat.element_size(), "host_issue": time.perf_counter()}
+        if self.flat.is_cuda:
+            if self.comm is None:
+                self.comm = torch.cuda.Stream(device=self.flat.device)
+            writes = self.writes[b] if getattr(self, "writes", None) else {}
+            if writes:
+                for ev in writes.values():
+                    self.comm.wait_event(ev)
+            else:
+                for o in (self.streams() if self.streams else []):
+                    self.comm.wait_stream(o)
+                self.comm.wait_stream(torch.cuda.current_stream(self.flat.device))
+            rec["start"], rec["end"] = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(self.comm):
+                rec["start"].record(self.comm)
+                h = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True)
+                h.wait()                          # the comm stream waits for the collective's own stream
+                rec["end"].record(self.comm)
+            self.handles.append(h)
+        else:
+            h = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, async_op=True)
+            h.wait()
+            rec["host_done"] = time.perf_counter()
+            self.handles.append(h)
+        self.trace.append(rec)
         self.launched[b] = True
 
     def finish(self, world: int):
@@ -177,6 +217,8 @@ class GradSync:
             return
         b = Buckets(plan.grad_flat, plan.params, plan.grad_views, self.cap)
         b.streams = getattr(plan, "comm_streams", None)
+        if getattr(self, "_trace_on", False):
+            b.trace = []
         self.buckets[id(plan)] = b
 
         def hook(params, writes=None, _b=b, _plan=plan):
@@ -187,8 +229,31 @@ class GradSync:
             _b.ready(params, writes)
         plan.grad_hook = hook
 
+    def set_trace(self, on: bool):
+        """Measurement mode for the following steps: every plan's buckets record their collectives (Buckets.trace);
+        last_trace() returns the records of the latest step."""
+        self._trace_on = on
+        for b in self.buckets.values():
+            if b is not None:
+                b.trace = [] if on else None
+
+    def last_trace(self):
+        return list(getattr(self, "_last_trace", []))
+
     def sync(self):
         plan = self.model.__dict__.get("_ym_last_plan")
+        tr = None
+        if getattr(self, "_trace_on", False) and plan is not None:
+            b = self.buckets.get(id(plan))
+            tr = b.trace if b is not None else None
+        try:
+            self._sync(plan)
+        finally:
+            if tr is not None:
+                self._last_trace = list(tr)
+                tr.clear()
+
+    def _sync(self, plan):
         if self.model.__dict__.pop("_ym_pooled_step", False):
             # several forwards were in flight before this step's backwards (yolomi.graph.run_model): their
             # plans' gradients were added together into .grad, which is reduced below as one buffer; the
