@@ -451,8 +451,11 @@ def test_conv_fwd_bias_on_every_policy(k, out_f32):
     prev = (L.ym_conv_set_hpipe(2), L.ym_conv_set_direct(2), L.ym_conv_set_pipe(2), L.ym_conv_set_halo(1))
     try:
         y = torch.zeros(n, h, w, cout, dtype=torch.float16 if out_f32 == 2 else torch.bfloat16, device=dev)
-        call("ym_conv_fwd", ctypes.byref(d), x.to(dev).data_ptr(), wt.permute(0, 2, 3, 1).contiguous().to(dev).data_ptr(),
-             y.data_ptr(), bias.to(dev).data_ptr(), None, None, torch.cuda.current_stream().cuda_stream)
+        # device copies held in names: a temporary's block returns to the caching allocator as soon as its
+        # data_ptr() is taken, and the next argument's copy can land in it (round 5: x overwritten by the bias)
+        xd, wd, bd = x.to(dev), wt.permute(0, 2, 3, 1).contiguous().to(dev), bias.to(dev)
+        call("ym_conv_fwd", ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), y.data_ptr(), bd.data_ptr(), None, None,
+             torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
     finally:
         L.ym_conv_set_hpipe(prev[0]); L.ym_conv_set_direct(prev[1]); L.ym_conv_set_pipe(prev[2]); L.ym_conv_set_halo(prev[3])

@@ -158,14 +158,20 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     // ---- issue side: weight stage s -> (chunk, tap); halo of global chunk h -> (tile, chunk)
     // weight stage s into its ring slot; past the stream's end (live false) the DMAs fetch nothing but still
     // count, so every step issues AI of them and the counted waits stay constant
-    auto issue_w = [&](int s, bool live) {
+    // issue position of the weight stream (stage s = g + NS): tap / chunk / ring slot advanced per stage — round 5: the
+    // divisions by the steps per tile (s % spt, / 9, % NS) this replaced ran twice per step on each side of the loop
+    int w_tap = 0, w_cc = 0, w_slot = 0;
+    auto issue_w = [&](bool live) {
         if constexpr (WRES) return;
-        const int within = s % spt;
-        const int cc = within / 9, tap = within - cc * 9;
-        const uint32_t soff = uint32_t(tap * a.Kin + cc * 64) * 2u;
-        char* st = wring + (s % NS) * WSLOT;
+        const uint32_t soff = uint32_t(w_tap * a.Kin + w_cc * 64) * 2u;
+        char* st = wring + w_slot * WSLOT;
 #pragma unroll
         for (int j = 0; j < AI; ++j) dma16(wres, st + (wave * AI + j) * 1024, live ? a_off[j] : OOB, soff);
+        if (++w_tap == 9) {
+            w_tap = 0;
+            if (++w_cc == CC) w_cc = 0;
+        }
+        w_slot = w_slot == NS - 1 ? 0 : w_slot + 1;
     };
     uint32_t hoff[HI_MAX];                    // per-lane halo offsets of the tile being staged
     int h_tile = -1;
@@ -200,13 +206,20 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
     }
     bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
-    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int g, int kk) {
-        const int within = g % spt;
-        const int cc = within / 9, tap = within - cc * 9;
-        const int kh = tap / 3, kw = tap - kh * 3;
-        const int dh = MODE == HF ? kh : 2 - kh, dw = MODE == HF ? kw : 2 - kw;
-        const char* As = wring + (g % NS) * WSLOT + offA[kk];
-        const char* Hs = hbuf0 + ((g / spt * CC + cc) & 1) * HBUF;
+    // compute-side position of a step: (kh, kw) of its tap, its weight ring slot, the halo buffer of its chunk
+    struct Pos { int kh, kw, slot, hb; };
+    auto next_pos = [&](Pos p) {
+        if (++p.kw == 3) {
+            p.kw = 0;
+            if (++p.kh == 3) { p.kh = 0; p.hb ^= 1; }       // a chunk's 9 taps done: the next chunk's halo buffer
+        }
+        p.slot = p.slot == NS - 1 ? 0 : p.slot + 1;
+        return p;
+    };
+    auto read_frags = [&](bf16x8* fa, bf16x8* fb, Pos p, int kk) {
+        const int dh = MODE == HF ? p.kh : 2 - p.kh, dw = MODE == HF ? p.kw : 2 - p.kw;
+        const char* As = wring + (WRES ? (p.kh * 3 + p.kw) : p.slot) * WSLOT + offA[kk];
+        const char* Hs = hbuf0 + p.hb * HBUF;
 #pragma unroll
         for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
 #pragma unroll
@@ -251,13 +264,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     } else {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
-            issue_w(s, s < total);
+            issue_w(s < total);
         vm_wait_n(AI * (NS - 1));
     }
     step_barrier();
-    if (total > 0) read_frags(f0a, f0b, 0, 0);
+    Pos pos{0, 0, 0, 0};
+    if (total > 0) read_frags(f0a, f0b, pos, 0);
 
     int ct = 0, ck = 0;
+    int c9 = 0, hc = 0;                       // g % 9 and g / 9 (the step's tap and global chunk), kept by counting
     for (int g = 0; g < total; ++g) {
         if (ck == 0) {
 #pragma unroll
@@ -265,30 +280,29 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        read_frags(f1a, f1b, g, 1);
+        read_frags(f1a, f1b, pos, 1);
         mma(f0a, f0b);
         // stage g+1 must have landed (own DMAs); stages g+2 and g+3 may stay in flight, and so may halos
         // issued in steps g-2 and g-1 (after stage g+1, when those steps began a chunk with a successor)
         if (WRES) {
             // the only in-loop DMA is the next chunk's halo (issued 9 steps ahead): retire it before its first read
-            if (g + 1 < total && (g + 1) % 9 == 0) vm_wait<0>();
+            if (g + 1 < total && c9 == 8) vm_wait<0>();
         } else if (g + 1 < total) {
-            int pend = 2 * AI;
-#pragma unroll
-            for (int b = 1; b <= 2; ++b) {
-                const int gs = g - b;
-                if (gs >= 0 && gs % 9 == 0 && gs / 9 + 1 < nchunks) pend += hi_w;
-            }
-            vm_wait_n(pend);
+            // a halo issued in step g-1 or g-2 (a chunk's first step, when a next chunk exists) is younger than stage
+            // g+1 and may stay in flight
+            vm_wait_n(2 * AI + ((c9 == 1 || c9 == 2) && hc + 1 < nchunks ? hi_w : 0));
         }
         step_barrier();
         // the halo buffer of chunk h-1 and the weight slot of step g are free (their reads returned before
         // the barrier): the next chunk's halo at its predecessor's first step, then weight stage g+4
-        if (g % 9 == 0 && g / 9 + 1 < nchunks) issue_h(g / 9 + 1);
+        if (c9 == 0 && hc + 1 < nchunks) issue_h(hc + 1);
         // the weight DMAs one at a time between the second half's MFMAs (a burst held both waves of a SIMD
         // off the MFMA pipe), then the next step's first-half reads (harmless past the end)
-        issue_w(g + NS, g + NS < total);
-        read_frags(f0a, f0b, g + 1, 0);
+        issue_w(g + NS < total);
+        const Pos npos = next_pos(pos);
+        read_frags(f0a, f0b, npos, 0);
+        pos = npos;
+        if (++c9 == 9) { c9 = 0; ++hc; }
         mma(f1a, f1b);
         if constexpr (!WRES) {
 #pragma unroll

@@ -173,6 +173,10 @@ struct Issuer {
         : a(a_), wave(wave_), lrow(lane >> 3), lslot(lane & 7), kc(a_.Kin >> 6), xld_b(uint32_t(a_.x_ld) * 2u),
           mt_lo(mt_lo_), qstride(qstride_), ntile(ntile_) {
         if constexpr (C1) {
+            // a zero-record resource until the first tile_setup: a workgroup without tiles still issues its prologue's
+            // (out-of-range) DMAs through it, and an uninitialised descriptor made them real loads (a memory fault at
+            // s@640 bs2 under ym_conv_set_select_batch(64), where most of the grid has no tile)
+            xres_t = make_rsrc(a.x, 0);
             ohw = uint32_t(a.OH) * uint32_t(a.OW);
             m0 = mt_lo * BM;
             tn = int(uint32_t(m0) / ohw);
