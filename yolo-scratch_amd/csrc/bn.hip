@@ -60,7 +60,7 @@ __device__ __forceinline__ void unpack8h(uint4 v, float* f) {
 __device__ __forceinline__ uint4 pack8h(const float* f) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2h(f[2 * i])) | (uint32_t(f2h(f[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pk2h(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {

@@ -58,9 +58,19 @@ __device__ __forceinline__ uint32_t pk2bf(float lo, float hi) {
 // fp16 bits <-> f32 (pre-BatchNorm conv outputs are kept in fp16: 3 more mantissa bits than
 // bf16 where normalisation amplifies rounding; |z| is clamped below the fp16 range)
 __device__ __forceinline__ float h2f(uint16_t v) { return __half2float(__ushort_as_half(v)); }
+// the clamp is one v_med3_f32 (IEEE minNum semantics: a NaN input comes out as -65504, as the fminf / fmaxf pair gave)
 __device__ __forceinline__ uint16_t f2h(float f) {
-    f = fminf(fmaxf(f, -65504.f), 65504.f);
+    f = __builtin_amdgcn_fmed3f(f, -65504.f, 65504.f);
     return __half_as_ushort(__float2half(f));
+}
+// two floats -> packed fp16 pair (lo in bits 0..15), clamped: two v_med3_f32 + one v_cvt_pk_f16_f32 (round 5: the
+// per-value fminf / fmaxf / cvt / shift / or sequence it replaces was 7 VALU per pair, a third of the 1x1 conv
+// epilogues' vector instructions)
+__device__ __forceinline__ uint32_t pk2h(float lo, float hi) {
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    f2_t v = {__builtin_amdgcn_fmed3f(lo, -65504.f, 65504.f), __builtin_amdgcn_fmed3f(hi, -65504.f, 65504.f)};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, h2_t));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

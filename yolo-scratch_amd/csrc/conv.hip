@@ -140,6 +140,19 @@ conv_gemm_kernel(GemmArgs a) {
     const int nk = ntap * kc;
     const uint32_t OHW = uint32_t(OHc) * uint32_t(OWc);
     const int64_t Mc = int64_t(a.N) * OHW;
+    // pixel decompositions by float reciprocals where every flat pixel index is exact as a float (round 5: the per-tile
+    // 64-bit division and per-row 32-bit divisions of the tile setup and the epilogue were most of this kernel's
+    // 7 VALU per MFMA on the short-K layers); larger maps keep the integer divisions
+    const bool fdiv = Mc < (int64_t(1) << 24);
+    const float inv_ohw = 1.0f / float(OHW), inv_owc = 1.0f / float(OWc);
+    auto dm_ohw = [&](uint32_t x, uint32_t& q, uint32_t& r) {
+        if (fdiv) fdivmod(x, OHW, inv_ohw, q, r);
+        else { q = x / OHW; r = x - q * OHW; }
+    };
+    auto dm_owc = [&](uint32_t x, uint32_t& q, uint32_t& r) {
+        if (fdiv) fdivmod(x, uint32_t(OWc), inv_owc, q, r);
+        else { q = x / uint32_t(OWc); r = x - q * uint32_t(OWc); }
+    };
     const int mtiles = int((Mc + BM - 1) / BM);
     const uint32_t wrow_b = uint32_t(a.KH * a.KW * a.Kin) * 2u;
     const uint32_t xld_b = uint32_t(a.x_ld) * 2u;
@@ -169,7 +182,7 @@ conv_gemm_kernel(GemmArgs a) {
     const int mt_end = min((xcd + 1) * per_xcd, mtiles);
     for (int mt = xcd * per_xcd + (bx >> 3); mt < mt_end; mt += lstride) {
         const int64_t m0 = int64_t(mt) * BM;
-        const uint32_t nfirst = uint32_t(m0 / OHW);
+        const uint32_t nfirst = uint32_t(m0) / OHW;          // Mc < 2^31 (host check): one 32-bit scalar division
         const __amdgpu_buffer_rsrc_t xres =
             make_rsrc(a.x + int64_t(nfirst) * a.x_bs, (int64_t(a.N) - nfirst) * a.x_bs * 2);
         int b_oh[BI], b_ow[BI];
@@ -179,16 +192,18 @@ conv_gemm_kernel(GemmArgs a) {
             const int r = (wave * BI + j) * RPI + lrow;
             const int64_t m = m0 + r;
             const uint32_t um = m < Mc ? uint32_t(m) : 0u;
-            const uint32_t n = um / OHW, pix = um - n * OHW;
-            const uint32_t i = pix / uint32_t(OWc);
+            uint32_t n, pix, i, col;
+            dm_ohw(um, n, pix);
+            dm_owc(pix, i, col);
             b_chk[j] = uint32_t(lslot ^ fsw<RB>(r)) * 8u;
             b_img[j] = m < Mc ? (n - nfirst) * uint32_t(a.x_bs) * 2u : OOB;
             b_oh[j] = int(i) * os + py;
-            b_ow[j] = int(pix - i * uint32_t(OWc)) * os + px;
+            b_ow[j] = int(col) * os + px;
         }
-        auto tap_setup = [&](int t) {
-            const int ti = t / nkw;
-            const int kh = kh0 + ti * os, kw = kw0 + (t - ti * nkw) * os;
+        int t_i = 0, t_j = 0;                // (row, column) of the next staged tap among the class's taps
+        auto tap_setup = [&]() {
+            const int kh = kh0 + t_i * os, kw = kw0 + t_j * os;
+            if (++t_j == nkw) { t_j = 0; ++t_i; }
 #pragma unroll
             for (int j = 0; j < BI; ++j) {
                 int gh, gw;
@@ -204,11 +219,11 @@ conv_gemm_kernel(GemmArgs a) {
             }
             return uint32_t((kh * a.KW + kw) * a.Kin) * 2u;
         };
-        int t_next = 0, c_next = 0;
+        int c_next = 0;
         uint32_t a_tap = 0;
         // issue one stage of LDS-DMA: AI + BI buffer_load_dwordx4 ... lds per wave
         auto issue = [&](int buf) {
-            if (c_next == 0) a_tap = tap_setup(t_next);
+            if (c_next == 0) a_tap = tap_setup();
             const int k0 = c_next * BK;
             char* st = smem + buf * STAGE;
 #pragma unroll
@@ -226,7 +241,7 @@ conv_gemm_kernel(GemmArgs a) {
                     xres, (__attribute__((address_space(3))) void*)(st + BN * RB + (wave * BI + j) * 1024), 16, off,
                     0, 0, 0);
             }
-            if (++c_next == kc) { c_next = 0; ++t_next; }
+            if (++c_next == kc) c_next = 0;
         };
 
         f32x4 acc[TM][TN];
@@ -300,9 +315,10 @@ conv_gemm_kernel(GemmArgs a) {
                 auto pix_off = [&](int q) -> uint32_t {
                     const int64_t m = m0 + wc * (BM / WN) + q;
                     if (m >= Mc) return OOB;
-                    const uint32_t n = uint32_t(m) / OHW, pix = uint32_t(m) - n * OHW;
-                    const uint32_t ci_ = pix / uint32_t(OWc);
-                    const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(pix - ci_ * uint32_t(OWc)) * os + px;
+                    uint32_t n, pix, ci_, col;
+                    dm_ohw(uint32_t(m), n, pix);
+                    dm_owc(pix, ci_, col);
+                    const int64_t opix = int64_t(ci_ * os + py) * a.OW + int64_t(col) * os + px;
                     return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
                 };
                 auto pix_ok = [&](int q) -> bool { return m0 + wc * (BM / WN) + q < Mc; };
@@ -338,8 +354,8 @@ conv_gemm_kernel(GemmArgs a) {
                     uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + obase + cb;
                     if (cb + 3 < a.Nout) {
                         uint2 o;
-                        o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
-                        o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
+                        o.x = pk2h(v[0], v[1]);
+                        o.y = pk2h(v[2], v[3]);
                         *reinterpret_cast<uint2*>(yp) = o;
                     } else {
 #pragma unroll
@@ -450,10 +466,10 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
             lq[r] += s * s;
         }
         uint4 o;
-        o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
-        o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
-        o.z = uint32_t(f2h(v[4])) | (uint32_t(f2h(v[5])) << 16);
-        o.w = uint32_t(f2h(v[6])) | (uint32_t(f2h(v[7])) << 16);
+        o.x = pk2h(v[0], v[1]);
+        o.y = pk2h(v[2], v[3]);
+        o.z = pk2h(v[4], v[5]);
+        o.w = pk2h(v[6], v[7]);
         if (y) *reinterpret_cast<uint4*>(y + size_t(m) * Cout + g * 8) = o;   // null: statistics only
     }
     // lanes with the same channel group: xor-reduce over the other lane bits, then the waves in order
@@ -582,10 +598,10 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
                 }
             }
         uint4 o;
-        o.x = uint32_t(f2h(s[0])) | (uint32_t(f2h(s[1])) << 16);
-        o.y = uint32_t(f2h(s[2])) | (uint32_t(f2h(s[3])) << 16);
-        o.z = uint32_t(f2h(s[4])) | (uint32_t(f2h(s[5])) << 16);
-        o.w = uint32_t(f2h(s[6])) | (uint32_t(f2h(s[7])) << 16);
+        o.x = pk2h(s[0], s[1]);
+        o.y = pk2h(s[2], s[3]);
+        o.z = pk2h(s[4], s[5]);
+        o.w = pk2h(s[6], s[7]);
         *reinterpret_cast<uint4*>(a.y + size_t(m) * a.C + c0) = o;
 #pragma unroll
         for (int r = 0; r < 8; ++r) { ls[r] += s[r]; lq[r] += s[r] * s[r]; }

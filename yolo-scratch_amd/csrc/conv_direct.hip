@@ -227,8 +227,8 @@ __device__ __forceinline__ void direct_body(const DirArgs& a, float (&ssum)[NT][
                         ssum[nt][r] += v[r];
                         ssq[nt][r] += v[r] * v[r];
                     }
-                    o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
-                    o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
+                    o.x = pk2h(v[0], v[1]);
+                    o.y = pk2h(v[2], v[3]);
                 } else {
                     float w4[4] = {v[0], v[1], v[2], v[3]};
                     if (a.accumulate) {

@@ -46,8 +46,8 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
             }
             uint2 o;
             if (half) {
-                o.x = uint32_t(f2h(acc[i][j][0])) | (uint32_t(f2h(acc[i][j][1])) << 16);
-                o.y = uint32_t(f2h(acc[i][j][2])) | (uint32_t(f2h(acc[i][j][3])) << 16);
+                o.x = pk2h(acc[i][j][0], acc[i][j][1]);
+                o.y = pk2h(acc[i][j][2], acc[i][j][3]);
             } else {
                 o.x = pk2bf(acc[i][j][0], acc[i][j][1]);
                 o.y = pk2bf(acc[i][j][2], acc[i][j][3]);
@@ -114,7 +114,7 @@ __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum
         }
     }
     auto pack = [&](float lo, float hi) -> uint32_t {
-        return half ? (uint32_t(f2h(lo)) | (uint32_t(f2h(hi)) << 16)) : pk2bf(lo, hi);
+        return half ? pk2h(lo, hi) : pk2bf(lo, hi);
     };
 #pragma unroll
     for (int jp = 0; jp < TN / 2; ++jp) {

@@ -57,6 +57,12 @@ struct HaloArgs {
 // (bank-conflict model over the kernel's fragment rows: 7.3-9.4 LDS cycles per read -> 4.0-6.4).
 __device__ __forceinline__ int fsw64(int r) { return ((r >> 2) & 1) << 1; }
 
+// one 1-KiB LDS-DMA piece: lane l's 16 bytes from rsrc + voff + soff land at lds + 16 l.  (A function, not the builtin
+// written inline in the kernel's lambdas: there hipcc's host pass silently dropped the kernels' launch stubs.)
+__device__ __forceinline__ void dma16h(__amdgpu_buffer_rsrc_t r, char* lds, uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, soff, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
     static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -111,13 +117,37 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
     // weight DMA: instruction j of this wave fills slot rows (wave*WI + j)*16 + lane/4 (row = tap-in-row x BN + channel),
     // 16-B slot lane%4
     const __amdgpu_buffer_rsrc_t wres = make_rsrc(a.w, int64_t(a.Nout) * wrow_b);
-    uint32_t a_off[WI], a_chk[WI];
+    // per-lane weight offsets including the lane's swizzled 16-B chunk; the step's (kernel row, 32-channel chunk) goes
+    // in the DMA's scalar soffset (Kin % 32 == 0, halo_plan): no vector instructions per DMA (round 5: the per-DMA
+    // bounds selects of the generic form were ~5 VALU each, and the kernel ran 7.7 VALU per MFMA)
+    // (Kin % 32 != 0: the last chunk's lanes past Kin go out of range in a separate, branched-to issue loop)
+    uint32_t a_off[WI];
+    int a_ch[WI];
 #pragma unroll
     for (int j = 0; j < WI; ++j) {
         const int r = (wave * WI + j) * 16 + (lane >> 2);
         const int ti = r / BN, co = n0 + (r & (BN - 1));
-        a_chk[j] = uint32_t((lane & 3) ^ fsw64(r)) * 8u;
-        a_off[j] = co < a.Nout ? uint32_t(co) * wrow_b + uint32_t(ti * a.Kin) * 2u : OOB;
+        a_ch[j] = ((lane & 3) ^ fsw64(r)) * 8;
+        a_off[j] = co < a.Nout ? uint32_t(co) * wrow_b + uint32_t(ti * a.Kin) * 2u + uint32_t(a_ch[j]) * 2u : OOB;
+    }
+    const int k_tail = (a.Kin & 31) ? (a.Kin >> 5) : -1;       // the partial last chunk, if any
+    // tile-invariant geometry of this lane's halo DMA rows and fragment pixels (hoisted out of the tile loop)
+    int h_r[HI], h_c[HI], h_ch[HI];
+#pragma unroll
+    for (int j = 0; j < HI; ++j) {
+        const int r = (wave * HI + j) * 16 + (lane >> 2);
+        h_r[j] = r < a.HP ? r / HWd : -(1 << 20);               // rows past the halo: never in the map
+        h_c[j] = r - (r / HWd) * HWd;
+        h_ch[j] = ((lane & 3) ^ fsw64(r)) * 8;
+    }
+    const int ntp0 = a.TH * a.TW;
+    int f_ph[TPW], f_pw[TPW], hb[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j) {
+        const int p = (wp * TPW + j) * 16 + fr;
+        f_ph[j] = p < ntp0 ? p / a.TW : (1 << 20);              // pixels past the tile: never in the output
+        f_pw[j] = p - (p / a.TW) * a.TW;
+        hb[j] = p < ntp0 ? (p / a.TW) * HWd + f_pw[j] : 0;
     }
     float ssum[TCW][4], ssq[TCW][4];
 #pragma unroll
@@ -135,51 +165,45 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
         const int oh0 = (rem / a.CT) * a.TH, ow0 = (rem % a.CT) * a.TW;
         const int ih0 = oh0 - 1, iw0 = ow0 - 1;
         const __amdgpu_buffer_rsrc_t xres = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
-        // halo DMA rows of this lane
-        uint32_t h_off[HI], h_chk[HI];
+        // halo DMA rows of this lane (chunk offsets in soffset); vmask bit j: fragment pixel j lies in the output (the
+        // register epilogue's statistics mask)
+        uint32_t h_off[HI];
 #pragma unroll
         for (int j = 0; j < HI; ++j) {
-            const int r = (wave * HI + j) * 16 + (lane >> 2);
-            const int hr = r / HWd, hc = r - hr * HWd;
-            const int gh = ih0 + hr, gw = iw0 + hc;
-            const bool ok = r < a.HP && gh >= 0 && gh < a.GH && gw >= 0 && gw < a.GW;
-            h_chk[j] = uint32_t((lane & 3) ^ fsw64(r)) * 8u;
-            h_off[j] = ok ? uint32_t(gh * a.GW + gw) * xld_b : OOB;
+            const int gh = ih0 + h_r[j], gw = iw0 + h_c[j];
+            const bool ok = uint32_t(gh) < uint32_t(a.GH) && uint32_t(gw) < uint32_t(a.GW);
+            h_off[j] = ok ? uint32_t(gh * a.GW + gw) * xld_b + uint32_t(h_ch[j]) * 2u : OOB;
         }
-        // halo row of each fragment pixel (tap (0,0) in forward order); vmask bit j: fragment pixel j lies in the
-        // output (the register epilogue's statistics mask)
-        int hb[TPW];
         uint32_t vmask = 0;
 #pragma unroll
-        for (int j = 0; j < TPW; ++j) {
-            const int p = (wp * TPW + j) * 16 + fr;
-            const int ph = p / a.TW, pw = p - ph * a.TW;
-            hb[j] = p < ntp ? ph * HWd + pw : 0;
-            vmask |= (p < ntp && oh0 + ph < a.OH && ow0 + pw < a.OW ? 1u : 0u) << j;
-        }
+        for (int j = 0; j < TPW; ++j) vmask |= (oh0 + f_ph[j] < a.OH && ow0 + f_pw[j] < a.OW ? 1u : 0u) << j;
 
         auto issue_halo = [&](int cc) {
             char* dst = hbuf + (cc & 1) * HBUF;
-            const uint32_t k0 = uint32_t(cc) * 32u;
+            if (cc == k_tail) {
 #pragma unroll
-            for (int j = 0; j < HI; ++j) {
-                const uint32_t kk = k0 + h_chk[j];
-                const uint32_t off = (kk < uint32_t(a.Kin) && h_off[j] != OOB) ? h_off[j] + kk * 2u : OOB;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    xres, (__attribute__((address_space(3))) void*)(dst + (wave * HI + j) * 1024), 16, off, 0, 0, 0);
+                for (int j = 0; j < HI; ++j)
+                    dma16h(xres, dst + (wave * HI + j) * 1024, cc * 32 + h_ch[j] < a.Kin ? h_off[j] : OOB, uint32_t(cc) * 64u);
+                return;
             }
+#pragma unroll
+            for (int j = 0; j < HI; ++j) dma16h(xres, dst + (wave * HI + j) * 1024, h_off[j], uint32_t(cc) * 64u);
         };
-        auto issue_w = [&](int k) {
-            const int cc = k / 3, kh = k - cc * 3;
-            char* dst = wring + (k % NW) * WSLOT;
+        // weight stream position (step k's chunk / kernel row / ring slot), advanced per issued step
+        int w_cc = 0, w_kh = 0, w_slot = 0;
+        auto issue_w = [&]() {
+            char* dst = wring + w_slot * WSLOT;
+            const uint32_t soff = uint32_t(w_kh * 3 * a.Kin + w_cc * 32) * 2u;
+            if (w_cc == k_tail) {
 #pragma unroll
-            for (int j = 0; j < WI; ++j) {
-                const uint32_t kk = uint32_t(cc) * 32u + a_chk[j];
-                const uint32_t off =
-                    (kk < uint32_t(a.Kin) && a_off[j] != OOB) ? a_off[j] + (uint32_t(kh * 3 * a.Kin) + kk) * 2u : OOB;
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                    wres, (__attribute__((address_space(3))) void*)(dst + (wave * WI + j) * 1024), 16, off, 0, 0, 0);
+                for (int j = 0; j < WI; ++j)
+                    dma16h(wres, dst + (wave * WI + j) * 1024, w_cc * 32 + a_ch[j] < a.Kin ? a_off[j] : OOB, soff);
+            } else {
+#pragma unroll
+                for (int j = 0; j < WI; ++j) dma16h(wres, dst + (wave * WI + j) * 1024, a_off[j], soff);
             }
+            if (++w_kh == 3) { w_kh = 0; ++w_cc; }
+            w_slot = w_slot == NW - 1 ? 0 : w_slot + 1;
         };
 
         f32x4 acc[TCW][TPW];
@@ -192,8 +216,8 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
         issue_halo(0);
 #pragma unroll
         for (int s = 0; s < NW - 1; ++s)
-            if (s < nk) issue_w(s);
-        int cc = 0, kh = 0;
+            if (s < nk) issue_w();
+        int cc = 0, kh = 0, slot = 0;
         for (int k = 0; k < nk; ++k) {
             // pending after the wait: the younger weight slots, and the next chunk's halo when it was
             // issued after this step's weights (at kernel row 0 of this chunk)
@@ -202,9 +226,10 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
             wait_vm_dyn<WI * (NW - 2) + HI>(pend);
             raw_barrier();
             if (kh == 0 && cc + 1 < CC) issue_halo(cc + 1);
-            if (k + NW - 1 < nk) issue_w(k + NW - 1);
+            if (k + NW - 1 < nk) issue_w();
 
-            const char* As = wring + (k % NW) * WSLOT;
+            const char* As = wring + slot * WSLOT;
+            slot = slot == NW - 1 ? 0 : slot + 1;
             const char* Hs = hbuf + (cc & 1) * HBUF;
             // the three taps of kernel row kh: the fragment reads of tap ti+1 are issued ahead of the
             // MFMAs of tap ti (two register sets; the order is pinned with sched_group_barrier, the
@@ -297,8 +322,8 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                     uint16_t* yp = reinterpret_cast<uint16_t*>(a.y) + obase + cb;
                     if (cb + 3 < a.Nout) {
                         uint2 o;
-                        o.x = uint32_t(f2h(v[0])) | (uint32_t(f2h(v[1])) << 16);
-                        o.y = uint32_t(f2h(v[2])) | (uint32_t(f2h(v[3])) << 16);
+                        o.x = pk2h(v[0], v[1]);
+                        o.y = pk2h(v[2], v[3]);
                         *reinterpret_cast<uint2*>(yp) = o;
                     } else {
 #pragma unroll

@@ -39,7 +39,7 @@ __device__ __forceinline__ void unpack8h(uint4 v, float* f) {
 __device__ __forceinline__ uint4 pack8h(const float* f) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f2h(f[2 * i])) | (uint32_t(f2h(f[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = pk2h(f[2 * i], f[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -83,8 +83,8 @@ __global__ void __launch_bounds__(256) maxpool5_f32_fwd_kernel(const float* __re
     *reinterpret_cast<float4*>(y + o) = make_float4(mx[0], mx[1], mx[2], mx[3]);
     *reinterpret_cast<uint32_t*>(code + o) = cd[0] | (cd[1] << 8) | (cd[2] << 16) | (cd[3] << 24);
     uint2 hv;
-    hv.x = uint32_t(f2h(mx[0])) | (uint32_t(f2h(mx[1])) << 16);
-    hv.y = uint32_t(f2h(mx[2])) | (uint32_t(f2h(mx[3])) << 16);
+    hv.x = pk2h(mx[0], mx[1]);
+    hv.y = pk2h(mx[2], mx[3]);
     *reinterpret_cast<uint2*>(yv + n * y_bs + int64_t(pix) * y_ld + c4 * 4) = hv;
 }
 
