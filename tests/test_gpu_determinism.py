@@ -144,3 +144,56 @@ def test_graph_replay_gradient_accumulation():
                                            msg=f"step {zero, nb} (count {count}) parameter {i}")
     finally:
         os.environ.pop("YM_GRAPH", None)
+
+
+def test_eval_graph_replay_matches_eager():
+    """The eval forward of a model plan replays as a HIP graph (YM_EVAL_GRAPH, on by default): eager on the
+    first call, capture on the second, replay after.  Every replay equals the eager forward bit for bit; an
+    in-place weight / running-statistics update is seen by the replay (the graph re-reads the fp32 masters and
+    the running statistics); a REPLACED parameter or buffer drops the graph (eager run, then a new capture)."""
+    import yaml
+    from pathlib import Path
+    from models import build_yolo11
+    root = Path(__file__).resolve().parents[1] / "yolo-scratch_amd"
+    cfg = yaml.safe_load((root / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = "n"
+    torch.manual_seed(5)
+    m = build_yolo11(cfg, ch=1, nc=5).cuda().eval()
+    g = torch.Generator().manual_seed(6)
+    imgs = [torch.rand(1, 1, 320, 320, generator=g).cuda() for _ in range(4)]
+
+    def run(img):
+        with torch.no_grad():
+            y, _ = m(img)
+        torch.cuda.synchronize()
+        return y.clone()
+
+    def eager(img):
+        os.environ["YM_EVAL_GRAPH"] = "0"
+        try:
+            return run(img)
+        finally:
+            os.environ.pop("YM_EVAL_GRAPH", None)
+
+    ref = [eager(i) for i in imgs]
+    out = [run(i) for i in imgs]                  # eager, capture, replay, replay
+    plan = next(iter(m.__dict__["_ym_plans"].values()))[0]
+    assert "fwd" in plan.__dict__.get("_graphs", {}), "the eval forward was not captured"
+    for a, b in zip(ref, out):
+        assert torch.equal(a, b)
+    # in-place updates: same pointers, the replay reads the new values
+    with torch.no_grad():
+        m.model[2].cv1.conv.weight.mul_(1.5)
+        m.model[3].bn.running_mean.add_(0.1)
+    r1 = eager(imgs[0])
+    assert not torch.equal(r1, ref[0])
+    assert torch.equal(run(imgs[0]), r1)
+    g0 = plan.__dict__["_graphs"]["fwd"][0]
+    # a replaced buffer: the graph is dropped and captured again over the new pointers
+    bn = m.model[4].cv2.bn
+    bn.running_var = bn.running_var.detach().clone() * 3.0
+    r2 = eager(imgs[1])
+    assert torch.equal(run(imgs[1]), r2)          # eager (new pointers)
+    assert torch.equal(run(imgs[1]), r2)          # capture
+    assert torch.equal(run(imgs[1]), r2)          # replay
+    assert plan.__dict__["_graphs"]["fwd"][0] is not g0

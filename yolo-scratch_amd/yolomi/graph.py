@@ -870,6 +870,11 @@ class Plan:
     def _nstreams(self):
         if self.dev.type != "cuda":
             return 1
+        if not self.training and self._graph_ok() and "YM_STREAMS" not in os.environ:
+            # an eval forward replayed as a HIP graph: ONE stream (bs1 s@640 1.50 ms per batch vs 1.83 with the three
+            # streams captured, same box, profiles/r05/eval_graph_streams.txt: the replayed cross-stream edges cost
+            # more than the overlap they allow at these sizes)
+            return 1
         k = max(1, int(os.environ.get("YM_STREAMS", "3")))
         return k
 
@@ -995,13 +1000,32 @@ class Plan:
     # launches point at fixed buffers: the input image and the head gradient are copied into the
     # plan's own static tensors when the caller's differ.  Not used while the bench probe times a
     # kernel with events, or for block plans.  Data parallelism in graph mode all-reduces the flat
-    # gradient once after the backward (yolomi/dist.py).  Opt-in (YM_GRAPH=1): the step is GPU-bound
-    # (host enqueue ~8 ms of a ~20 ms step), so replay has no host time to win back.
+    # gradient once after the backward (yolomi/dist.py).  Training: opt-in (YM_GRAPH=1): the step is
+    # GPU-bound (host enqueue ~8 ms of a ~20 ms step), so replay has no host time to win back (DESIGN.md
+    # §10).  Eval: on by default (YM_EVAL_GRAPH=0 opts out), captured on ONE stream (_nstreams): a bs-1
+    # eval forward is ~100 launches of a few us each whose Python enqueue leaves the GPU idle between
+    # them (bs1 s@640: 1.50 ms per batch replayed vs 1.83 eager on three streams, same box,
+    # profiles/r05/eval_graph_streams.txt).  A captured graph holds raw pointers, so every
+    # call compares the pointers of the model's parameters and buffers with the captured ones
+    # (_graph_key) and re-captures after an eager run when one was replaced.
     def _graph_ok(self):
         if not (self.dev.type == "cuda" and getattr(self, "is_model", False) and self.probe is None
                 and self.family_events is None):
             return False
-        return self.training and os.environ.get("YM_GRAPH", "0") == "1"
+        if self.training:
+            return os.environ.get("YM_GRAPH", "0") == "1"
+        return os.environ.get("YM_EVAL_GRAPH", "1") == "1"
+
+    def _graph_key(self):
+        """Data pointers of every parameter and buffer of the model, looked up in the modules' live
+        dictionaries (a replaced Parameter / buffer is seen)."""
+        pairs = self.__dict__.get("_gk_pairs")
+        if pairs is None:
+            pairs = self._gk_pairs = []
+            for mod in self.root.modules():
+                pairs += [(mod._parameters, n) for n in mod._parameters]
+                pairs += [(mod._buffers, n) for n in mod._buffers]
+        return tuple(t.data_ptr() if t is not None else 0 for t in (d.get(n) for d, n in pairs))
 
     @property
     def graph_active(self):
@@ -1009,17 +1033,24 @@ class Plan:
 
     def _replay(self, phase, body, static_in):
         """Eager on the first call of a phase, capture on the second, replay afterwards.
-        static_in: list of (attribute name, tensor) inputs the captured kernels read by address."""
+        static_in: list of (attribute name, tensor) inputs the captured kernels read by address.
+        A capture only follows an eager run over the same parameter / buffer pointers: the eager run
+        rebuilds the pointer tables (weight preparation, eval coefficients) and uploads them, which a
+        capture must not do.  A replaced parameter or buffer drops the graph (eager, then capture again)."""
         graphs = self.__dict__.setdefault("_graphs", {})
-        runs = self.__dict__.setdefault("_eager_runs", {})
+        eager_keys = self.__dict__.setdefault("_eager_keys", {})
         if not self._graph_ok():
             body()
             return
-        if runs.get(phase, 0) < 1:
-            runs[phase] = runs.get(phase, 0) + 1
+        key = self._graph_key()
+        ent = graphs.get(phase)
+        if ent is not None and ent[2] != key:
+            del graphs[phase]
+            ent = None
+        if ent is None and eager_keys.get(phase) != key:
+            eager_keys[phase] = key
             body()
             return
-        ent = graphs.get(phase)
         if ent is None:
             statics = {}
             for name, t in static_in:
@@ -1030,8 +1061,8 @@ class Plan:
             torch.cuda.synchronize(self.dev)
             with torch.cuda.graph(g):
                 body()
-            graphs[phase] = ent = (g, statics)
-        g, statics = ent
+            graphs[phase] = ent = (g, statics, key)
+        g, statics, _ = ent
         for name, t in static_in:
             st_t = statics[name]
             if t.data_ptr() != st_t.data_ptr():
