@@ -250,6 +250,14 @@ def main():
     from datasets import prepare_batch
     import yaml
 
+    # A/B runs of a library policy in the step: YM_LIB_SET="ym_bn_set_bwd_fold=2 ym_conv_set_pipe=1" calls those
+    # process-wide setters (include/yolomi.h) before the model is built; unset in the driver's runs
+    if os.environ.get("YM_LIB_SET"):
+        from yolomi._lib import lib as _yl0
+        for kv in os.environ["YM_LIB_SET"].split():
+            name, val = kv.split("=")
+            getattr(_yl0(), name)(int(val))
+
     ctx = ydist.init_from_env()
     rank = ctx.rank if ctx else 0
     world = ctx.world if ctx else 1

@@ -275,7 +275,7 @@ int ym_bn_bwd_reduce(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint1
 int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, int parts, int c, double count,
                        const float* gamma, const float* rstd, float* dgamma, float* dbeta, int accumulate,
                        float* coef, void* workspace, void* stream);
-/* Backward statistics AND finalize in one launch on the small maps (m <= 25600 pixels = 20x20 x 64
+/* Backward statistics AND finalize in one launch on the small maps (m <= 102400 pixels = 40x40 x 64
  * images, c % 64 == 0):
  * ym_bn_bwd_reduce followed by ym_bn_bwd_finalize over its rows, with the same outputs (dgamma / dbeta /
  * coef; part_sum / part_dot as scratch rows, ym_bn_bwd_blocks(m, c) x c floats each).  Where
@@ -285,8 +285,9 @@ int ym_bn_bwd_reduce_fold(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const 
                           const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                           float* part_sum, float* part_dot, const float* gamma, float* dgamma, float* dbeta,
                           int accumulate, float* coef, void* workspace, void* stream);
-/* Policy of the fused backward statistics + finalize for later calls: -1 default (on), 0 never, 1 on.
- * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+/* Policy of the fused backward statistics + finalize for later calls: -1 default (= 2), 0 never, 1 on maps up
+ * to 25600 pixels (20x20 x 64 images), 2 up to 102400 (40x40 x 64).  Returns the previous setting.  Process-wide,
+ * like ym_conv_set_halo. */
 int ym_bn_set_bwd_fold(int mode);
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,

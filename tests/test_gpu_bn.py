@@ -90,15 +90,27 @@ def test_bn_bwd_finalize_vs_host_fp64(G, C):
 # each 64-channel group folds its rows) against the two launches it replaces: dgamma / dbeta (overwrite, then
 # accumulate) and the apply coefficients to 1e-6, three calls in a row (tickets re-armed), SiLU on and off,
 # a channel-slice view of dy; a map past the size limit falls back to the two launches.
-@pytest.mark.parametrize("m,c,act,extra", [(25600, 128, 1, 0), (400 * 7, 512, 1, 64), (102400, 64, 0, 0),
-                                           (200000, 128, 1, 0), (25600, 256, 0, 0), (25600, 256, 1, 256),
-                                           (25600, 64, 0, 64), (25600, 512, 0, 0)])
-def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra):
-    import ctypes
+# The default (= mode 2) takes the 40x40 maps too (<= 102400 pixels, up to 256 workgroups per 64-channel group);
+# mode 1 only the 20x20 ones.
+@pytest.mark.parametrize("m,c,act,extra,mode", [(25600, 128, 1, 0, -1), (400 * 7, 512, 1, 64, -1), (102400, 64, 0, 0, -1),
+                                                (200000, 128, 1, 0, -1), (25600, 256, 0, 0, -1), (25600, 256, 1, 256, -1),
+                                                (25600, 64, 0, 64, -1), (25600, 512, 0, 0, -1), (102400, 64, 1, 0, 2), (102400, 128, 0, 0, 1),
+                                                (102400, 128, 1, 64, 2), (102400, 256, 0, 0, 2), (1600 * 37, 512, 1, 0, 2),
+                                                (200000, 64, 1, 0, 2)])
+def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra, mode):
+    from yolomi._lib import lib
+    prev = lib().ym_bn_set_bwd_fold(mode)
+    try:
+        _bwd_fold_case(m, c, act, extra, mode)
+    finally:
+        lib().ym_bn_set_bwd_fold(prev)
+
+
+def _bwd_fold_case(m, c, act, extra, mode):
     from yolomi._lib import call, lib
     dev = torch.device("cuda", 0)
     g = torch.Generator().manual_seed(c + m)
-    hw = 400 if m % 400 == 0 else m
+    hw = 400 if m % 400 == 0 else (1600 if m % 1600 == 0 else m)
     z = torch.randn(m, c, generator=g).half().to(dev)
     dyb = torch.zeros(m, c + extra, dtype=torch.bfloat16, device=dev)
     dyb[:, :c] = torch.randn(m, c, generator=g).bfloat16().to(dev)
@@ -108,7 +120,7 @@ def test_bn_bwd_reduce_fold_matches_two_launches(m, c, act, extra):
     rstd = (1 + 0.1 * torch.rand(c, generator=g)).to(dev)
     gamma = (1 + 0.1 * torch.randn(c, generator=g)).to(dev)
     Gb = lib().ym_bn_bwd_blocks(m, c)
-    assert lib().ym_bn_bwd_fold_ok(m, c) == (1 if m <= 25600 else 0)
+    assert lib().ym_bn_bwd_fold_ok(m, c) == (1 if m <= (25600 if mode == 1 else 102400) else 0)
     st = torch.cuda.current_stream().cuda_stream
     d_bs, d_ld = hw * (c + extra), c + extra
 

@@ -377,13 +377,13 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(const bf16_t* __restr
 }
 
 // BatchNorm backward statistics AND finalize in one launch for the small maps (ym_bn_bwd_reduce_fold): grid
-// (FOLD_GP pixel blocks, C / 64 channel groups), 256 threads = 8 lanes of 8 channels x 32 pixel rows.  Each
+// (G pixel blocks, C / 64 channel groups; fold_blocks), 256 threads = 8 lanes of 8 channels x 32 pixel rows.  Each
 // workgroup reduces its rows for its 64 channels, publishes one partial row write-through, takes an agent-scope
-// ticket of its channel group; the last workgroup of the group folds the group's FOLD_GP rows in fp64 in a fixed
-// order (4 row subsets, 8 rows' loads in flight) and writes what ym_bn_bwd_finalize writes (dgamma, dbeta,
+// ticket of its channel group; the last workgroup of the group folds the group's G rows in fp64 in a fixed
+// order (4 row subsets, 16 rows' loads in flight) and writes what ym_bn_bwd_finalize writes (dgamma, dbeta,
 // the apply coefficients) for those channels, then re-arms the ticket.  The partial rows of a group are few
-// (FOLD_GP = 64): the fold is 8 K loads, where one folding workgroup over the streaming kernel's 512 full-width
-// rows would be latency-bound for tens of us.
+// (G = 64 on the 20x20 maps, <= 256 on 40x40): the fold is <= 4 rounds of loads, where one folding workgroup over
+// the streaming kernel's 512 full-width rows would be latency-bound for tens of us.
 constexpr int FOLD_GP = 64;
 
 __global__ void __launch_bounds__(256) bn_bwd_reduce_fold_kernel(
@@ -460,15 +460,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_fold_kernel(
     };
     double fs = 0.0, fq = 0.0;
     int row = k;
-    for (; row + 28 < rows; row += 32) {
-        float vs[8], vq[8];
+    for (; row + 60 < rows; row += 64) {
+        float vs[16], vq[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 16; ++u) {
             vs[u] = ld(ps, row + 4 * u);
             vq[u] = ld(pg, row + 4 * u);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < 16; ++u) {
             fs += double(vs[u]);
             fq += double(vq[u]);
         }
@@ -596,22 +596,31 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
     return YM_OK;
 }
 
-// fused backward statistics + finalize policy (ym_bn_set_bwd_fold): -1 default (on), 0 off, 1 on
+// fused backward statistics + finalize policy (ym_bn_set_bwd_fold): -1 default (= 2), 0 off, 1 / 2 on (map size caps)
 static int g_bwd_fold = -1;
-// the maps it takes: whole 64-channel groups and at most 25600 pixels = 20x20 x 64 images (FOLD_GP workgroups per
-// group stream the tensor; on the larger maps, 40x40 included, the streaming kernel's 512 full-width workgroups win:
-// profiles/r04/bn_bwd_fold_ab.txt)
-static constexpr int64_t FOLD_MAX_M = 25600;
+// the maps it takes: whole 64-channel groups and at most 25600 pixels = 20x20 x 64 images on 64 workgroups per group
+// (on larger maps 64 workgroups per group streamed the tensor slower than the streaming kernel's 512 full-width ones:
+// 40x40 -0.5 %, profiles/r04/bn_bwd_fold_ab.txt); by default (round 5) it also takes <= 102400 pixels (40x40 x 64
+// images) with 512 / groups workgroups per group (64..256): +0.0..+0.7 % img/s in three same-box pairs
+// (profiles/r05/bn_bwd_fold40_ab.txt); mode 1 keeps the 20x20-only rule
+static constexpr int64_t FOLD_MAX_M = 25600, FOLD_MAX_M2 = 102400;
+
+static int fold_blocks(int64_t m, int c) {
+    if (m <= FOLD_MAX_M) return FOLD_GP;
+    return std::min(256, std::max(FOLD_GP, 512 / (c / 64)));
+}
 
 extern "C" int ym_bn_bwd_fold_ok(int64_t m, int c) {
     if (g_bwd_fold == 0) return 0;
-    return m > 0 && m <= FOLD_MAX_M && c % 64 == 0 && c <= 2048 && ym_bn_bwd_blocks(m, c) >= FOLD_GP ? 1 : 0;
+    const int64_t cap = g_bwd_fold == 1 ? FOLD_MAX_M : FOLD_MAX_M2;
+    return m > 0 && m <= cap && c % 64 == 0 && c <= 2048 && ym_bn_bwd_blocks(m, c) >= fold_blocks(m, c) ? 1 : 0;
 }
 
 extern "C" int ym_bn_set_bwd_fold(int mode) {
-    // fused backward statistics + finalize: -1 default (on), 0 off, 1 on; returns the previous setting
+    // fused backward statistics + finalize: -1 default (= 2), 0 off, 1 on up to 25600 pixels, 2 up to 102400;
+    // returns the previous setting
     const int prev = g_bwd_fold;
-    g_bwd_fold = mode < -1 || mode > 1 ? -1 : mode;
+    g_bwd_fold = mode < -1 || mode > 2 ? -1 : mode;
     return prev;
 }
 
@@ -631,7 +640,7 @@ extern "C" int ym_bn_bwd_reduce_fold(const uint16_t* dy, int64_t d_bs, int64_t d
         return ym_bn_bwd_finalize(part_sum, part_dot, ym_bn_bwd_blocks(m, c), c, double(m), gamma, rstd, dgamma,
                                   dbeta, accumulate, coef, workspace, stream);
     }
-    hipLaunchKernelGGL(bn_bwd_reduce_fold_kernel, dim3(FOLD_GP, c / 64), dim3(256), 0, as_stream(stream), dy, d_ld, z,
+    hipLaunchKernelGGL(bn_bwd_reduce_fold_kernel, dim3(fold_blocks(m, c), c / 64), dim3(256), 0, as_stream(stream), dy, d_ld, z,
                        m, c, scale, shift, mean, rstd, act, part_sum, part_dot, gamma, dgamma, dbeta, accumulate, coef,
                        static_cast<unsigned*>(workspace), double(m));
     YM_LAUNCH_CHECK("ym_bn_bwd_reduce_fold");
