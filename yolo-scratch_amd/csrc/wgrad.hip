@@ -128,6 +128,17 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
     const int ntw = (a.OW + TW - 1) / TW, nth = (a.OH + TH - 1) / TH;
     const int64_t t_begin = int64_t(split) * a.chunk;
     const int64_t t_end = std::min<int64_t>(a.units, t_begin + a.chunk);
+    // the unit the next load() stages, stepped from one call to the next (every call site loads units in order, one
+    // per call): round 5, in place of four runtime divisions per load (precomputing the chunks' offsets as well cost
+    // 17 VGPRs, one workgroup per CU on the 8-wave tiles)
+    int64_t l_t = t_begin;
+    int l_tw, l_th, l_n;
+    {
+        const int u = int(t_begin < t_end ? t_begin : 0), r = u / ntw;
+        l_tw = u - r * ntw;
+        l_th = r % nth;
+        l_n = r / nth;
+    }
 
     // fragment-read geometry: lane's k rows (pixels of the unit) for the two 32-pixel halves; pixel
     // slots past the unit read halo row 0 (always staged, finite) against their zero dz rows
@@ -150,10 +161,16 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
 
     uint4 da[DI], xa[XI], db[DI], xb[XI];
     auto load = [&](int64_t t, uint4 (&rdz)[DI], uint4 (&rx)[XI]) {
-        const bool live = t < t_end;              // past the split: zeros, no branch around the loads
-        const int u = int(live ? t : t_begin);     // units < 2^31 (M < 2^31, checked on the host)
-        const int tw = u % ntw, r = u / ntw;
-        const int th = r % nth, n = r / nth;
+        (void)t;                                   // == l_t
+        const bool live = l_t < t_end;             // past the split: zeros, no branch around the loads
+        const int tw = l_tw, th = l_th, n = l_n;
+        if (live) {
+            ++l_t;
+            if (++l_tw == ntw) {
+                l_tw = 0;
+                if (++l_th == nth) { l_th = 0; ++l_n; }
+            }
+        }
         const int oh0 = th * TH, ow0 = tw * TW;
         const __amdgpu_buffer_rsrc_t rd = make_rsrc(a.dz + int64_t(n) * a.dz_bs, a.dz_bs * 2);
         const __amdgpu_buffer_rsrc_t rxs = make_rsrc(a.x + int64_t(n) * a.x_bs, a.x_bs * 2);
