@@ -22,11 +22,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, in
 __device__ __forceinline__ uint4 buf_load16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
-// the same with a wave-uniform part of the offset in the instruction's scalar soffset (an OOB voffset stays out of
-// range: soffset is far below 2^31)
-__device__ __forceinline__ uint4 buf_load16s(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff) {
-    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, 0));
-}
 
 // 8 fp16 -> 8 bf16 (v_cvt_f32_f16 + v_cvt_pk_bf16_f32)
 __device__ __forceinline__ uint4 h8_to_bf8(uint4 h) {
