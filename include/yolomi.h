@@ -254,6 +254,16 @@ int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                    float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* workspace,
                    void* stream);
+/* Eval-mode Conv block in ONE launch (inference): conv -> BatchNorm with the running-statistics scale / shift
+ * (ym_bn_eval_coeff[_batch]) -> SiLU if act -> + residual, written into the fp16 activation view y — what
+ * ym_conv_fwd (fp16 z) + ym_bn_apply compute, without the z round trip and the apply launch (Conv.forward of
+ * yolo11_modules.py:21-33 in eval mode).  d describes the conv with d->y_bs / d->y_ld the OUTPUT VIEW's strides
+ * (out_f32 = 2, accumulate 0); the residual (or NULL) is a view with the same strides.  ym_conv_fwd_eval_ok(d) is 1
+ * where the kernel this conv selects has the eval epilogue (the halo-staged 3x3 kernel, the 2-stage implicit GEMM with
+ * >= 64 output channels); elsewhere run ym_conv_fwd + ym_bn_apply.  Bias-free convs only. */
+int ym_conv_fwd_eval_ok(const ym_conv_desc* d);
+int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
+                     const float* shift, int act, const uint16_t* res, uint16_t* y, void* stream);
 /* Eval-mode coefficients of many BatchNorm layers in ONE launch (the eval forward's per-layer
  * ym_bn_eval_coeff calls were 77 launches per YOLOv11-s forward); table in device memory. */
 typedef struct ym_bn_eval_entry {

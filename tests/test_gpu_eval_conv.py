@@ -1,0 +1,129 @@
+"""ym_conv_fwd_eval — the eval-mode Conv block in one launch (conv -> BatchNorm with the running-statistics scale /
+shift -> SiLU -> + residual, yolo11_modules.py:21-47 in eval mode) — vs a PyTorch fp32 reference of the same op, and
+the eval forward of a whole model with it vs without it.
+
+Kernel cases: the halo-staged 3x3 kernel's C4 tile (20x20 / 10x10 maps, channel counts off the 32-channel chunk) and
+the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2), with and without SiLU and a residual; the output is a
+channel slice of a wider buffer (a concat slice: the other channels must stay untouched) and the residual a slice of
+another buffer with the same strides.  The operands are rounded to the kernel's dtypes first (fp16 activations,
+weights, residual), so the reference differs by fp32 accumulation order and the fp16 output rounding: rel 2e-3 of
+max |y| (+1e-3).
+"""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # n, h, w, cin, cout, k, stride
+    (1, 20, 20, 128, 128, 3, 1),
+    (2, 20, 20, 72, 64, 3, 1),
+    (1, 10, 10, 256, 128, 3, 1),
+    (1, 20, 20, 512, 256, 1, 1),
+    (2, 40, 40, 128, 128, 3, 2),
+    (2, 13, 11, 64, 96, 3, 2),
+    (1, 80, 80, 64, 64, 1, 1),
+]
+
+
+def _desc(n, h, w, cin, cout, k, s, ld):
+    from yolomi._lib import ConvDesc
+    p = k // 2
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    d = ConvDesc()
+    d.n, d.h, d.w, d.cin, d.oh, d.ow, d.cout, d.k, d.stride, d.pad = n, h, w, cin, oh, ow, cout, k, s, p
+    d.x_bs, d.x_ld, d.y_bs, d.y_ld = h * w * cin, cin, oh * ow * ld, ld
+    d.out_f32, d.accumulate = 2, 0
+    return d, oh, ow
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"n{c[0]}h{c[1]}w{c[2]}c{c[3]}o{c[4]}k{c[5]}s{c[6]}" for c in CASES])
+@pytest.mark.parametrize("act,with_res", [(1, False), (0, True), (1, True)])
+def test_conv_fwd_eval_vs_torch(case, act, with_res):
+    from yolomi._lib import call, lib, stream_ptr
+    n, h, w, cin, cout, k, s = case
+    ld = cout + 24                                   # output / residual: channel slices of wider buffers
+    d, oh, ow = _desc(n, h, w, cin, cout, k, s, ld)
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1, case
+    g = torch.Generator().manual_seed(hash((case, act, with_res)) & 0xFFFF)
+    x = torch.randn(n, h, w, cin, generator=g).half()
+    wt = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).half()
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.2
+    res = torch.randn(n, oh, ow, cout, generator=g).half() if with_res else None
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), wt.float(), stride=s, padding=k // 2).permute(0, 2, 3, 1)
+    ref = ref * scale + shift
+    if act:
+        ref = F.silu(ref)
+    if res is not None:
+        ref = ref + res.float()
+    dev = torch.device("cuda")
+    xd, wd = x.to(dev), wt.permute(0, 2, 3, 1).contiguous().to(dev)
+    scd, shd = scale.to(dev), shift.to(dev)
+    rbuf = torch.zeros(n, oh, ow, ld, dtype=torch.float16, device=dev)
+    if res is not None:
+        rbuf[..., 8:8 + cout] = res.to(dev)
+    buf = torch.full((n, oh, ow, ld), 7.0, dtype=torch.float16, device=dev)
+    torch.cuda.synchronize()
+    call("ym_conv_fwd_eval", ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), scd.data_ptr(), shd.data_ptr(), act,
+         rbuf[..., 8:].data_ptr() if res is not None else None, buf[..., 8:].data_ptr(), stream_ptr(dev))
+    torch.cuda.synchronize()
+    out = buf.float().cpu()
+    assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"
+    y = out[..., 8:8 + cout]
+    err, mag = float((y - ref).abs().max()), float(ref.abs().max())
+    assert err <= 2e-3 * mag + 1e-3, f"max |diff| {err:.3e} vs max |ref| {mag:.3e}"
+
+
+def test_conv_fwd_eval_ok_scope():
+    """Not eval-epilogue cases: a map the direct kernel takes, a GEMM with < 64 output channels, an accumulating or
+    non-fp16 output."""
+    from yolomi._lib import lib
+    d, _, _ = _desc(8, 160, 160, 64, 64, 3, 1, 64)              # >= 1 M output pixels: direct kernel
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+    d, _, _ = _desc(1, 20, 20, 64, 32, 1, 1, 32)                # 2-stage GEMM, 32 output channels
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+    d, _, _ = _desc(1, 20, 20, 256, 128, 1, 1, 128)
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1
+    d.accumulate = 1
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+    d.accumulate, d.out_f32 = 0, 1
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+
+
+@pytest.mark.parametrize("scale_name,imgsz,bs", [("s", 640, 1), ("n", 320, 2)])
+def test_eval_forward_one_launch_blocks_vs_unfused(scale_name, imgsz, bs, monkeypatch):
+    """The eval forward with the one-launch Conv blocks (default) against the same model with them off
+    (YM_EVAL_FUSE=0: conv with an fp16 z, then ym_bn_apply): most blocks take the one-launch path at these sizes, and
+    the outputs agree to fp16 rounding (the one-launch path normalises the fp32 accumulator instead of the fp16 z)."""
+    import yaml
+    from pathlib import Path
+    from models import build_yolo11
+    root = Path(__file__).resolve().parents[1] / "yolo-scratch_amd"
+    cfg = yaml.safe_load((root / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = scale_name
+    torch.manual_seed(7)
+    m = build_yolo11(cfg, ch=1, nc=5).cuda().eval()
+    img = torch.rand(bs, 1, imgsz, imgsz, generator=torch.Generator().manual_seed(8)).cuda()
+
+    def run():
+        with torch.no_grad():
+            y, maps = m(img)
+        torch.cuda.synchronize()
+        return y.clone(), [t.clone() for t in maps]
+    monkeypatch.setenv("YM_EVAL_GRAPH", "0")
+    monkeypatch.setenv("YM_EVAL_FUSE", "0")
+    y0, m0 = run()
+    monkeypatch.setenv("YM_EVAL_FUSE", "1")
+    y1, m1 = run()
+    from yolomi.graph import ConvBN
+    plan = next(iter(m.__dict__["_ym_plans"].values()))[0]
+    convs = [op for op in plan.ops if type(op) is ConvBN]
+    fused = [op for op in convs if op.__dict__.get("_evf", (0, None))[1] is not None]
+    assert len(fused) >= len(convs) // 2, (len(fused), len(convs))
+    for a, b in zip(m0, m1):
+        err, mag = float((a - b).abs().max()), float(a.abs().max())
+        assert err <= 2e-2 * mag + 1e-2, (err, mag)

@@ -42,6 +42,15 @@ static inline int64_t select_n(const ym_conv_desc* d) { return g_select_n > 0 ? 
 // the weight-gradient kernel instance ym_conv_wgrad runs for d (wgrad.hip; ym_conv_kernel dir 2)
 int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len);
 
+// eval-mode Conv block epilogue arguments (ym_conv_fwd_eval; conv_epi.h EvalEpi is built from them in the kernel):
+// BatchNorm scale / shift from the running statistics, SiLU when act, and an fp16 residual view with the output's
+// strides (res null: none; res_bytes: its extent from res for the buffer resource)
+struct EvalArgs {
+    const float* sc; const float* sh;
+    int act;
+    const uint16_t* res; int64_t res_bytes;
+};
+
 typedef uint16_t bf16_t;   // raw bf16 bits in memory
 
 __device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }

@@ -96,9 +96,11 @@ __device__ __forceinline__ void raw_barrier() {
 
 // WM x WN waves: wave (wr, wc) owns BN/WM channels x BM/WN pixels of the tile; KB-deep K stages
 // (rows of KB*2 bytes), an NS-stage LDS ring with NS-1 stages in flight
-template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
+// EV: the eval-mode Conv block instance (ym_conv_fwd_eval: BatchNorm / SiLU / residual in the register epilogue; e is
+// not read by the other instances)
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE, bool EV = false>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 4 && NS * (BM + BN) * KB * 2 <= 72 * 1024) ? 2 : 1)
-conv_gemm_kernel(GemmArgs a) {
+conv_gemm_kernel(GemmArgs a, EvalArgs e) {
     constexpr int BK = KB;
     constexpr int RB = KB * 2;           // LDS row bytes
     constexpr int CPR = KB / 8;          // 16-B chunks per row
@@ -322,8 +324,15 @@ conv_gemm_kernel(GemmArgs a) {
                     return uint32_t((int64_t(n) * a.y_bs + opix * a.y_ld + wch0) * 2);
                 };
                 auto pix_ok = [&](int q) -> bool { return m0 + wc * (BM / WN) + q < Mc; };
-                epilogue_regs<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr, lane, wch0, a.Nout, yres,
-                                      MODE == MODE_FWD, MODE == MODE_DGRAD && a.accumulate != 0, pix_off, pix_ok);
+                if constexpr (EV) {
+                    const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
+                    epilogue_regs<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
+                                          &ee);
+                } else {
+                    epilogue_regs<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr, lane, wch0, a.Nout,
+                                          yres, MODE == MODE_FWD, MODE == MODE_DGRAD && a.accumulate != 0, pix_off,
+                                          pix_ok);
+                }
                 continue;
             }
         }
@@ -795,8 +804,8 @@ static bool offsets_fit(int64_t bs, int64_t class_pixels) {
     return bs * 2 * images < (int64_t(1) << 31);
 }
 
-template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE>
-int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
+template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE, bool EV = false>
+int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st, const EvalArgs& e = EvalArgs{}) {
     GemmArgs a = a0;
     const int os = a.ostep;
     const int64_t Mc = int64_t(a.N) * ((a.OH + os - 1) / os) * ((a.OW + os - 1) / os);   // largest class
@@ -806,7 +815,7 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st) {
     // channel tiles of one m-tile sequence interleaved into grid x (dispatched together)
     a.ntl = ntiles > 1 ? ntiles : 0;
     const dim3 grid(a.ntl ? gx * ntiles : gx, a.ntl ? 1 : ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
-    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, EV>), grid, block, 0, st, a, e);
     return gx;
 }
 
@@ -830,19 +839,25 @@ static Tile pick_tile(int64_t Mc, int classes, int nout) {
     return {128, bn};
 }
 
-template <int KB, int NS, int MODE>
-static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
-    if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
-    if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
-    // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
-    return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
+template <int KB, int NS, int MODE, bool EV = false>
+static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st, const EvalArgs& e) {
+    if constexpr (EV) {
+        // the eval epilogue is the register epilogue's (>= 32 channels per wave); 128x64 only (with it the 128x128
+        // instance spills)
+        return launch_gemm<128, 64, 2, 2, KB, NS, MODE, EV>(a, max_blocks, st, e);
+    } else {
+        if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+        if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+        // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
+        return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
+    }
 }
 
 // K-stage depth x ring depth, measured per layer (tools/layer_bench.py): 64-channel tiles prefer 32-deep stages
-template <int MODE>
-static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
-    return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE>(a, t, max_blocks, st)
-                                     : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
+template <int MODE, bool EV = false>
+static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st, const EvalArgs& e = EvalArgs{}) {
+    return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE, EV>(a, t, max_blocks, st, e)
+                                     : launch_tile_k<64, 2, MODE, EV>(a, t, max_blocks, st, e);
 }
 
 // nsel: the batch the tile choice is made for (select_n: the real batch unless a parity test pins the
@@ -1062,6 +1077,60 @@ extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const ui
     return ym_bn_finalize(stat_sum, stat_sq, ym_conv_fwd_stat_rows(d), d->cout, bn->count, bn->gamma, bn->beta,
                           bn->running_mean, bn->running_var, bn->num_batches_tracked, bn->momentum, bn->eps,
                           bn->scale, bn->shift, bn->mean, bn->rstd, bn->workspace, stream);
+}
+
+// ------------------------------------------------------------------ eval-mode Conv block in one launch
+// (inference: conv -> BatchNorm with the running statistics -> SiLU -> + residual, yolo11_modules.py:21-33 in eval mode):
+// where the forward runs the halo-staged kernel or the 2-stage implicit GEMM, the BatchNorm / SiLU / residual are
+// applied by their register epilogue (conv_epi.h EvalEpi) and the launch writes the activation view; the fp16 z and
+// ym_bn_apply's launch go (a bs-1 s@640 eval forward is ~75 conv blocks, each ~4 us of apply launch).
+// The eval GEMM tile is 128x64 (the register epilogue needs >= 32 channels per wave; the 128x128 instance spills with
+// it); the halo kernel's eval instance is its 4-wave C4 tile (C8 spills).
+static Tile eval_tile(int64_t, int) { return Tile{128, 64}; }
+
+extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
+    if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return 0;
+    if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return 0;
+    if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return 0;
+    if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok || pipe_plan(d, 0).ok) return 0;   // no eval epilogue there
+    const HaloPlan hp = halo_plan(d, 0);
+    if (hp.ok) return hp.cfg == 1 ? 1 : 0;
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    return d->cout >= 64 && M < (int64_t(1) << 31) && offsets_fit(d->x_bs, int64_t(d->oh) * d->ow) ? 1 : 0;
+}
+
+extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
+                                const float* shift, int act, const uint16_t* res, uint16_t* y, void* stream) {
+    YM_CHECK_ARG(d && x && w && scale && shift && y, "ym_conv_fwd_eval: null argument");
+    YM_CHECK_ARG(ym_conv_fwd_eval_ok(d), "ym_conv_fwd_eval: not an eval-epilogue case (ym_conv_fwd_eval_ok = 0)");
+    YM_CHECK_ARG(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(res) % 8 == 0 &&
+                 reinterpret_cast<uintptr_t>(scale) % 16 == 0 && reinterpret_cast<uintptr_t>(shift) % 16 == 0,
+                 "ym_conv_fwd_eval: misaligned output / residual / coefficient pointer");
+    if (int64_t(d->n) * d->oh * d->ow == 0) return YM_OK;
+    const EvalArgs ev{scale, shift, act, res, int64_t(d->n) * d->y_bs * 2};
+    hipStream_t st = as_stream(stream);
+    const HaloPlan hp = halo_plan(d, 0);
+    if (hp.ok) {
+        YM_CHECK_ARG(halo_launch(hp, d, 0, x, w, y, nullptr, nullptr, nullptr, st, nullptr, &ev) == 0,
+                     "ym_conv_fwd_eval: halo launch refused");
+        YM_LAUNCH_CHECK("ym_conv_fwd_eval (halo)");
+        return YM_OK;
+    }
+    GemmArgs a{};
+    a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
+    a.w = w;
+    a.y = y; a.y_bs = d->y_bs; a.y_ld = d->y_ld;
+    a.GH = d->h; a.GW = d->w; a.Kin = d->cin;
+    a.OH = d->oh; a.OW = d->ow; a.Nout = d->cout;
+    a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad;
+    a.M = int64_t(d->n) * d->oh * d->ow;
+    a.out_f32 = 2;
+    a.N = d->n;
+    a.ostep = 1;
+    a.ep_lds = 1;
+    launch_tile<MODE_FWD, true>(a, eval_tile(a.M, d->cout), FWD_STAT_BLOCKS, st, ev);
+    YM_LAUNCH_CHECK("ym_conv_fwd_eval");
+    return YM_OK;
 }
 
 extern "C" int ym_conv_set_fold(int mode) {

@@ -80,6 +80,17 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
     }
 }
 
+// Eval-mode Conv block epilogue (ym_conv_fwd_eval): the running-statistics BatchNorm (scale / shift per output
+// channel), SiLU when act, then + the fp16 residual read at the output's own offset from the residual view's base (the
+// residual view has the output's image / pixel strides) — ym_bn_apply's arithmetic (fp32, one fp16 rounding), applied to
+// the accumulators before the pack instead of to a stored fp16 z.
+struct EvalEpi {
+    const float* sc; const float* sh;
+    int act;
+    __amdgpu_buffer_rsrc_t rres;
+    int res;
+};
+
 // Register-only form (round 3; the pipelined kernel's data gradient): each pair of 16-pixel subtiles (ja, jb) is exchanged
 // between lane rows with v_permlane16_swap (rows 1 / 3 of ja's packed values <-> rows 0 / 2 of jb's), after which
 // lane (fc, fr) holds 8 consecutive channels (i*16 + (fc >> 1)*8 ..) of ONE pixel (subtile fc odd ? jb : ja, row
@@ -88,13 +99,47 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
 // pix_off(q) as above (byte offset of wave-local pixel q's channel wch0, OOB outside); nout % 8 == 0.
 // pix_ok(q): pixel q of the wave lies inside the output (the statistics' mask; a compare, where pix_off also
 // decomposes the pixel).
+// ea: the eval-mode BatchNorm / SiLU / residual (a null constant for every other caller: no code, no registers).
 template <int TM, int TN, class PixOff, class PixOk>
 __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
                                               bool stats, int lane, int wch0, int nout,
                                               __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
-                                              PixOff pix_off, PixOk pix_ok) {
+                                              PixOff pix_off, PixOk pix_ok, const EvalEpi* ea = nullptr) {
     static_assert(TN % 2 == 0, "subtile pairs");
     const int fc = lane >> 4, fr = lane & 15;
+    if (ea) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int cb = wch0 + i * 16 + fc * 4;
+            if (cb >= nout) continue;                                  // nout % 8 == 0: all four or none
+            const float4 s4 = *reinterpret_cast<const float4*>(ea->sc + cb);
+            const float4 h4 = *reinterpret_cast<const float4*>(ea->sh + cb);
+            const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, hv[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float t = fmaf(acc[i][j][r], sv[r], hv[r]);
+                    acc[i][j][r] = ea->act ? silu_f(t) : t;
+                }
+        }
+        if (ea->res) {                                                 // + residual in fp32, one rounding (as ym_bn_apply)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const uint32_t b = pix_off(j * 16 + fr);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    const int co = i * 16 + fc * 4;
+                    const uint32_t off = b != OOB && wch0 + co < nout ? b + uint32_t(co) * 2u : OOB;
+                    const uint2 rv = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ea->rres, off, 0, 0));
+                    acc[i][j][0] += h2f(uint16_t(rv.x & 0xffff));
+                    acc[i][j][1] += h2f(uint16_t(rv.x >> 16));
+                    acc[i][j][2] += h2f(uint16_t(rv.y & 0xffff));
+                    acc[i][j][3] += h2f(uint16_t(rv.y >> 16));
+                }
+            }
+        }
+    }
     if (stats) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -138,6 +183,7 @@ __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum
                                   bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
                 v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
             }
+
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
                                                    yres, off, 0, 0);
         }

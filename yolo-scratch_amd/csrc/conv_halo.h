@@ -21,7 +21,9 @@ extern int g_halo_force;
 // dgrad = 0: forward conv described by d; 1: its data gradient
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad);
 // fold: the BatchNorm finalize as the launch's tail (ym_conv_fwd_bn; forward with statistics only) or null
+// ev: the eval-mode Conv block epilogue (ym_conv_fwd_eval: forward, fp16 output view, no statistics) or null
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold = nullptr);
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold = nullptr,
+                const EvalArgs* ev = nullptr);
 
 }  // namespace ym

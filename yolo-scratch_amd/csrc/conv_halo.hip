@@ -88,9 +88,11 @@ __device__ __forceinline__ void raw_barrier() {
 }
 
 // WPX x WCO waves; wave tile TPW x 16 pixels by TCW x 16 channels; HI halo DMA instructions per
-// wave (halo capacity HI * waves * 16 rows); NW-deep weight ring
-template <int WPX, int WCO, int TPW, int TCW, int HI, int NW, int MODE>
-__global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_per_eu(1, 2))) conv_halo_kernel(HaloArgs a) {
+// wave (halo capacity HI * waves * 16 rows); NW-deep weight ring.  EV: the eval-mode Conv block instance
+// (ym_conv_fwd_eval: BatchNorm / SiLU / residual in the register epilogue; e is not read by the other instances)
+template <int WPX, int WCO, int TPW, int TCW, int HI, int NW, int MODE, bool EV = false>
+__global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_per_eu(1, 2)))
+conv_halo_kernel(HaloArgs a, EvalArgs e) {
     constexpr int NWV = WPX * WCO, NT = NWV * 64;
     constexpr int BN = WCO * TCW * 16;            // output channels per tile
     static_assert(WPX * TPW * 16 <= 512, "pixel capacity per tile");
@@ -292,8 +294,14 @@ __global__ void __launch_bounds__(WPX * WCO * 64) __attribute__((amdgpu_waves_pe
                 return uint32_t((int64_t(n) * a.y_bs + int64_t(oh * a.OW + ow) * a.y_ld + wch0) * 2);
             };
             auto pix_ok = [&](int q) -> bool { return (vmask >> (q >> 4)) & 1u; };
-            epilogue_regs<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_mode == 2,
-                                    a.accumulate != 0 && a.out_mode == 0, pix_off, pix_ok);
+            if constexpr (EV) {
+                const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
+                epilogue_regs<TCW, TPW>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
+                                        &ee);
+            } else {
+                epilogue_regs<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_mode == 2,
+                                        a.accumulate != 0 && a.out_mode == 0, pix_off, pix_ok);
+            }
             continue;
         }
         // epilogue: lane holds channels cb..cb+3 of pixel p
@@ -459,7 +467,8 @@ HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
 }
 
 int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
-                const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold) {
+                const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold,
+                const EvalArgs* ev) {
     HaloArgs a{};
     a.x = x;
     a.w = w;
@@ -485,14 +494,18 @@ int halo_launch(const HaloPlan& p, const ym_conv_desc* d, int dgrad, const uint1
     a.RT = p.RT; a.CT = p.CT; a.ntiles = p.ntiles;
     if (!dgrad && st_sum) a.fold = bn_fold_args(fold);
     const dim3 grid(p.gx, p.nco);
+    const EvalArgs e = ev ? *ev : EvalArgs{};
+    // the eval epilogue: the fp16 register epilogue of the C4 tile (C8's eval instance spills)
+    if (ev && (dgrad || !a.ep_lds || st_sum || p.cfg == 0)) return -1;
     if (p.cfg == 0) {
-        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_DGRAD>), grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD>), grid, dim3(512), 0, st, a);
+        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_DGRAD>), grid, dim3(512), 0, st, a, e);
+        else hipLaunchKernelGGL((conv_halo_kernel<4, 2, 4, 4, 3, 3, H_FWD>), grid, dim3(512), 0, st, a, e);
     } else {
         // 4-deep weight ring (round 4, same-process A/B: -1..-5 % against 3 slots; 6 slots cost the second
         // workgroup per CU: +47..+61 %, profiles/r04/halo_ring_depth_ab.txt)
-        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_DGRAD>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_FWD>), grid, dim3(256), 0, st, a);
+        if (dgrad) hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_DGRAD>), grid, dim3(256), 0, st, a, e);
+        else if (ev) hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_FWD, true>), grid, dim3(256), 0, st, a, e);
+        else hipLaunchKernelGGL((conv_halo_kernel<2, 2, 4, 2, 4, 4, H_FWD>), grid, dim3(256), 0, st, a, e);
     }
     return 0;
 }
