@@ -257,13 +257,17 @@ int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c
 /* Eval-mode Conv block in ONE launch (inference): conv -> BatchNorm with the running-statistics scale / shift
  * (ym_bn_eval_coeff[_batch]) -> SiLU if act -> + residual, written into the fp16 activation view y — what
  * ym_conv_fwd (fp16 z) + ym_bn_apply compute, without the z round trip and the apply launch (Conv.forward of
- * yolo11_modules.py:21-33 in eval mode).  d describes the conv with d->y_bs / d->y_ld the OUTPUT VIEW's strides
- * (out_f32 = 2, accumulate 0); the residual (or NULL) is a view with the same strides.  ym_conv_fwd_eval_ok(d) is 1
- * where the kernel this conv selects has the eval epilogue (the halo-staged 3x3 kernel, the 2-stage implicit GEMM with
- * >= 64 output channels); elsewhere run ym_conv_fwd + ym_bn_apply.  Bias-free convs only. */
+ * yolo11_modules.py:21-47 in eval mode).  d describes the conv with d->y_bs / d->y_ld the OUTPUT VIEW's strides
+ * (out_f32 = 2, accumulate 0); the residual (or NULL) is an fp16 view with strides r_bs / r_ld (elements, multiples
+ * of 4).  ym_conv_fwd_eval_ok(d) is 1 where the kernel this conv selects has the eval epilogue (the halo-staged 3x3
+ * kernel's 4-wave tile, the 2-stage implicit GEMM); elsewhere run ym_conv_fwd + ym_bn_apply.  Bias-free convs only. */
 int ym_conv_fwd_eval_ok(const ym_conv_desc* d);
+/* Stage / ring configuration of ym_conv_fwd_eval's implicit GEMM (0: 32-deep K stages x 3, 1: 64 x 3 (default),
+ * 2: 64 x 4); <0 restores the default.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
+int ym_conv_set_eval_cfg(int cfg);
 int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
-                     const float* shift, int act, const uint16_t* res, uint16_t* y, void* stream);
+                     const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* y,
+                     void* stream);
 /* Eval-mode coefficients of many BatchNorm layers in ONE launch (the eval forward's per-layer
  * ym_bn_eval_coeff calls were 77 launches per YOLOv11-s forward); table in device memory. */
 typedef struct ym_bn_eval_entry {

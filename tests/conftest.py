@@ -15,6 +15,13 @@ for p in (str(ROOT), str(PKG)):
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
     config.addinivalue_line("markers", "slow: long CPU test")
+    # parity runs of a non-default library policy: YM_LIB_SET="ym_conv_set_eval_cfg=2 ..." calls those process-wide
+    # setters (include/yolomi.h) before any test (unset in the driver's runs)
+    if os.environ.get("YM_LIB_SET"):
+        from yolomi._lib import lib
+        for kv in os.environ["YM_LIB_SET"].split():
+            name, val = kv.split("=")
+            getattr(lib(), name)(int(val))
 
 
 @pytest.fixture(scope="session")

@@ -3,7 +3,7 @@ shift -> SiLU -> + residual, yolo11_modules.py:21-47 in eval mode) — vs a PyTo
 the eval forward of a whole model with it vs without it.
 
 Kernel cases: the halo-staged 3x3 kernel's C4 tile (20x20 / 10x10 maps, channel counts off the 32-channel chunk) and
-the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2), with and without SiLU and a residual; the output is a
+the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2, outputs narrower than the tile), with and without SiLU and a residual (its own strides at n > 1); the output is a
 channel slice of a wider buffer (a concat slice: the other channels must stay untouched) and the residual a slice of
 another buffer with the same strides.  The operands are rounded to the kernel's dtypes first (fp16 activations,
 weights, residual), so the reference differs by fp32 accumulation order and the fp16 output rounding: rel 2e-3 of
@@ -26,6 +26,8 @@ CASES = [
     (2, 40, 40, 128, 128, 3, 2),
     (2, 13, 11, 64, 96, 3, 2),
     (1, 80, 80, 64, 64, 1, 1),
+    (1, 160, 160, 32, 32, 3, 1),
+    (2, 20, 20, 64, 40, 1, 1),
 ]
 
 
@@ -63,13 +65,15 @@ def test_conv_fwd_eval_vs_torch(case, act, with_res):
     dev = torch.device("cuda")
     xd, wd = x.to(dev), wt.permute(0, 2, 3, 1).contiguous().to(dev)
     scd, shd = scale.to(dev), shift.to(dev)
-    rbuf = torch.zeros(n, oh, ow, ld, dtype=torch.float16, device=dev)
+    rld = cout + 40 if n > 1 else ld                  # a residual with its own strides, or the output's
+    rbuf = torch.zeros(n, oh, ow, rld, dtype=torch.float16, device=dev)
     if res is not None:
         rbuf[..., 8:8 + cout] = res.to(dev)
     buf = torch.full((n, oh, ow, ld), 7.0, dtype=torch.float16, device=dev)
     torch.cuda.synchronize()
     call("ym_conv_fwd_eval", ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), scd.data_ptr(), shd.data_ptr(), act,
-         rbuf[..., 8:].data_ptr() if res is not None else None, buf[..., 8:].data_ptr(), stream_ptr(dev))
+         rbuf[..., 8:].data_ptr() if res is not None else None, oh * ow * rld, rld, buf[..., 8:].data_ptr(),
+         stream_ptr(dev))
     torch.cuda.synchronize()
     out = buf.float().cpu()
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"
@@ -79,13 +83,12 @@ def test_conv_fwd_eval_vs_torch(case, act, with_res):
 
 
 def test_conv_fwd_eval_ok_scope():
-    """Not eval-epilogue cases: a map the direct kernel takes, a GEMM with < 64 output channels, an accumulating or
-    non-fp16 output."""
+    """Not eval-epilogue cases: a map the direct kernel takes, an accumulating or non-fp16 output."""
     from yolomi._lib import lib
     d, _, _ = _desc(8, 160, 160, 64, 64, 3, 1, 64)              # >= 1 M output pixels: direct kernel
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
-    d, _, _ = _desc(1, 20, 20, 64, 32, 1, 1, 32)                # 2-stage GEMM, 32 output channels
-    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+    d, _, _ = _desc(1, 20, 20, 64, 32, 1, 1, 32)                # 2-stage GEMM, 32 output channels (masked tile half)
+    assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1
     d, _, _ = _desc(1, 20, 20, 256, 128, 1, 1, 128)
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1
     d.accumulate = 1

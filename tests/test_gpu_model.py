@@ -238,16 +238,17 @@ def test_sppf_pool_chain_exact(H, W, C):
     torch.testing.assert_close(cur_chk.cpu().view(B, H, W, C), xr2.grad.permute(0, 2, 3, 1), rtol=1e-6, atol=1e-5)
 
 
-@pytest.mark.parametrize("H,W,C", [(20, 20, 16), (9, 7, 12), (40, 40, 8)])
-def test_sppf_fused_chain_bit_identical(H, W, C):
+@pytest.mark.parametrize("H,W,C,B", [(20, 20, 16, 3), (9, 7, 12, 3), (40, 40, 8, 3), (20, 20, 256, 8),
+                                     (10, 10, 128, 8)])
+def test_sppf_fused_chain_bit_identical(H, W, C, B):
     """ym_sppf_fwd / ym_sppf_bwd (the three pools in one launch, chain in LDS) against three chained
     ym_maxpool5_f32_fwd / _bwd launches on the same inputs: pool values, argmax codes, fp16 slices,
     the fp32 routed gradient and the accumulated bf16 slice-0 gradient all bit-identical.
-    Shapes: 8- and 4-channel blocks, odd maps, the m@1280 40x40 map."""
+    Shapes: forward blocks of 8 / 4 channels (8 images) and 2 / 1 (3 images: the small-batch grid), odd maps, the
+    m@1280 40x40 map."""
     from yolomi._lib import call, lib, stream_ptr
     assert lib().ym_sppf_supported(H, W, C)
     g = torch.Generator().manual_seed(H * W + C)
-    B = 3
     M = B * H * W
     x = (torch.randint(-8, 8, (M, C), generator=g).float() / 4).cuda()    # exact ties, as chained pools make
     st = stream_ptr()

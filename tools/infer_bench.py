@@ -58,6 +58,12 @@ def main():
 
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
+    # A/B of a library policy: YM_LIB_SET="ym_conv_set_eval_cfg=2 ..." (process-wide setters, include/yolomi.h)
+    if os.environ.get("YM_LIB_SET"):
+        from yolomi._lib import lib as _yl0
+        for kv in os.environ["YM_LIB_SET"].split():
+            name, val = kv.split("=")
+            getattr(_yl0(), name)(int(val))
     cfg = yaml.safe_load((ROOT / "yolo-scratch_amd" / "configs" / "yolo11n_crater.yaml").read_text())
     cfg["scale"] = "s"
     torch.manual_seed(0)

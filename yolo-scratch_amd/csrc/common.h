@@ -43,12 +43,13 @@ static inline int64_t select_n(const ym_conv_desc* d) { return g_select_n > 0 ? 
 int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len);
 
 // eval-mode Conv block epilogue arguments (ym_conv_fwd_eval; conv_epi.h EvalEpi is built from them in the kernel):
-// BatchNorm scale / shift from the running statistics, SiLU when act, and an fp16 residual view with the output's
-// strides (res null: none; res_bytes: its extent from res for the buffer resource)
+// BatchNorm scale / shift from the running statistics, SiLU when act, and an fp16 residual view (res null: none;
+// r_bs / r_ld its image / pixel strides in elements; res_bytes its extent from res for the buffer resource)
 struct EvalArgs {
     const float* sc; const float* sh;
     int act;
     const uint16_t* res; int64_t res_bytes;
+    int64_t r_bs, r_ld;
 };
 
 typedef uint16_t bf16_t;   // raw bf16 bits in memory

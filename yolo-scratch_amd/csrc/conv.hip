@@ -326,8 +326,15 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
                 auto pix_ok = [&](int q) -> bool { return m0 + wc * (BM / WN) + q < Mc; };
                 if constexpr (EV) {
                     const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
-                    epilogue_regs<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
-                                          &ee);
+                    auto res_off = [&](int q) -> uint32_t {        // the forward: one class, stride-1 output grid
+                        const int64_t m = m0 + wc * (BM / WN) + q;
+                        if (m >= Mc) return OOB;
+                        uint32_t n, pix;
+                        dm_ohw(uint32_t(m), n, pix);
+                        return uint32_t((int64_t(n) * e.r_bs + int64_t(pix) * e.r_ld + wch0) * 2);
+                    };
+                    epilogue_regs_x<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off,
+                                            pix_ok, &ee, res_off);
                 } else {
                     epilogue_regs<TM, TN>(acc, ssum, ssq, MODE == MODE_FWD && a.st_sum != nullptr, lane, wch0, a.Nout,
                                           yres, MODE == MODE_FWD, MODE == MODE_DGRAD && a.accumulate != 0, pix_off,
@@ -839,25 +846,19 @@ static Tile pick_tile(int64_t Mc, int classes, int nout) {
     return {128, bn};
 }
 
-template <int KB, int NS, int MODE, bool EV = false>
-static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st, const EvalArgs& e) {
-    if constexpr (EV) {
-        // the eval epilogue is the register epilogue's (>= 32 channels per wave); 128x64 only (with it the 128x128
-        // instance spills)
-        return launch_gemm<128, 64, 2, 2, KB, NS, MODE, EV>(a, max_blocks, st, e);
-    } else {
-        if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
-        if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
-        // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
-        return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
-    }
+template <int KB, int NS, int MODE>
+static int launch_tile_k(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
+    if (t.bn == 128) return launch_gemm<128, 128, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+    if (t.bn == 64) return launch_gemm<128, 64, 2, 2, KB, NS, MODE>(a, max_blocks, st);
+    // 32-channel tiles need 64-deep stages (one 8-row DMA instruction per wave)
+    return launch_gemm<128, 32, 2, 2, 64, (KB == 64 ? NS : 2), MODE>(a, max_blocks, st);
 }
 
 // K-stage depth x ring depth, measured per layer (tools/layer_bench.py): 64-channel tiles prefer 32-deep stages
-template <int MODE, bool EV = false>
-static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st, const EvalArgs& e = EvalArgs{}) {
-    return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE, EV>(a, t, max_blocks, st, e)
-                                     : launch_tile_k<64, 2, MODE, EV>(a, t, max_blocks, st, e);
+template <int MODE>
+static int launch_tile(const GemmArgs& a, Tile t, int max_blocks, hipStream_t st) {
+    return t.bm == 128 && t.bn == 64 ? launch_tile_k<32, 3, MODE>(a, t, max_blocks, st)
+                                     : launch_tile_k<64, 2, MODE>(a, t, max_blocks, st);
 }
 
 // nsel: the batch the tile choice is made for (select_n: the real batch unless a parity test pins the
@@ -1086,7 +1087,17 @@ extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const ui
 // ym_bn_apply's launch go (a bs-1 s@640 eval forward is ~75 conv blocks, each ~4 us of apply launch).
 // The eval GEMM tile is 128x64 (the register epilogue needs >= 32 channels per wave; the 128x128 instance spills with
 // it); the halo kernel's eval instance is its 4-wave C4 tile (C8 spills).
-static Tile eval_tile(int64_t, int) { return Tile{128, 64}; }
+// the eval GEMM's K stage x ring (ym_conv_set_eval_cfg): 0: 32-deep stages, 3-stage ring (the training 128x64 tile's),
+// 1: 64-deep x 3, 2: 64-deep x 4 — at bs 1 a launch covers a few tiles and walks its whole K serially, so deeper
+// stages halve its DMA round trips
+static int g_eval_cfg = 1;
+
+extern "C" int ym_conv_set_eval_cfg(int cfg) {
+    // the eval GEMM's stage / ring configuration (0..2, -1 default 1); returns the previous setting
+    const int prev = g_eval_cfg;
+    g_eval_cfg = cfg < 0 || cfg > 2 ? 1 : cfg;
+    return prev;
+}
 
 extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
     if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return 0;
@@ -1096,18 +1107,22 @@ extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) return hp.cfg == 1 ? 1 : 0;
     const int64_t M = int64_t(d->n) * d->oh * d->ow;
-    return d->cout >= 64 && M < (int64_t(1) << 31) && offsets_fit(d->x_bs, int64_t(d->oh) * d->ow) ? 1 : 0;
+    return M < (int64_t(1) << 31) && offsets_fit(d->x_bs, int64_t(d->oh) * d->ow) ? 1 : 0;
 }
 
 extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
-                                const float* shift, int act, const uint16_t* res, uint16_t* y, void* stream) {
+                                const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld,
+                                uint16_t* y, void* stream) {
     YM_CHECK_ARG(d && x && w && scale && shift && y, "ym_conv_fwd_eval: null argument");
     YM_CHECK_ARG(ym_conv_fwd_eval_ok(d), "ym_conv_fwd_eval: not an eval-epilogue case (ym_conv_fwd_eval_ok = 0)");
     YM_CHECK_ARG(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(res) % 8 == 0 &&
                  reinterpret_cast<uintptr_t>(scale) % 16 == 0 && reinterpret_cast<uintptr_t>(shift) % 16 == 0,
                  "ym_conv_fwd_eval: misaligned output / residual / coefficient pointer");
+    YM_CHECK_ARG(!res || (r_ld % 4 == 0 && r_bs % 4 == 0 && r_ld >= d->cout && r_bs >= int64_t(d->oh) * d->ow * r_ld &&
+                          int64_t(d->n) * r_bs * 2 < (int64_t(1) << 31)),
+                 "ym_conv_fwd_eval: residual view strides");
     if (int64_t(d->n) * d->oh * d->ow == 0) return YM_OK;
-    const EvalArgs ev{scale, shift, act, res, int64_t(d->n) * d->y_bs * 2};
+    const EvalArgs ev{scale, shift, act, res, int64_t(d->n) * r_bs * 2, r_bs, r_ld};
     hipStream_t st = as_stream(stream);
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) {
@@ -1128,7 +1143,9 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
     a.N = d->n;
     a.ostep = 1;
     a.ep_lds = 1;
-    launch_tile<MODE_FWD, true>(a, eval_tile(a.M, d->cout), FWD_STAT_BLOCKS, st, ev);
+    if (g_eval_cfg == 0) launch_gemm<128, 64, 2, 2, 32, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
+    else if (g_eval_cfg == 1) launch_gemm<128, 64, 2, 2, 64, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
+    else launch_gemm<128, 64, 2, 2, 64, 4, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     YM_LAUNCH_CHECK("ym_conv_fwd_eval");
     return YM_OK;
 }

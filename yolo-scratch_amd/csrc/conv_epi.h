@@ -81,9 +81,9 @@ __device__ __forceinline__ void epilogue_store(f32x4 (&acc)[TM][TN], float (&ssu
 }
 
 // Eval-mode Conv block epilogue (ym_conv_fwd_eval): the running-statistics BatchNorm (scale / shift per output
-// channel), SiLU when act, then + the fp16 residual read at the output's own offset from the residual view's base (the
-// residual view has the output's image / pixel strides) — ym_bn_apply's arithmetic (fp32, one fp16 rounding), applied to
-// the accumulators before the pack instead of to a stored fp16 z.
+// channel), SiLU when act, then + the fp16 residual (res_off(q): byte offset of wave-local pixel q's channel wch0 in the
+// residual view) — ym_bn_apply's arithmetic (fp32, one fp16 rounding), applied to the accumulators before the pack
+// instead of to a stored fp16 z.
 struct EvalEpi {
     const float* sc; const float* sh;
     int act;
@@ -99,12 +99,13 @@ struct EvalEpi {
 // pix_off(q) as above (byte offset of wave-local pixel q's channel wch0, OOB outside); nout % 8 == 0.
 // pix_ok(q): pixel q of the wave lies inside the output (the statistics' mask; a compare, where pix_off also
 // decomposes the pixel).
-// ea: the eval-mode BatchNorm / SiLU / residual (a null constant for every other caller: no code, no registers).
-template <int TM, int TN, class PixOff, class PixOk>
-__device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
-                                              bool stats, int lane, int wch0, int nout,
-                                              __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
-                                              PixOff pix_off, PixOk pix_ok, const EvalEpi* ea = nullptr) {
+// ea: the eval-mode BatchNorm / SiLU / residual (a null constant for every other caller: no code, no registers),
+// res_off its residual offsets (see EvalEpi).
+template <int TM, int TN, class PixOff, class PixOk, class ResOff>
+__device__ __forceinline__ void epilogue_regs_x(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
+                                                bool stats, int lane, int wch0, int nout,
+                                                __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
+                                                PixOff pix_off, PixOk pix_ok, const EvalEpi* ea, ResOff res_off) {
     static_assert(TN % 2 == 0, "subtile pairs");
     const int fc = lane >> 4, fr = lane & 15;
     if (ea) {
@@ -126,7 +127,7 @@ __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum
         if (ea->res) {                                                 // + residual in fp32, one rounding (as ym_bn_apply)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const uint32_t b = pix_off(j * 16 + fr);
+                const uint32_t b = res_off(j * 16 + fr);
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     const int co = i * 16 + fc * 4;
@@ -188,6 +189,15 @@ __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum
                                                    yres, off, 0, 0);
         }
     }
+}
+
+template <int TM, int TN, class PixOff, class PixOk>
+__device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
+                                              bool stats, int lane, int wch0, int nout,
+                                              __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
+                                              PixOff pix_off, PixOk pix_ok) {
+    epilogue_regs_x<TM, TN>(acc, ssum, ssq, stats, lane, wch0, nout, yres, half, accumulate, pix_off, pix_ok, nullptr,
+                            pix_off);
 }
 
 }  // namespace ym

@@ -296,8 +296,15 @@ conv_halo_kernel(HaloArgs a, EvalArgs e) {
             auto pix_ok = [&](int q) -> bool { return (vmask >> (q >> 4)) & 1u; };
             if constexpr (EV) {
                 const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
-                epilogue_regs<TCW, TPW>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
-                                        &ee);
+                auto res_off = [&](int q) -> uint32_t {
+                    const int p = wp * TPW * 16 + q;
+                    const int ph = p / a.TW, pw = p - ph * a.TW;
+                    const int oh = oh0 + ph, ow = ow0 + pw;
+                    if (p >= ntp || oh >= a.OH || ow >= a.OW) return OOB;
+                    return uint32_t((int64_t(n) * e.r_bs + int64_t(oh * a.OW + ow) * e.r_ld + wch0) * 2);
+                };
+                epilogue_regs_x<TCW, TPW>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
+                                          &ee, res_off);
             } else {
                 epilogue_regs<TCW, TPW>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres, a.out_mode == 2,
                                         a.accumulate != 0 && a.out_mode == 0, pix_off, pix_ok);

@@ -368,6 +368,13 @@ int sppf_cg(int h, int w, int c) {
     return 0;
 }
 int sppf_cg_bwd(int h, int w, int c) { return sppf_cg(h, w, c) ? 4 : 0; }
+// the forward's channels per block for n images: narrower blocks until the grid holds ~256 of them (bs 1 at 20x20 x 256
+// channels ran 32 blocks of 8: 37 us; every (pixel, channel) is computed alone, so the width changes no result)
+static int sppf_cg_fwd(int n, int h, int w, int c) {
+    int cg = sppf_cg(h, w, c);
+    while (cg > 1 && int64_t(n) * (c / cg) < 256) cg >>= 1;
+    return cg;
+}
 
 // channels per block of the LDS forms (0: the map does not fit, use the direct kernels)
 int pool_cg(int h, int w, int c) {
@@ -613,18 +620,25 @@ extern "C" int ym_sppf_supported(int h, int w, int c) { return sppf_cg(h, w, c) 
 extern "C" int ym_sppf_fwd(const float* x, uint8_t* code, uint16_t* y1, uint16_t* y2, uint16_t* y3, int64_t y_bs,
                            int64_t y_ld, float* p_out, int n, int h, int w, int c, void* stream) {
     YM_CHECK_ARG(x && code && y1 && y2 && y3, "ym_sppf_fwd: null argument");
-    const int cg = sppf_cg(h, w, c);
+    const int cg = sppf_cg_fwd(n, h, w, c);
     YM_CHECK_ARG(cg != 0, "ym_sppf_fwd: map %dx%d x %d channels does not fit the fused kernel", h, w, c);
     YM_CHECK_ARG(int64_t(n) * h * w * c < (int64_t(1) << 31), "ym_sppf_fwd: too large");
     if (n == 0) return YM_OK;
     const int64_t plane = int64_t(n) * h * w * c;
     const size_t lds = size_t(h) * w * cg * 13;
+    const dim3 grid(unsigned(c / cg), unsigned(n));
     if (cg == 8)
-        hipLaunchKernelGGL(sppf_fwd_kernel<8>, dim3(unsigned(c / 8), unsigned(n)), dim3(256), lds, as_stream(stream), x,
-                           code, plane, y1, y2, y3, y_bs, y_ld, p_out, h, w, c);
+        hipLaunchKernelGGL(sppf_fwd_kernel<8>, grid, dim3(256), lds, as_stream(stream), x, code, plane, y1, y2, y3, y_bs,
+                           y_ld, p_out, h, w, c);
+    else if (cg == 4)
+        hipLaunchKernelGGL(sppf_fwd_kernel<4>, grid, dim3(256), lds, as_stream(stream), x, code, plane, y1, y2, y3, y_bs,
+                           y_ld, p_out, h, w, c);
+    else if (cg == 2)
+        hipLaunchKernelGGL(sppf_fwd_kernel<2>, grid, dim3(256), lds, as_stream(stream), x, code, plane, y1, y2, y3, y_bs,
+                           y_ld, p_out, h, w, c);
     else
-        hipLaunchKernelGGL(sppf_fwd_kernel<4>, dim3(unsigned(c / 4), unsigned(n)), dim3(256), lds, as_stream(stream), x,
-                           code, plane, y1, y2, y3, y_bs, y_ld, p_out, h, w, c);
+        hipLaunchKernelGGL(sppf_fwd_kernel<1>, grid, dim3(256), lds, as_stream(stream), x, code, plane, y1, y2, y3, y_bs,
+                           y_ld, p_out, h, w, c);
     YM_LAUNCH_CHECK("ym_sppf_fwd");
     return YM_OK;
 }

@@ -87,7 +87,8 @@ SIGNATURES = {
     "ym_conv_fwd_bn": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_set_fold": (R, [INT]),
     "ym_conv_fwd_eval_ok": (R, [P]),
-    "ym_conv_fwd_eval": (R, [P, P, P, P, P, INT, P, P, P]),
+    "ym_conv_set_eval_cfg": (R, [INT]),
+    "ym_conv_fwd_eval": (R, [P, P, P, P, P, INT, P, I64, I64, P, P]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
     "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
     "ym_bn_eval_coeff_batch": (R, [P, INT, P]),

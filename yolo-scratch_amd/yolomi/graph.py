@@ -306,21 +306,21 @@ class ConvBN:
 
     def _eval_one_launch(self, plan):
         """ym_conv_fwd_eval arguments for this op's eval forward (conv + eval BatchNorm + SiLU + residual in one
-        launch), or None: the selected kernel has no eval epilogue, the residual's strides differ from the output's, a
-        view is misaligned, or SPPF's pools need the fp32 copy.  YM_EVAL_FUSE=0 opts out."""
+        launch), or None: the selected kernel has no eval epilogue, a view is misaligned, or SPPF's pools need the
+        fp32 copy.  YM_EVAL_FUSE=0 opts out."""
         on = os.environ.get("YM_EVAL_FUSE", "1") != "0" and "out32" not in self.__dict__
         f = self.__dict__.get("_evf")
         if f is None or f[0] != on:
             args = None
             r = self.res
-            if on and (r is None or (r.bs == self.y.bs and r.ld == self.y.ld and r.ptr() % 8 == 0)) \
-                    and self.y.ptr() % 16 == 0:
+            if on and (r is None or (r.ptr() % 8 == 0 and r.ld % 4 == 0)) and self.y.ptr() % 16 == 0:
                 d = ConvDesc.from_buffer_copy(self.desc)
                 d.y_bs, d.y_ld, d.out_f32, d.accumulate = self.y.bs, self.y.ld, 2, 0
                 if lib().ym_conv_fwd_eval_ok(ctypes.byref(d)):
                     (sc, sh, _, _), _, _, _ = self._static_args(plan)
                     args = (d, ctypes.byref(d), self.x.ptr(), self.wf.data_ptr(), sc, sh, self.act,
-                            r.ptr() if r is not None else None, self.y.ptr())
+                            r.ptr() if r is not None else None, r.bs if r is not None else 0,
+                            r.ld if r is not None else 0, self.y.ptr())
             f = self._evf = (on, args)
         return f[1]
 
