@@ -191,6 +191,12 @@ int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, 
 /* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0); y = NULL: statistics only. */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
                       int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
+/* Eval-mode stem Conv block in one launch (inference): the stem conv, BatchNorm with the running-statistics scale /
+ * shift, SiLU if act, written into the fp16 activation view y (strides y_bs / y_ld, multiples of 8, y 16-B aligned)
+ * — what ym_conv_first_fwd + ym_bn_apply compute, without the statistics, the fp16 z and the apply launch. */
+int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, const float* scale, const float* shift, int act,
+                           uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh, int ow, int cout,
+                           int stride, int pad, void* stream);
 /* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
  * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). cout <= 128. */
 size_t ym_conv_first_wgrad_workspace_size(int cout);
@@ -212,8 +218,11 @@ size_t ym_dw3x3_bwd_workspace_size(int c);
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,
                  int c, int accumulate, float* workspace, size_t workspace_bytes, void* stream);
-/* All conv weights fp32 OIHW -> fp16 forward / bf16 dgrad layouts in one launch (table in device memory). */
+/* All conv weights fp32 OIHW -> fp16 forward / bf16 dgrad layouts in one launch (table in device memory).
+ * ym_prep_weights_fwd: the fp16 forward copies only (dst_t ignored) — for tables without data-gradient copies
+ * (an eval plan's): one grid row of workgroups, no LDS tile. */
 int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream);
+int ym_prep_weights_fwd(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream);
 
 /* ------------------------------------------------------------------ BatchNorm2d (train) + SiLU
  * Replaces BatchNorm2d + the shared in-place SiLU of Conv (models/yolo11_modules.py:24-33;
@@ -265,9 +274,21 @@ int ym_conv_fwd_eval_ok(const ym_conv_desc* d);
 /* Stage / ring configuration of ym_conv_fwd_eval's implicit GEMM (0: 32-deep K stages x 3, 1: 64 x 3 (default),
  * 2: 64 x 4); <0 restores the default.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_eval_cfg(int cfg);
+/* Small grids (a bs-1 forward's late layers: a few dozen tiles, each walking a long K serially) run as a K-split: the
+ * GEMM launch writes ks fp32 partial slices into the caller's workspace and a second launch applies BatchNorm / SiLU /
+ * residual to their sum.  ym_conv_fwd_eval_workspace_size(d) is the workspace that takes (0: one launch); with a
+ * NULL or smaller workspace the call runs unsplit.  ym_conv_set_eval_split(max_tiles): split layers of <= max_tiles
+ * 128x64 tiles and >= 12 K stages (default 64; 0 never; <0 restores the default); returns the previous setting.
+ * Process-wide, like ym_conv_set_halo; a workspace size queried under one setting serves only that setting. */
+size_t ym_conv_fwd_eval_workspace_size(const ym_conv_desc* d);
+int ym_conv_set_eval_split(int max_tiles);
+/* The K-split's K-stage threshold (split layers of >= min_stages 64-deep stages; default 12; <0 restores it) and the
+ * tile count at or below which an eval conv the halo kernel would take runs the 2-stage GEMM instead (default 0). */
+int ym_conv_set_eval_split_nk(int min_stages);
+int ym_conv_set_eval_gemm_tiles(int max_tiles);
 int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
                      const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* y,
-                     void* stream);
+                     void* workspace, size_t workspace_bytes, void* stream);
 /* Eval-mode coefficients of many BatchNorm layers in ONE launch (the eval forward's per-layer
  * ym_bn_eval_coeff calls were 77 launches per YOLOv11-s forward); table in device memory. */
 typedef struct ym_bn_eval_entry {

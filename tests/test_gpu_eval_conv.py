@@ -3,7 +3,9 @@ shift -> SiLU -> + residual, yolo11_modules.py:21-47 in eval mode) — vs a PyTo
 the eval forward of a whole model with it vs without it.
 
 Kernel cases: the halo-staged 3x3 kernel's C4 tile (20x20 / 10x10 maps, channel counts off the 32-channel chunk) and
-the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2, outputs narrower than the tile), with and without SiLU and a residual (its own strides at n > 1); the output is a
+the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2, outputs narrower than the tile), each with the workspace
+(the small-grid K-split: fp32 slices + a fold launch, where the policy splits) and without it (one launch), with and
+without SiLU and a residual (its own strides at n > 1); the output is a
 channel slice of a wider buffer (a concat slice: the other channels must stay untouched) and the residual a slice of
 another buffer with the same strides.  The operands are rounded to the kernel's dtypes first (fp16 activations,
 weights, residual), so the reference differs by fp32 accumulation order and the fp16 output rounding: rel 2e-3 of
@@ -28,6 +30,8 @@ CASES = [
     (1, 80, 80, 64, 64, 1, 1),
     (1, 160, 160, 32, 32, 3, 1),
     (2, 20, 20, 64, 40, 1, 1),
+    (1, 20, 20, 136, 64, 3, 1),       # K-split: 27 K stages in 6 slices, slices starting inside a tap
+    (1, 10, 10, 1024, 64, 1, 1),      # K-split of a 1x1: 16 stages in 4 slices
 ]
 
 
@@ -44,7 +48,8 @@ def _desc(n, h, w, cin, cout, k, s, ld):
 
 @pytest.mark.parametrize("case", CASES, ids=[f"n{c[0]}h{c[1]}w{c[2]}c{c[3]}o{c[4]}k{c[5]}s{c[6]}" for c in CASES])
 @pytest.mark.parametrize("act,with_res", [(1, False), (0, True), (1, True)])
-def test_conv_fwd_eval_vs_torch(case, act, with_res):
+@pytest.mark.parametrize("split", [True, False], ids=["ws", "nows"])
+def test_conv_fwd_eval_vs_torch(case, act, with_res, split):
     from yolomi._lib import call, lib, stream_ptr
     n, h, w, cin, cout, k, s = case
     ld = cout + 24                                   # output / residual: channel slices of wider buffers
@@ -70,10 +75,13 @@ def test_conv_fwd_eval_vs_torch(case, act, with_res):
     if res is not None:
         rbuf[..., 8:8 + cout] = res.to(dev)
     buf = torch.full((n, oh, ow, ld), 7.0, dtype=torch.float16, device=dev)
+    # with the workspace: the K-split (two launches) where the grid is small; without it: one launch
+    nws = lib().ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) if split else 0
+    ws = torch.full((max(nws, 1),), 255, dtype=torch.uint8, device=dev)     # NaN-filled: every slice element written
     torch.cuda.synchronize()
     call("ym_conv_fwd_eval", ctypes.byref(d), xd.data_ptr(), wd.data_ptr(), scd.data_ptr(), shd.data_ptr(), act,
          rbuf[..., 8:].data_ptr() if res is not None else None, oh * ow * rld, rld, buf[..., 8:].data_ptr(),
-         stream_ptr(dev))
+         ws.data_ptr() if nws else None, nws, stream_ptr(dev))
     torch.cuda.synchronize()
     out = buf.float().cpu()
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"
@@ -95,6 +103,29 @@ def test_conv_fwd_eval_ok_scope():
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
     d.accumulate, d.out_f32 = 0, 1
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
+    assert lib().ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 0
+
+
+def test_conv_fwd_eval_split_policy():
+    """K-split where a layer is <= 64 tiles with >= 12 K stages: ks = min(stages / 4, 256 / tiles, 16) fp32 slices of
+    M x Cout; none with the setter at 0 or on a large grid."""
+    from yolomi._lib import lib
+    L = lib()
+    d, _, _ = _desc(1, 20, 20, 256, 256, 3, 2, 256)            # 100 px x 256: 4 tiles, 36 stages -> 9 slices
+    assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 9 * 100 * 256 * 4
+    d, _, _ = _desc(1, 80, 80, 128, 64, 3, 1, 64)              # 50 tiles, 18 stages -> 4 slices
+    assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 4 * 6400 * 64 * 4
+    assert L.ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1
+    d, _, _ = _desc(16, 80, 80, 128, 64, 3, 1, 64)             # 800 tiles: one launch
+    assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 0
+    d, _, _ = _desc(1, 20, 20, 256, 128, 1, 1, 128)            # 4 K stages: one launch
+    assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 0
+    prev = L.ym_conv_set_eval_split(0)
+    try:
+        d, _, _ = _desc(1, 20, 20, 256, 256, 3, 2, 256)
+        assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 0
+    finally:
+        L.ym_conv_set_eval_split(prev)
 
 
 @pytest.mark.parametrize("scale_name,imgsz,bs", [("s", 640, 1), ("n", 320, 2)])
@@ -130,3 +161,31 @@ def test_eval_forward_one_launch_blocks_vs_unfused(scale_name, imgsz, bs, monkey
     for a, b in zip(m0, m1):
         err, mag = float((a - b).abs().max()), float(a.abs().max())
         assert err <= 2e-2 * mag + 1e-2, (err, mag)
+
+
+@pytest.mark.parametrize("n,h,w,cout,act", [(1, 64, 64, 32, 1), (2, 37, 41, 16, 1), (1, 20, 20, 64, 0)])
+def test_conv_first_fwd_eval_vs_torch(n, h, w, cout, act):
+    """ym_conv_first_fwd_eval — the stem Conv block (ch 1 -> cout, 3x3 s2 on the fp32 image) with the eval BatchNorm and
+    SiLU in one launch, into a channel slice of a wider buffer, vs torch fp32 (fp16 output rounding)."""
+    from yolomi._lib import call, stream_ptr
+    g = torch.Generator().manual_seed(n * 1000 + h + cout)
+    img = torch.rand(n, 1, h, w, generator=g)
+    wt = torch.randn(cout, 1, 3, 3, generator=g) / 3
+    scale = torch.rand(cout, generator=g) + 0.5
+    shift = torch.randn(cout, generator=g) * 0.2
+    ref = F.conv2d(img, wt, stride=2, padding=1).permute(0, 2, 3, 1) * scale + shift
+    if act:
+        ref = F.silu(ref)
+    oh, ow = ref.shape[1], ref.shape[2]
+    ld = cout + 16
+    dev = torch.device("cuda")
+    buf = torch.full((n, oh, ow, ld), 7.0, dtype=torch.float16, device=dev)
+    imgd, wd, scd, shd = img.to(dev), wt.to(dev), scale.to(dev), shift.to(dev)
+    torch.cuda.synchronize()
+    call("ym_conv_first_fwd_eval", imgd.data_ptr(), wd.data_ptr(), scd.data_ptr(), shd.data_ptr(), act,
+         buf[..., 8:].data_ptr(), oh * ow * ld, ld, n, h, w, oh, ow, cout, 2, 1, stream_ptr(dev))
+    torch.cuda.synchronize()
+    out = buf.float().cpu()
+    assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"
+    err, mag = float((out[..., 8:8 + cout] - ref).abs().max()), float(ref.abs().max())
+    assert err <= 2e-3 * mag + 1e-3, f"max |diff| {err:.3e} vs max |ref| {mag:.3e}"

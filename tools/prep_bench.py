@@ -1,50 +1,63 @@
-"""Times ym_prep_weights (the once-per-step fp32 -> fp16/bf16 weight conversion) over a model plan's
-whole weight table: python3 tools/prep_bench.py [--scale s] [--reps 50]."""
+"""ym_prep_weights alone on a model's conv weights (the table a plan's WeightStore builds): average launch time over
+--reps launches, HIP events on the launch stream.  --train adds the transposed data-gradient copies (the training
+plan's table); without it the forward copies only (the eval plan's).  YOLOMI_LIB picks the library (A/B).
+
+usage: python tools/prep_bench.py [--scale s --train --reps 200]
+"""
 import argparse
+import json
 import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-sys.path.insert(0, str(ROOT / "yolo-scratch_amd"))
+for p in (str(ROOT), str(ROOT / "yolo-scratch_amd")):
+    sys.path.insert(0, p)
+
+import torch  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", default="s")
-    ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--train", action="store_true")
+    ap.add_argument("--reps", type=int, default=200)
     args = ap.parse_args()
-    import torch
     import yaml
     from models import build_yolo11
-    from losses import v8DetectionLoss
-    from datasets.synthetic import synth_batch
-    from yolomi._lib import stream_ptr
+    from yolomi._lib import WPrepEntry, call, lib, stream_ptr
 
     dev = torch.device("cuda", 0)
     cfg = yaml.safe_load((ROOT / "yolo-scratch_amd" / "configs" / "yolo11n_crater.yaml").read_text())
     cfg["scale"] = args.scale
-    model = build_yolo11(cfg, ch=1, nc=5).to(dev).train()
-    crit = v8DetectionLoss(model)
-    b = {k: v.to(dev) for k, v in synth_batch(2, 640, seed=1).items()}
-    loss, _ = crit(model(b["img"]), b)
-    loss.backward()
-    torch.cuda.synchronize()
-    ws = model.__dict__["_ym_last_plan"].weights
-    st = stream_ptr(dev)
-    s = torch.cuda.current_stream(dev)
-    for _ in range(5):
-        ws.refresh(st)
+    torch.manual_seed(0)
+    model = build_yolo11(cfg, ch=1, nc=5).to(dev)
+    ws = [p for p in model.parameters() if p.dim() == 4]
+    keep = []
+    arr = (WPrepEntry * len(ws))()
+    off = 0
+    for e, w in zip(arr, ws):
+        co, ci, kh, kw = w.shape
+        fwd = torch.empty(co, kh, kw, ci, dtype=torch.float16, device=dev)
+        t = torch.empty(ci, kh, kw, co, dtype=torch.bfloat16, device=dev) if args.train else None
+        keep += [fwd, t]
+        e.src, e.dst_fwd, e.dst_t = w.data_ptr(), fwd.data_ptr(), (t.data_ptr() if t is not None else None)
+        e.elem_offset, e.cout, e.cin, e.kh, e.kw, e.cout_t = off, co, ci, kh, kw, co
+        off += w.numel()
+    table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+    st = torch.cuda.current_stream(dev)
+    # a forward-only table takes the forward-only launch where the library has it (as WeightStore.refresh does)
+    entry = "ym_prep_weights_fwd" if not args.train and hasattr(lib(), "ym_prep_weights_fwd") else "ym_prep_weights"
+    for _ in range(10):
+        call(entry, table.data_ptr(), len(ws), off, stream_ptr(dev))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
+    e0.record(st)
     for _ in range(args.reps):
-        ws.refresh(st)
-    e1.record(s)
+        call(entry, table.data_ptr(), len(ws), off, stream_ptr(dev))
+    e1.record(st)
     torch.cuda.synchronize()
-    us = e0.elapsed_time(e1) * 1e3 / args.reps
-    n_t = sum(t.numel() for _, _, t, _ in ws.items if t is not None)
-    byts = ws.total * 4 + ws.total * 2 + n_t * 2        # fp32 read once (ideal) + fp16 + bf16 writes
-    print(f"prep_weights: {len(ws.items)} entries, {ws.total} elements, {us:.1f} us/launch, "
-          f"{byts / us / 1e6:.2f} TB/s algorithmic")
+    us = e0.elapsed_time(e1) / args.reps * 1e3
+    print(json.dumps({"scale": args.scale, "train": args.train, "entry": entry, "entries": len(ws), "elements": off,
+                      "us_per_launch": round(us, 2)}))
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@ iteration, e.g. the first kernel of a forward), also the per-iteration wall span
 iteration's kernels), the summed kernel time and the time no kernel was running, averaged over the last --last
 iterations.
 
-usage: python tools/rocpd_summary.py DB [--iter-kernel prep_weights_kernel --last 20 --top 30]
+usage: python tools/rocpd_summary.py DB [--iter-kernel prep_weights_kernel --last 20 --top 30 --sequence]
 """
 import argparse
 import collections
@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--iter-kernel", default=None)
     ap.add_argument("--last", type=int, default=20)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--sequence", action="store_true", help="also list the last iteration's kernels in order")
     args = ap.parse_args()
     db = sqlite3.connect(args.db)
     rows = db.execute("select name, start, end from kernels order by start").fetchall()
@@ -49,6 +50,13 @@ def main():
             idle.append((t1 - t0 - cover) / 1e3)
             nk.append(len(seg))
         k = len(its)
+        if args.sequence:
+            seg = rows[its[-1][0]:its[-1][1]]
+            prev = seg[0][1]
+            print("start_us  gap_us  dur_us  kernel (last iteration)")
+            for n, s_, e_ in seg:
+                print(f"{(s_ - seg[0][1]) / 1e3:8.1f} {(s_ - prev) / 1e3:7.1f} {(e_ - s_) / 1e3:7.2f}  {n[:100]}")
+                prev = max(prev, e_)
         print(f"per iteration (last {k}): {sum(nk) / k:.0f} kernels, span {sum(spans) / k:.1f} us, "
               f"summed kernel time {sum(busy) / k:.1f} us, no kernel running {sum(idle) / k:.1f} us")
 

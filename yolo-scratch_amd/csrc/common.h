@@ -44,12 +44,15 @@ int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len);
 
 // eval-mode Conv block epilogue arguments (ym_conv_fwd_eval; conv_epi.h EvalEpi is built from them in the kernel):
 // BatchNorm scale / shift from the running statistics, SiLU when act, and an fp16 residual view (res null: none;
-// r_bs / r_ld its image / pixel strides in elements; res_bytes its extent from res for the buffer resource)
+// r_bs / r_ld its image / pixel strides in elements; res_bytes its extent from res for the buffer resource).
+// ks > 1: the K-split form (the 2-stage GEMM only): blockIdx.z walks K slice z of ks and stores its fp32 partial sums to
+// part[z][M][Nout]; eval_fold_kernel applies the epilogue to their sum
 struct EvalArgs {
     const float* sc; const float* sh;
     int act;
     const uint16_t* res; int64_t res_bytes;
     int64_t r_bs, r_ld;
+    int ks; float* part;
 };
 
 typedef uint16_t bf16_t;   // raw bf16 bits in memory

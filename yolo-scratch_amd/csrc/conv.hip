@@ -182,6 +182,14 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
     const int xcd = bx & 7, lstride = gxx >> 3;
     const int per_xcd = (mtiles + 7) >> 3;
     const int mt_end = min((xcd + 1) * per_xcd, mtiles);
+    // K steps this workgroup walks: all nk, or the eval K-split's slice blockIdx.z of e.ks (k_lo .. k_lo + nkl)
+    int k_lo = 0, nkl = nk;
+    if constexpr (EV) {
+        if (e.ks > 1) {
+            k_lo = int(blockIdx.z) * nk / e.ks;
+            nkl = (int(blockIdx.z) + 1) * nk / e.ks - k_lo;
+        }
+    }
     for (int mt = xcd * per_xcd + (bx >> 3); mt < mt_end; mt += lstride) {
         const int64_t m0 = int64_t(mt) * BM;
         const uint32_t nfirst = uint32_t(m0) / OHW;          // Mc < 2^31 (host check): one 32-bit scalar division
@@ -223,6 +231,15 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
         };
         int c_next = 0;
         uint32_t a_tap = 0;
+        if constexpr (EV) {
+            if (k_lo) {                    // a K slice starting at tap k_lo / kc, chunk k_lo % kc
+                const int tap = k_lo / kc;
+                t_i = tap / nkw;
+                t_j = tap - t_i * nkw;
+                c_next = k_lo - tap * kc;
+                if (c_next) a_tap = tap_setup();
+            }
+        }
         // issue one stage of LDS-DMA: AI + BI buffer_load_dwordx4 ... lds per wave
         auto issue = [&](int buf) {
             if (c_next == 0) a_tap = tap_setup();
@@ -256,16 +273,16 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
         raw_barrier();                     // previous tile's readers are done with every stage
 #pragma unroll
         for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
-            if (s0 < nk) issue(s0);
-        for (int k = 0; k < nk; ++k) {
+            if (s0 < nkl) issue(s0);
+        for (int k = 0; k < nkl; ++k) {
             const int buf = k % NSTAGE;
             // this wave's DMAs of stage k have landed (the later stages may stay in flight)
-            const int ahead = min(NSTAGE - 2, nk - 1 - k);
+            const int ahead = min(NSTAGE - 2, nkl - 1 - k);
             if (NSTAGE >= 4 && ahead >= 2) wait_vmcnt<(NSTAGE >= 4 ? 2 : 0) * (AI + BI)>();
             else if (NSTAGE >= 3 && ahead >= 1) wait_vmcnt<(NSTAGE >= 3 ? 1 : 0) * (AI + BI)>();
             else wait_vmcnt<0>();
             raw_barrier();                 // ... everyone's, and everyone finished reading stage k-1
-            if (k + NSTAGE - 1 < nk) issue((k + NSTAGE - 1) % NSTAGE);
+            if (k + NSTAGE - 1 < nkl) issue((k + NSTAGE - 1) % NSTAGE);
             const char* As = smem + buf * STAGE;
             const char* Bs = As + BN * RB;
             // fragments of both 32-deep halves first, then the MFMAs (two register sets; the order is
@@ -325,6 +342,22 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
                 };
                 auto pix_ok = [&](int q) -> bool { return m0 + wc * (BM / WN) + q < Mc; };
                 if constexpr (EV) {
+                    if (e.ks > 1) {        // K slice: fp32 partial sums, 4 channels of one pixel per lane (Nout % 8 == 0)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const int64_t m = m0 + wc * (BM / WN) + j * 16 + fr;
+                            if (m >= Mc) continue;
+                            float* pp = e.part + (int64_t(blockIdx.z) * Mc + m) * a.Nout;
+#pragma unroll
+                            for (int i = 0; i < TM; ++i) {
+                                const int cb = wch0 + i * 16 + fc * 4;
+                                if (cb < a.Nout)
+                                    *reinterpret_cast<float4*>(pp + cb) =
+                                        make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+                            }
+                        }
+                        continue;
+                    }
                     const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
                     auto res_off = [&](int q) -> uint32_t {        // the forward: one class, stride-1 output grid
                         const int64_t m = m0 + wc * (BM / WN) + q;
@@ -499,6 +532,55 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
     for (int c = threadIdx.x; c < Cout; c += 256) {
         st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
         st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
+    }
+}
+
+// eval-mode stem Conv block in one launch (ym_conv_first_fwd_eval): the same per-(pixel, 8 channels) conv, then the
+// running-statistics BatchNorm + SiLU on the fp32 sum (EvalEpi's arithmetic) and one 16-B store into the activation
+// view; no statistics, no fp16 z, no apply launch
+__global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __restrict__ img, const float* __restrict__ w,
+                                                              const float* __restrict__ sc, const float* __restrict__ sh,
+                                                              int act, uint16_t* __restrict__ y, int64_t y_bs,
+                                                              int64_t y_ld, int N, int H, int W, int OH, int OW,
+                                                              int Cout, int stride, int pad) {
+    const int G = Cout >> 3;
+    const int g = threadIdx.x % G;
+    float wr[8][9], s[8], h[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[r][t] = w[(g * 8 + r) * 9 + t];
+        s[r] = sc[g * 8 + r];
+        h[r] = sh[g * 8 + r];
+    }
+    const int M = N * OH * OW, OHW = OH * OW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
+        float patch[9];
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+                patch[kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
+                                         ? img[(n * H + ih) * W + iw] : 0.f;
+            }
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            float a = 0.f;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) a += wr[r][t] * patch[t];
+            const float u = fmaf(a, s[r], h[r]);
+            v[r] = act ? silu_f(u) : u;
+        }
+        uint4 o;
+        o.x = pk2h(v[0], v[1]);
+        o.y = pk2h(v[2], v[3]);
+        o.z = pk2h(v[4], v[5]);
+        o.w = pk2h(v[6], v[7]);
+        *reinterpret_cast<uint4*>(y + int64_t(n) * y_bs + int64_t(pix) * y_ld + g * 8) = o;
     }
 }
 
@@ -722,11 +804,32 @@ __device__ __forceinline__ void prep_one(const ym_wprep_entry& t, int j, int pas
     }
 }
 
+// FWD_ONLY: the forward copies alone (ym_prep_weights_fwd: tables without transposed copies, e.g. an eval plan's) —
+// no LDS tile, so twice the resident workgroups per CU, and no second grid row of workgroups that find nothing to do
+template <bool FWD_ONLY>
 __global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int n_entries,
                                                            int64_t total) {
     const int64_t c0 = int64_t(blockIdx.x) * PREP_CHUNK, c1 = min(c0 + PREP_CHUNK, total);
-    const int pass = blockIdx.y;
+    const int pass = FWD_ONLY ? 0 : int(blockIdx.y);
+    // the chunk's first entry (the last with elem_offset <= c0; offsets ascending): a two-level 64-ary search, each level
+    // one load per lane + a ballot (every wave repeats it: no LDS, no barrier) — 2 memory round trips for <= 4096
+    // entries where a binary search chains ~log2(entries) dependent loads (~7 x ~0.8 us per workgroup on s@640, most
+    // of this launch's time: 5.5 k short workgroups); larger tables continue with the binary search
+    const int lane = threadIdx.x & 63;
+    const int s1 = (n_entries + 63) >> 6;
     int lo = 0, hi = n_entries - 1;
+    {
+        const int i1 = min(lane * s1, n_entries - 1);
+        const uint64_t m1 = __ballot(lane * s1 < n_entries && tab[i1].elem_offset <= c0);
+        lo = (__popcll(m1) - 1) * s1;                            // lane 0 (offset 0) always qualifies
+        hi = min(lo + s1 - 1, n_entries - 1);
+        if (s1 > 1 && s1 <= 64) {
+            const int i2 = min(lo + lane, hi);
+            const uint64_t m2 = __ballot(lane < s1 && lo + lane <= hi && tab[i2].elem_offset <= c0);
+            lo += __popcll(m2) - 1;
+            hi = lo;
+        }
+    }
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (tab[mid].elem_offset <= c0) lo = mid;
@@ -747,18 +850,20 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry*
         const int j0 = int(c0 - t.elem_offset);
         const int fs = j0 / t.cout, fe = (nj - 1) / t.cout, nf = fe - fs + 1;
         const int ld = nf | 1;                                   // odd row stride: conflict-free column reads
-        if (pass == 1 && t.cout * ld <= PREP_LDS) {
-            __shared__ float tile[PREP_LDS];
-            for (int idx = threadIdx.x; idx < t.cout * nf; idx += 256) {
-                const int co = idx / nf, fi = idx - co * nf;
-                tile[co * ld + fi] = t.src[int64_t(co) * F + fs + fi];
+        if constexpr (!FWD_ONLY) {
+            if (pass == 1 && t.cout * ld <= PREP_LDS) {
+                __shared__ float tile[PREP_LDS];
+                for (int idx = threadIdx.x; idx < t.cout * nf; idx += 256) {
+                    const int co = idx / nf, fi = idx - co * nf;
+                    tile[co * ld + fi] = t.src[int64_t(co) * F + fs + fi];
+                }
+                __syncthreads();
+                for (int j = jb; j < nj; j += 256) {
+                    const int f = j / t.cout, co = j - f * t.cout;
+                    dst[int64_t(f) * t.cout_t + co] = f2bf(tile[co * ld + (f - fs)]);
+                }
+                return;
             }
-            __syncthreads();
-            for (int j = jb; j < nj; j += 256) {
-                const int f = j / t.cout, co = j - f * t.cout;
-                dst[int64_t(f) * t.cout_t + co] = f2bf(tile[co * ld + (f - fs)]);
-            }
-            return;
         }
         float v[PREP_PER];
         int64_t di[PREP_PER];
@@ -811,6 +916,54 @@ static bool offsets_fit(int64_t bs, int64_t class_pixels) {
     return bs * 2 * images < (int64_t(1) << 31);
 }
 
+// the eval K-split's second launch (ym_conv_fwd_eval with ks > 1): y = act(sum_z part[z] * scale + shift) (+ res),
+// the register epilogue's arithmetic (EvalEpi) on the slices' fp32 sum, summed in slice order (deterministic);
+// one thread per (pixel, 8 channels), C % 8 == 0, M * C / 8 < 2^31 and M < 2^32 (host checks)
+__global__ void __launch_bounds__(256) eval_fold_kernel(const float* __restrict__ part, int ks, int64_t M, int C,
+                                                        uint32_t OHW, const float* __restrict__ sc,
+                                                        const float* __restrict__ sh, int act,
+                                                        const uint16_t* __restrict__ res, int64_t r_bs, int64_t r_ld,
+                                                        uint16_t* __restrict__ y, int64_t y_bs, int64_t y_ld) {
+    const int G = C >> 3;
+    const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+    if (idx >= M * G) return;
+    const int64_t m = idx / G;
+    const int c0 = int(idx - m * G) * 8;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < ks; ++z) {
+        const float4* p = reinterpret_cast<const float4*>(part + (int64_t(z) * M + m) * C + c0);
+        const float4 a = p[0], b = p[1];
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w;
+        v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+    }
+    const float4 s0 = *reinterpret_cast<const float4*>(sc + c0), s1 = *reinterpret_cast<const float4*>(sc + c0 + 4);
+    const float4 h0 = *reinterpret_cast<const float4*>(sh + c0), h1 = *reinterpret_cast<const float4*>(sh + c0 + 4);
+    const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float t = fmaf(v[k], s[k], h[k]);
+        v[k] = act ? silu_f(t) : t;
+    }
+    const uint32_t n = uint32_t(m) / OHW, pix = uint32_t(m) - n * OHW;
+    if (res) {                                                   // 8-B aligned residual rows (r_ld % 4 == 0)
+        const uint2* rp = reinterpret_cast<const uint2*>(res + int64_t(n) * r_bs + int64_t(pix) * r_ld + c0);
+        const uint2 r0 = rp[0], r1 = rp[1];
+        const uint32_t rw[4] = {r0.x, r0.y, r1.x, r1.y};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            v[2 * k] += h2f(uint16_t(rw[k] & 0xffff));
+            v[2 * k + 1] += h2f(uint16_t(rw[k] >> 16));
+        }
+    }
+    uint4 o;
+    o.x = pk2h(v[0], v[1]);
+    o.y = pk2h(v[2], v[3]);
+    o.z = pk2h(v[4], v[5]);
+    o.w = pk2h(v[6], v[7]);
+    *reinterpret_cast<uint4*>(y + int64_t(n) * y_bs + int64_t(pix) * y_ld + c0) = o;
+}
+
 template <int BM, int BN, int WM, int WN, int KB, int NS, int MODE, bool EV = false>
 int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st, const EvalArgs& e = EvalArgs{}) {
     GemmArgs a = a0;
@@ -821,7 +974,8 @@ int launch_gemm(const GemmArgs& a0, int max_blocks, hipStream_t st, const EvalAr
     int gx = grid_x(a.mtiles, ntiles, a.st_sum != nullptr, max_blocks);
     // channel tiles of one m-tile sequence interleaved into grid x (dispatched together)
     a.ntl = ntiles > 1 ? ntiles : 0;
-    const dim3 grid(a.ntl ? gx * ntiles : gx, a.ntl ? 1 : ntiles, os == 2 ? 4 : 1), block(WM * WN * 64);
+    const int gz = os == 2 ? 4 : (EV && e.ks > 1 ? e.ks : 1);   // parity classes / eval K slices
+    const dim3 grid(a.ntl ? gx * ntiles : gx, a.ntl ? 1 : ntiles, gz), block(WM * WN * 64);
     hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, WM, WN, KB, NS, MODE, EV>), grid, block, 0, st, a, e);
     return gx;
 }
@@ -1099,20 +1253,87 @@ extern "C" int ym_conv_set_eval_cfg(int cfg) {
     return prev;
 }
 
+// K-split on small grids (ym_conv_set_eval_split): a bs-1 late layer is a few dozen 128x64 tiles, each walking a K of
+// up to 72 stages serially (~0.6 us a stage); with ks > 1 the launch's blockIdx.z walks K slice z of ks into an fp32
+// partial slab (EvalArgs.part) and eval_fold_kernel applies BatchNorm / SiLU / residual to the slices' sum — one
+// extra launch (~4 us) for a K walk ks times shorter.  Split where the layer has <= g_eval_split tiles and >= 12 K
+// stages: ks = min(stages / 4, 256 / tiles, 16) (>= 4 stages a slice, <= ~one workgroup per CU).
+static int g_eval_split = 64, g_eval_split_nk = 12, g_eval_gemm_tiles = 0;
+
+extern "C" int ym_conv_set_eval_split(int max_tiles) {
+    // the eval K-split's tile threshold (0: never split, -1: default 64); returns the previous setting
+    const int prev = g_eval_split;
+    g_eval_split = max_tiles < 0 ? 64 : max_tiles;
+    return prev;
+}
+
+extern "C" int ym_conv_set_eval_split_nk(int min_stages) {
+    // the eval K-split's K-stage threshold (-1: default 12); returns the previous setting
+    const int prev = g_eval_split_nk;
+    g_eval_split_nk = min_stages < 0 ? 12 : min_stages;
+    return prev;
+}
+
+extern "C" int ym_conv_set_eval_gemm_tiles(int max_tiles) {
+    // eval convs of <= max_tiles 128x64 tiles take the 2-stage GEMM where the halo kernel would run (0: never,
+    // -1: default 0); returns the previous setting
+    const int prev = g_eval_gemm_tiles;
+    g_eval_gemm_tiles = max_tiles < 0 ? 0 : max_tiles;
+    return prev;
+}
+
+static int64_t eval_tiles(const ym_conv_desc* d) {
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    return ((M + 127) / 128) * ((d->cout + 63) / 64);
+}
+
+static bool eval_gemm_fits(const ym_conv_desc* d) {
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    return M < (int64_t(1) << 31) && offsets_fit(d->x_bs, int64_t(d->oh) * d->ow);
+}
+
+// K slices of d's eval forward (1: no split); d passed ym_conv_fwd_eval_ok's layout checks
+static int eval_ks(const ym_conv_desc* d) {
+    if (g_eval_split == 0 || !eval_gemm_fits(d)) return 1;
+    const int64_t M = int64_t(d->n) * d->oh * d->ow;
+    const int64_t tiles = ((M + 127) / 128) * ((d->cout + 63) / 64);
+    const int KB = g_eval_cfg == 0 ? 32 : 64;
+    const int nk = d->k * d->k * ((d->cin + KB - 1) / KB);
+    if (tiles > g_eval_split || nk < g_eval_split_nk) return 1;
+    const int64_t ks = std::min<int64_t>(std::min<int64_t>(nk / 4, std::max<int64_t>(1, 256 / tiles)), 16);
+    return ks >= 2 && M * (d->cout / 8) < (int64_t(1) << 31) ? int(ks) : 1;
+}
+
+static bool eval_layout_ok(const ym_conv_desc* d) {
+    if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return false;
+    if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return false;
+    if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return false;
+    return !(direct_plan(d, 0).ok || hpipe_plan(d, 0).ok || pipe_plan(d, 0).ok);   // no eval epilogue there
+}
+
+// the eval forward runs the halo kernel's eval instance (not the GEMM) for d
+static bool eval_halo(const ym_conv_desc* d, const HaloPlan& hp) {
+    return hp.ok && hp.cfg == 1 && !(eval_tiles(d) <= g_eval_gemm_tiles && eval_gemm_fits(d));
+}
+
 extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
-    if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return 0;
-    if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return 0;
-    if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return 0;
-    if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok || pipe_plan(d, 0).ok) return 0;   // no eval epilogue there
+    if (!eval_layout_ok(d)) return 0;
+    if (eval_ks(d) > 1 || (eval_tiles(d) <= g_eval_gemm_tiles && eval_gemm_fits(d))) return 1;
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) return hp.cfg == 1 ? 1 : 0;
-    const int64_t M = int64_t(d->n) * d->oh * d->ow;
-    return M < (int64_t(1) << 31) && offsets_fit(d->x_bs, int64_t(d->oh) * d->ow) ? 1 : 0;
+    return eval_gemm_fits(d) ? 1 : 0;
+}
+
+extern "C" size_t ym_conv_fwd_eval_workspace_size(const ym_conv_desc* d) {
+    // bytes of the fp32 slice partials ym_conv_fwd_eval's K-split takes for d (0: one launch, no workspace)
+    if (!eval_layout_ok(d)) return 0;
+    const int ks = eval_ks(d);
+    return ks > 1 ? size_t(ks) * size_t(int64_t(d->n) * d->oh * d->ow) * size_t(d->cout) * sizeof(float) : 0;
 }
 
 extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
                                 const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld,
-                                uint16_t* y, void* stream) {
+                                uint16_t* y, void* workspace, size_t workspace_bytes, void* stream) {
     YM_CHECK_ARG(d && x && w && scale && shift && y, "ym_conv_fwd_eval: null argument");
     YM_CHECK_ARG(ym_conv_fwd_eval_ok(d), "ym_conv_fwd_eval: not an eval-epilogue case (ym_conv_fwd_eval_ok = 0)");
     YM_CHECK_ARG(reinterpret_cast<uintptr_t>(y) % 16 == 0 && reinterpret_cast<uintptr_t>(res) % 8 == 0 &&
@@ -1122,10 +1343,18 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
                           int64_t(d->n) * r_bs * 2 < (int64_t(1) << 31)),
                  "ym_conv_fwd_eval: residual view strides");
     if (int64_t(d->n) * d->oh * d->ow == 0) return YM_OK;
-    const EvalArgs ev{scale, shift, act, res, int64_t(d->n) * r_bs * 2, r_bs, r_ld};
+    // the K-split where it applies and the caller gave its workspace (null / too small: one launch)
+    const size_t need = ym_conv_fwd_eval_workspace_size(d);
+    const int ks = need && workspace && workspace_bytes >= need && reinterpret_cast<uintptr_t>(workspace) % 16 == 0
+                       ? eval_ks(d) : 1;
+    EvalArgs ev{scale, shift, act, res, int64_t(d->n) * r_bs * 2, r_bs, r_ld};
+    if (ks > 1) {
+        ev.ks = ks;
+        ev.part = static_cast<float*>(workspace);
+    }
     hipStream_t st = as_stream(stream);
     const HaloPlan hp = halo_plan(d, 0);
-    if (hp.ok) {
+    if (ks == 1 && eval_halo(d, hp)) {
         YM_CHECK_ARG(halo_launch(hp, d, 0, x, w, y, nullptr, nullptr, nullptr, st, nullptr, &ev) == 0,
                      "ym_conv_fwd_eval: halo launch refused");
         YM_LAUNCH_CHECK("ym_conv_fwd_eval (halo)");
@@ -1146,6 +1375,12 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
     if (g_eval_cfg == 0) launch_gemm<128, 64, 2, 2, 32, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     else if (g_eval_cfg == 1) launch_gemm<128, 64, 2, 2, 64, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     else launch_gemm<128, 64, 2, 2, 64, 4, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
+    if (ks > 1) {
+        const int64_t threads = a.M * (d->cout / 8);
+        hipLaunchKernelGGL(eval_fold_kernel, dim3(unsigned((threads + 255) / 256)), dim3(256), 0, st, ev.part, ks, a.M,
+                           d->cout, uint32_t(d->oh) * uint32_t(d->ow), scale, shift, act, res, r_bs, r_ld, y, d->y_bs,
+                           d->y_ld);
+    }
     YM_LAUNCH_CHECK("ym_conv_fwd_eval");
     return YM_OK;
 }
@@ -1225,6 +1460,26 @@ extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t
     return YM_OK;
 }
 
+extern "C" int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, const float* scale, const float* shift,
+                                      int act, uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh,
+                                      int ow, int cout, int stride, int pad, void* stream) {
+    YM_CHECK_ARG(img && w_oihw && scale && shift && y, "ym_conv_first_fwd_eval: null argument");
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd_eval: cout=%d unsupported",
+                 cout);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+                 "ym_conv_first_fwd_eval: too many pixels");
+    YM_CHECK_ARG(y_ld % 8 == 0 && y_bs % 8 == 0 && y_ld >= cout && y_bs >= int64_t(oh) * ow * y_ld &&
+                     reinterpret_cast<uintptr_t>(y) % 16 == 0,
+                 "ym_conv_first_fwd_eval: output view not 16-byte aligned");
+    const int64_t threads = int64_t(n) * oh * ow * (cout / 8);
+    if (threads == 0) return YM_OK;
+    const int blocks = int(std::min<int64_t>((threads + 255) / 256, 4096));
+    hipLaunchKernelGGL(conv_first_eval_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, scale,
+                       shift, act, y, y_bs, y_ld, n, h, w, oh, ow, cout, stride, pad);
+    YM_LAUNCH_CHECK("ym_conv_first_fwd_eval");
+    return YM_OK;
+}
+
 extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
     return size_t(PARTIAL_BLOCKS) * size_t(cout > 0 ? cout : 0) * 9 * sizeof(float);
 }
@@ -1286,9 +1541,16 @@ extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
 
 extern "C" int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream) {
     if (total_elems == 0) return YM_OK;
-    hipLaunchKernelGGL(prep_weights_kernel, dim3(unsigned((total_elems + PREP_CHUNK - 1) / PREP_CHUNK), 2), dim3(256), 0,
-                       as_stream(stream),
-                       table_dev, n_entries, total_elems);
+    hipLaunchKernelGGL(prep_weights_kernel<false>, dim3(unsigned((total_elems + PREP_CHUNK - 1) / PREP_CHUNK), 2),
+                       dim3(256), 0, as_stream(stream), table_dev, n_entries, total_elems);
     YM_LAUNCH_CHECK("ym_prep_weights");
+    return YM_OK;
+}
+
+extern "C" int ym_prep_weights_fwd(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream) {
+    if (total_elems == 0) return YM_OK;
+    hipLaunchKernelGGL(prep_weights_kernel<true>, dim3(unsigned((total_elems + PREP_CHUNK - 1) / PREP_CHUNK)), dim3(256),
+                       0, as_stream(stream), table_dev, n_entries, total_elems);
+    YM_LAUNCH_CHECK("ym_prep_weights_fwd");
     return YM_OK;
 }

@@ -74,6 +74,7 @@ SIGNATURES = {
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_fwd_eval": (R, [P, P, P, P, INT, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_stem_bwd_wgrad_workspace_size": (SZ, [INT]),
     "ym_stem_bwd_wgrad_stored": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
@@ -82,13 +83,18 @@ SIGNATURES = {
     "ym_dw3x3_bwd_workspace_size": (SZ, [INT]),
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),
+    "ym_prep_weights_fwd": (R, [P, INT, I64, P]),
     "ym_bn_workspace_size": (SZ, [INT]),
     "ym_conv_fwd_bn_fused": (R, [P]),
     "ym_conv_fwd_bn": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_set_fold": (R, [INT]),
     "ym_conv_fwd_eval_ok": (R, [P]),
     "ym_conv_set_eval_cfg": (R, [INT]),
-    "ym_conv_fwd_eval": (R, [P, P, P, P, P, INT, P, I64, I64, P, P]),
+    "ym_conv_fwd_eval_workspace_size": (SZ, [P]),
+    "ym_conv_set_eval_split": (R, [INT]),
+    "ym_conv_set_eval_split_nk": (R, [INT]),
+    "ym_conv_set_eval_gemm_tiles": (R, [INT]),
+    "ym_conv_fwd_eval": (R, [P, P, P, P, P, INT, P, I64, I64, P, P, SZ, P]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
     "ym_bn_eval_coeff": (R, [INT, P, P, P, P, F32, P, P, P]),
     "ym_bn_eval_coeff_batch": (R, [P, INT, P]),
@@ -154,7 +160,10 @@ def lib():
             raise YolomiError(f"libyolomi not built: {LIB_PATH} missing (run `make -C yolo-scratch_amd/csrc`)")
         L = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
+            # a library named by YOLOMI_LIB (an earlier build, for A/B runs) may predate later entry points
+            fn = getattr(L, name, None) if "YOLOMI_LIB" in os.environ else getattr(L, name)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _LIB = L

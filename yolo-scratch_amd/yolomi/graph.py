@@ -157,7 +157,10 @@ class WeightStore:
             self.table_dev = raw.to(self.plan.dev)
             self.total = off
             self.key = key
-        call("ym_prep_weights", self.table_dev.data_ptr(), len(self.items), self.total, st)
+        # no transposed copy in the table (an eval plan): the forward-only launch
+        fwd_only = all(t is None for _, _, t, _ in self.items)
+        call("ym_prep_weights_fwd" if fwd_only else "ym_prep_weights", self.table_dev.data_ptr(), len(self.items),
+             self.total, st)
 
 
 # ----------------------------------------------------------------------------- ops
@@ -318,9 +321,13 @@ class ConvBN:
                 d.y_bs, d.y_ld, d.out_f32, d.accumulate = self.y.bs, self.y.ld, 2, 0
                 if lib().ym_conv_fwd_eval_ok(ctypes.byref(d)):
                     (sc, sh, _, _), _, _, _ = self._static_args(plan)
+                    # the small-grid K-split's fp32 slices: this op's own buffer (ops of a plan may run on side streams)
+                    nws = lib().ym_conv_fwd_eval_workspace_size(ctypes.byref(d))
+                    self._evws = torch.empty(nws, dtype=torch.uint8, device=plan.dev) if nws else None
                     args = (d, ctypes.byref(d), self.x.ptr(), self.wf.data_ptr(), sc, sh, self.act,
                             r.ptr() if r is not None else None, r.bs if r is not None else 0,
-                            r.ld if r is not None else 0, self.y.ptr())
+                            r.ld if r is not None else 0, self.y.ptr(),
+                            self._evws.data_ptr() if nws else None, nws)
             f = self._evf = (on, args)
         return f[1]
 
@@ -437,6 +444,18 @@ class StemConvBN(ConvBN):
         return (plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1)
 
     def forward(self, plan, st):
+        y = self.y
+        if (not plan.training and os.environ.get("YM_EVAL_FUSE", "1") != "0" and y.ptr() % 16 == 0 and y.ld % 8 == 0
+                and y.bs % 8 == 0):
+            # eval: conv + running-statistics BatchNorm + SiLU in one launch (ym_conv_first_fwd_eval)
+            bn = self.m.bn
+            (sc, sh, _, _), _, _, _ = self._static_args(plan)
+            if not plan.eval_coeff_batched:
+                call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
+                     _p(bn.running_var), float(bn.eps), sc, sh, st)
+            call("ym_conv_first_fwd_eval", plan.img.data_ptr(), _p(self.m.conv.weight), sc, sh, self.act, y.ptr(),
+                 y.bs, y.ld, plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, st)
+            return
         ss, sq = self.ps[0], self.ps[1]
         call("ym_conv_first_fwd", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(), ss.data_ptr(),
              sq.data_ptr(), plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
