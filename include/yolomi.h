@@ -70,6 +70,12 @@ int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C, int64_t ro
                   float conf, float iou_thr, float img_size, void* workspace, size_t workspace_bytes,
                   int32_t* out_count, float* out_boxes, float* out_scores, int64_t* out_labels,
                   int64_t* out_index, void* stream);
+/* The same with a row's elements `col_stride` apart (1: ym_decode_nms): the anchor-major view pred.transpose(1, 2)
+ * of the (B, 4+C, A) eval output is read in place (row_stride 1, col_stride A), no contiguous copy. */
+int ym_decode_nms_strided(const float* pred, int64_t B, int64_t N, int64_t C, int64_t row_stride,
+                          int64_t img_stride, int64_t col_stride, float conf, float iou_thr, float img_size,
+                          void* workspace, size_t workspace_bytes, int32_t* out_count, float* out_boxes,
+                          float* out_scores, int64_t* out_labels, int64_t* out_index, void* stream);
 
 /* nms_simple (train_yolo11_cuda.py:361-399) on one set of n xyxy boxes:
  * keep[0..*count) are indices into boxes in kept (score-descending) order. */
@@ -214,6 +220,12 @@ int ym_stem_bwd_wgrad_stored(const uint16_t* dy, int64_t d_bs, int64_t d_ld, con
  * channel (c / gsz) * gstride + goff + c % gsz of the x view. */
 int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c, int blocks, void* stream);
+/* Eval-mode form in one launch: + BatchNorm with the running-statistics scale / shift, SiLU if act, + the fp16
+ * residual view res (NULL: none; strides multiples of 4) into the fp16 y view (strides multiples of 8, 16-B aligned) —
+ * ym_dw3x3_fwd + ym_bn_apply without the statistics, the z round trip and the apply launch. */
+int ym_dw3x3_fwd_eval(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
+                      const float* scale, const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld,
+                      uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int wd, int c, void* stream);
 size_t ym_dw3x3_bwd_workspace_size(int c);
 int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, const float* w,
                  const uint16_t* dz, uint16_t* dx, int64_t dx_bs, int64_t dx_ld, float* dw, int n, int h, int wd,

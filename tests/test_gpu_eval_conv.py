@@ -111,6 +111,14 @@ def test_conv_fwd_eval_split_policy():
     M x Cout; none with the setter at 0 or on a large grid."""
     from yolomi._lib import lib
     L = lib()
+    prev_cfg, prev_split, prev_nk = L.ym_conv_set_eval_cfg(-1), L.ym_conv_set_eval_split(-1), L.ym_conv_set_eval_split_nk(-1)
+    try:
+        _split_policy_defaults(L)
+    finally:
+        L.ym_conv_set_eval_cfg(prev_cfg), L.ym_conv_set_eval_split(prev_split), L.ym_conv_set_eval_split_nk(prev_nk)
+
+
+def _split_policy_defaults(L):
     d, _, _ = _desc(1, 20, 20, 256, 256, 3, 2, 256)            # 100 px x 256: 4 tiles, 36 stages -> 9 slices
     assert L.ym_conv_fwd_eval_workspace_size(ctypes.byref(d)) == 9 * 100 * 256 * 4
     d, _, _ = _desc(1, 80, 80, 128, 64, 3, 1, 64)              # 50 tiles, 18 stages -> 4 slices
@@ -188,4 +196,42 @@ def test_conv_first_fwd_eval_vs_torch(n, h, w, cout, act):
     out = buf.float().cpu()
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"
     err, mag = float((out[..., 8:8 + cout] - ref).abs().max()), float(ref.abs().max())
+    assert err <= 2e-3 * mag + 1e-3, f"max |diff| {err:.3e} vs max |ref| {mag:.3e}"
+
+
+@pytest.mark.parametrize("n,h,w,heads,kd,hd,act,with_res", [(1, 20, 20, 4, 16, 32, 0, True), (2, 7, 9, 2, 8, 16, 1, False)])
+def test_dw3x3_fwd_eval_vs_torch(n, h, w, heads, kd, hd, act, with_res):
+    """ym_dw3x3_fwd_eval — Attention.pe (depthwise 3x3 on the v channels of qkv, channel map (c / hd) * (2kd + hd) + 2kd
+    + c % hd) with the eval BatchNorm (+ SiLU) and + a residual view in one launch, vs torch fp32 (fp16 output rounding).
+    The output and residual are channel slices of wider buffers."""
+    from yolomi._lib import call, stream_ptr
+    C, S = heads * hd, heads * (2 * kd + hd)
+    g = torch.Generator().manual_seed(n * 100 + h + C)
+    qkv = torch.randn(n, h, w, S, generator=g).half()
+    wt = torch.randn(C, 1, 3, 3, generator=g) / 3
+    scale = torch.rand(C, generator=g) + 0.5
+    shift = torch.randn(C, generator=g) * 0.2
+    res = torch.randn(n, h, w, C, generator=g).half() if with_res else None
+    idx = torch.tensor([(c // hd) * (2 * kd + hd) + 2 * kd + c % hd for c in range(C)])
+    v = qkv.float()[..., idx].permute(0, 3, 1, 2)
+    ref = F.conv2d(v, wt, padding=1, groups=C).permute(0, 2, 3, 1) * scale + shift
+    if act:
+        ref = F.silu(ref)
+    if res is not None:
+        ref = ref + res.float()
+    dev = torch.device("cuda")
+    ld, rld = C + 16, C + 8
+    buf = torch.full((n, h, w, ld), 7.0, dtype=torch.float16, device=dev)
+    rbuf = torch.zeros(n, h, w, rld, dtype=torch.float16, device=dev)
+    if res is not None:
+        rbuf[..., 4:4 + C] = res.to(dev)
+    qd, wd, scd, shd = qkv.to(dev), wt.reshape(C, 9).contiguous().to(dev), scale.to(dev), shift.to(dev)
+    torch.cuda.synchronize()
+    call("ym_dw3x3_fwd_eval", qd.data_ptr(), h * w * S, S, hd, 2 * kd + hd, 2 * kd, wd.data_ptr(), scd.data_ptr(),
+         shd.data_ptr(), act, rbuf[..., 4:].data_ptr() if res is not None else None, h * w * rld, rld,
+         buf[..., 8:].data_ptr(), h * w * ld, ld, n, h, w, C, stream_ptr(dev))
+    torch.cuda.synchronize()
+    out = buf.float().cpu()
+    assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + C:] == 7.0), "channels outside the view written"
+    err, mag = float((out[..., 8:8 + C] - ref).abs().max()), float(ref.abs().max())
     assert err <= 2e-3 * mag + 1e-3, f"max |diff| {err:.3e} vs max |ref| {mag:.3e}"

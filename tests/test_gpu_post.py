@@ -37,6 +37,23 @@ def test_decode_nms_bitexact(golden, kind):
     np.testing.assert_array_equal(torch.cat([o["labels"] for o in out]).cpu().numpy(), d[f"{kind}_labels"])
 
 
+@pytest.mark.parametrize("seed,B,N", [(5, 1, 8400), (6, 8, 8400), (7, 3, 17)])
+def test_decode_nms_strided_view_vs_oracle(seed, B, N):
+    """The anchor-major VIEW of a (B, 4+nc, A) tensor (what the eval loop passes: y.transpose(1, 2)) decodes in place
+    (ym_decode_nms_strided, elements A apart) to the oracle's result on the same rows, bit-exact."""
+    import train_yolo11_cuda as T
+    from datasets.synthetic import synth_eval_preds
+    pred = synth_eval_preds(B, N, seed=seed)
+    ref = op.decode(pred.numpy(), 640, 0.25, 0.45)
+    view = pred.cuda().transpose(1, 2).contiguous().transpose(1, 2)
+    assert view.stride(-1) == N
+    out = T.decode_predictions_for_metrics(view, 640, 0.25, 0.45, torch.device("cuda"))
+    for (rb, rs, rl), o in zip(ref, out):
+        np.testing.assert_array_equal(o["scores"].cpu().numpy(), rs)
+        np.testing.assert_array_equal(o["boxes"].cpu().numpy(), rb)
+        np.testing.assert_array_equal(o["labels"].cpu().numpy(), rl)
+
+
 @pytest.mark.parametrize("seed,B,N", [(1, 4, 8400), (2, 128, 8400), (3, 2, 33600), (4, 3, 17)])
 def test_decode_nms_vs_oracle_random(seed, B, N):
     """Fresh synthetic inputs (incl. the 1280² anchor count) against the C oracle."""

@@ -93,7 +93,10 @@ def main():
             def e2e():
                 y, _ = model(img)
                 return T.decode_predictions_for_metrics(y.transpose(1, 2), 640, 0.25, 0.45, dev)
-            e2e()
+            # warm-up: the eval plan runs eagerly once, is captured as a HIP graph on its second call and replays from
+            # the third on (yolomi.graph Plan._replay) — the one-time capture stays outside the timed batches
+            for _ in range(3):
+                e2e()
             _, wall_ms, e2e_gpu_ms = timed(e2e, args.reps, st)
             pred = synth_eval_preds(B, 8400, seed=7 + B)
             pd = pred.to(dev)

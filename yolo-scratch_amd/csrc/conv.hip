@@ -717,6 +717,65 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
     }
 }
 
+// eval-mode depthwise Conv block in one launch (ym_dw3x3_fwd_eval, Attention.pe in eval mode): the same per-(pixel,
+// 8 channels) depthwise conv, then the running-statistics BatchNorm (+ SiLU if act) and + the fp16 residual view in
+// fp32, one fp16 rounding (ym_bn_apply's arithmetic on the fp32 sum), one 16-B store into the y view (a.y_bs / a.y_ld)
+__global__ void __launch_bounds__(256) dw3x3_fwd_eval_kernel(DwArgs a, const float* __restrict__ sc,
+                                                             const float* __restrict__ sh, int act,
+                                                             const uint16_t* __restrict__ res, int64_t r_bs,
+                                                             int64_t r_ld) {
+    const int G = a.C >> 3, g = threadIdx.x % G;
+    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    float wr[8][9], s8[8], h8[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wr[r][t] = a.w[(c0 + r) * 9 + t];
+        s8[r] = sc[c0 + r];
+        h8[r] = sh[c0 + r];
+    }
+    const int HW = a.H * a.W, M = a.N * HW;
+    const int step = gridDim.x * (256 / G);
+    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+        const int n = m / HW, pix = m - n * HW, h = pix / a.W, wc = pix - h * a.W;
+        float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = h - 1 + kh, iw = wc - 1 + kw;
+                if (unsigned(ih) < unsigned(a.H) && unsigned(iw) < unsigned(a.W)) {
+                    float xv[8];
+                    unpack8(*reinterpret_cast<const uint4*>(a.x + n * a.x_bs + int64_t(ih * a.W + iw) * a.x_ld + sc0),
+                            xv, true);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) s[r] += wr[r][kh * 3 + kw] * xv[r];
+                }
+            }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const float t = fmaf(s[r], s8[r], h8[r]);
+            s[r] = act ? silu_f(t) : t;
+        }
+        if (res) {                                               // 8-B aligned residual rows
+            const uint2* rp = reinterpret_cast<const uint2*>(res + int64_t(n) * r_bs + int64_t(pix) * r_ld + c0);
+            const uint2 r0 = rp[0], r1 = rp[1];
+            const uint32_t rw[4] = {r0.x, r0.y, r1.x, r1.y};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                s[2 * k] += h2f(uint16_t(rw[k] & 0xffff));
+                s[2 * k + 1] += h2f(uint16_t(rw[k] >> 16));
+            }
+        }
+        uint4 o;
+        o.x = pk2h(s[0], s[1]);
+        o.y = pk2h(s[2], s[3]);
+        o.z = pk2h(s[4], s[5]);
+        o.w = pk2h(s[6], s[7]);
+        *reinterpret_cast<uint4*>(a.y + int64_t(n) * a.y_bs + int64_t(pix) * a.y_ld + c0) = o;
+    }
+}
+
 // dx (mapped channels, overwrite or accumulate into the view) and dW (+=) from dense dz (N,H,W,C)
 __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* __restrict__ dz, float* __restrict__ part,
                                                         int accumulate) {
@@ -1243,7 +1302,7 @@ extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const ui
 // it); the halo kernel's eval instance is its 4-wave C4 tile (C8 spills).
 // the eval GEMM's K stage x ring (ym_conv_set_eval_cfg): 0: 32-deep stages, 3-stage ring (the training 128x64 tile's),
 // 1: 64-deep x 3, 2: 64-deep x 4 — at bs 1 a launch covers a few tiles and walks its whole K serially, so deeper
-// stages halve its DMA round trips
+// stages halve its DMA round trips (128-deep x 3, one workgroup per CU, measured slower: profiles/r05/eval_split_ab.txt)
 static int g_eval_cfg = 1;
 
 extern "C" int ym_conv_set_eval_cfg(int cfg) {
@@ -1516,6 +1575,25 @@ extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
     DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
     hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
     YM_LAUNCH_CHECK("ym_dw3x3_fwd");
+    return YM_OK;
+}
+
+extern "C" int ym_dw3x3_fwd_eval(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
+                                 const float* w, const float* scale, const float* shift, int act, const uint16_t* res,
+                                 int64_t r_bs, int64_t r_ld, uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h,
+                                 int wd, int c, void* stream) {
+    YM_CHECK_ARG(x && w && scale && shift && y, "ym_dw3x3_fwd_eval: null argument");
+    YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
+                 "ym_dw3x3_fwd_eval: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+    YM_CHECK_ARG(y_bs % 8 == 0 && y_ld % 8 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0 &&
+                     (!res || (r_bs % 4 == 0 && r_ld % 4 == 0 && reinterpret_cast<uintptr_t>(res) % 8 == 0)),
+                 "ym_dw3x3_fwd_eval: output / residual view alignment");
+    const int64_t threads = int64_t(n) * h * wd * (c / 8);
+    if (threads == 0) return YM_OK;
+    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, y_bs, y_ld, n, h, wd, c};
+    hipLaunchKernelGGL(dw3x3_fwd_eval_kernel, dim3(unsigned(std::min<int64_t>((threads + 255) / 256, 4096))), dim3(256),
+                       0, as_stream(stream), a, scale, shift, act, res, r_bs, r_ld);
+    YM_LAUNCH_CHECK("ym_dw3x3_fwd_eval");
     return YM_OK;
 }
 

@@ -111,20 +111,21 @@ __device__ __forceinline__ uint32_t desc_bits(float s) {
 }
 
 // ---------------------------------------------------------------- stage 1
-// thread per row (C small) — max/argmax with the first maximal index winning
+// thread per row (C small) — max/argmax with the first maximal index winning; cs: the stride between a row's
+// elements (1: row-major rows; A: the anchor-major view of the (B, 4+nc, A) eval output, read coalesced across rows)
 __global__ void rowmax_thread_kernel(const float* __restrict__ pred, int64_t B, int64_t N, int64_t C,
-                                     int64_t rs, int64_t is, float conf, Ws w) {
+                                     int64_t rs, int64_t is, int64_t cs, float conf, Ws w) {
     int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= B * N) return;
     int64_t b = i / N, n = i - b * N;
     const float* r = pred + b * is + n * rs;
-    float mx = r[4];
+    float mx = r[4 * cs];
     int lab = 0;
     for (int64_t c = 1; c < C; ++c) {
-        float v = r[4 + c];
+        float v = r[(4 + c) * cs];
         if (v > mx) { mx = v; lab = int(c); }
     }
-    float x = r[0], y = r[1], hw = r[2] / 2.0f, hh = r[3] / 2.0f;
+    float x = r[0], y = r[cs], hw = r[2 * cs] / 2.0f, hh = r[3 * cs] / 2.0f;
     w.box[i] = make_float4(x - hw, y - hh, x + hw, y + hh);
     w.score[i] = mx;
     w.label[i] = lab;
@@ -133,7 +134,7 @@ __global__ void rowmax_thread_kernel(const float* __restrict__ pred, int64_t B, 
 
 // wave per row (C large, e.g. the literal (B, 4+nc, A) eval layout)
 __global__ void rowmax_wave_kernel(const float* __restrict__ pred, int64_t B, int64_t N, int64_t C,
-                                   int64_t rs, int64_t is, float conf, Ws w) {
+                                   int64_t rs, int64_t is, int64_t cs, float conf, Ws w) {
     int64_t i = int64_t(blockIdx.x) * (blockDim.x / 64) + threadIdx.x / 64;
     int lane = threadIdx.x & 63;
     if (i >= B * N) return;
@@ -142,7 +143,7 @@ __global__ void rowmax_wave_kernel(const float* __restrict__ pred, int64_t B, in
     float mx = -INFINITY;
     int64_t lab = INT64_MAX;
     for (int64_t c = lane; c < C; c += 64) {
-        float v = r[4 + c];
+        float v = r[(4 + c) * cs];
         if (v > mx || (v == mx && c < lab)) { mx = v; lab = c; }
     }
 #pragma unroll
@@ -152,7 +153,7 @@ __global__ void rowmax_wave_kernel(const float* __restrict__ pred, int64_t B, in
         if (om > mx || (om == mx && ol < lab)) { mx = om; lab = ol; }
     }
     if (lane == 0) {
-        float x = r[0], y = r[1], hw = r[2] / 2.0f, hh = r[3] / 2.0f;
+        float x = r[0], y = r[cs], hw = r[2 * cs] / 2.0f, hh = r[3 * cs] / 2.0f;
         w.box[i] = make_float4(x - hw, y - hh, x + hw, y + hh);
         w.score[i] = mx;
         w.label[i] = int32_t(lab);
@@ -692,13 +693,13 @@ extern "C" int ym_iou_row(const float* box1, const float* boxes2, int64_t m, flo
     return YM_OK;
 }
 
-extern "C" int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C, int64_t row_stride,
-                             int64_t img_stride, float conf, float iou_thr, float img_size, void* workspace,
-                             size_t workspace_bytes, int32_t* out_count, float* out_boxes, float* out_scores,
-                             int64_t* out_labels, int64_t* out_index, void* stream) {
+extern "C" int ym_decode_nms_strided(const float* pred, int64_t B, int64_t N, int64_t C, int64_t row_stride,
+                                     int64_t img_stride, int64_t col_stride, float conf, float iou_thr, float img_size,
+                                     void* workspace, size_t workspace_bytes, int32_t* out_count, float* out_boxes,
+                                     float* out_scores, int64_t* out_labels, int64_t* out_index, void* stream) {
     YM_CHECK_ARG(B >= 0 && N >= 0 && C >= 1, "ym_decode_nms: bad shape B=%lld N=%lld C=%lld", (long long)B,
                  (long long)N, (long long)C);
-    YM_CHECK_ARG(row_stride >= 4 + C, "ym_decode_nms: row_stride < 4+C");
+    YM_CHECK_ARG(col_stride >= 1 && (col_stride > 1 || row_stride >= 4 + C), "ym_decode_nms: row_stride < 4+C");
     YM_CHECK_ARG(N < (int64_t(1) << 30), "ym_decode_nms: N too large");
     if (B == 0) return YM_OK;
     hipStream_t st = as_stream(stream);
@@ -708,12 +709,20 @@ extern "C" int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C,
     Ws w = carve(workspace, B, N);
     if (C <= 64)
         hipLaunchKernelGGL(rowmax_thread_kernel, dim3(unsigned((B * N + 255) / 256)), dim3(256), 0, st, pred, B, N,
-                           C, row_stride, img_stride, conf, w);
+                           C, row_stride, img_stride, col_stride, conf, w);
     else
         hipLaunchKernelGGL(rowmax_wave_kernel, dim3(unsigned((B * N + 3) / 4)), dim3(256), 0, st, pred, B, N, C,
-                           row_stride, img_stride, conf, w);
+                           row_stride, img_stride, col_stride, conf, w);
     YM_LAUNCH_CHECK("rowmax");
     return launch_nms(B, N, iou_thr, img_size, 1, w, out_count, out_boxes, out_scores, out_labels, out_index, st);
+}
+
+extern "C" int ym_decode_nms(const float* pred, int64_t B, int64_t N, int64_t C, int64_t row_stride,
+                             int64_t img_stride, float conf, float iou_thr, float img_size, void* workspace,
+                             size_t workspace_bytes, int32_t* out_count, float* out_boxes, float* out_scores,
+                             int64_t* out_labels, int64_t* out_index, void* stream) {
+    return ym_decode_nms_strided(pred, B, N, C, row_stride, img_stride, 1, conf, iou_thr, img_size, workspace,
+                                 workspace_bytes, out_count, out_boxes, out_scores, out_labels, out_index, stream);
 }
 
 extern "C" int ym_nms(const float* boxes, const float* scores, int64_t n, float iou_thr, void* workspace,

@@ -59,6 +59,7 @@ SIGNATURES = {
     "ym_iou_row": (R, [P, P, I64, P, P]),
     "ym_nms_workspace_size": (SZ, [I64, I64]),
     "ym_decode_nms": (R, [P, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
+    "ym_decode_nms_strided": (R, [P, I64, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
     "ym_nms": (R, [P, P, I64, F32, P, SZ, P, P, P]),
     "ym_conv_stat_blocks": (R, [I64, INT]),
     "ym_conv_fwd_stat_rows": (R, [P]),
@@ -80,6 +81,8 @@ SIGNATURES = {
     "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
     "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
+    "ym_dw3x3_fwd_eval": (R, [P, I64, I64, INT, INT, INT, P, P, P, INT, P, I64, I64, P, I64, I64, INT, INT, INT, INT,
+                              P]),
     "ym_dw3x3_bwd_workspace_size": (SZ, [INT]),
     "ym_dw3x3_bwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, I64, I64, P, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_prep_weights": (R, [P, INT, I64, P]),

@@ -514,8 +514,21 @@ class DWConvBN(ConvBN):
         self.coef = torch.empty(3, C, dtype=F32, device=plan.dev)
 
     def forward(self, plan, st):
-        ss, sq = self.ps[0], self.ps[1]
         gsz, gstr, goff = self.map
+        y, r = self.y, self.res
+        if (not plan.training and os.environ.get("YM_EVAL_FUSE", "1") != "0" and y.ptr() % 16 == 0 and y.ld % 8 == 0
+                and y.bs % 8 == 0 and (r is None or (r.ptr() % 8 == 0 and r.ld % 4 == 0 and r.bs % 4 == 0))):
+            # eval: depthwise conv + running-statistics BatchNorm + the residual in one launch (ym_dw3x3_fwd_eval)
+            bn = self.m.bn
+            (sc, sh, _, _), _, _, _ = self._static_args(plan)
+            if not plan.eval_coeff_batched:
+                call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
+                     _p(bn.running_var), float(bn.eps), sc, sh, st)
+            call("ym_dw3x3_fwd_eval", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight), sc,
+                 sh, self.act, r.ptr() if r is not None else None, r.bs if r is not None else 0,
+                 r.ld if r is not None else 0, y.ptr(), y.bs, y.ld, plan.B, y.H, y.W, self.C, st)
+            return
+        ss, sq = self.ps[0], self.ps[1]
         call("ym_dw3x3_fwd", self.x.ptr(), self.x.bs, self.x.ld, gsz, gstr, goff, _p(self.m.conv.weight),
              self.z.data_ptr(), ss.data_ptr(), sq.data_ptr(), plan.B, self.y.H, self.y.W, self.C, self.G, st)
         self._bn_fwd(plan, st, ss, sq)
@@ -1282,26 +1295,32 @@ def _attention(plan, m, x: View, out: View, res: View):
 
 def _psa(plan, m, x: View, out=None):
     c = m.c
-    y = _conv(plan, m.cv1, x)                      # [a | b]
-    a, b = y.sub(0, c), y.sub(c, c)
     cat = plan.act(2 * c, x.H, x.W)
+    # eval plans: cv1 writes [a | b] straight into the concat and b3 overwrites b there (b is dead once the attention's
+    # qkv conv and its residual have read it; the scheduler orders that write after those reads) — no copy of a.
+    # Training keeps b: the backward reads it (the qkv conv's weight gradient)
+    y = _conv(plan, m.cv1, x, None if plan.training else cat)      # [a | b]
+    a, b = y.sub(0, c), y.sub(c, c)
     b2 = plan.act(c, x.H, x.W)
     _attention(plan, m.attn, b, b2, res=b)         # b2 = b + attn(b)
     f1 = _conv(plan, m.ffn[0], b2)
     _conv(plan, m.ffn[1], f1, cat.sub(c, c), res=b2, act=False)   # b3 = b2 + ffn(b2)
-    plan.ops.append(Copy(plan, a, cat.sub(0, c)))
+    if plan.training:
+        plan.ops.append(Copy(plan, a, cat.sub(0, c)))
     return _conv(plan, m.cv2, cat, out)
 
 
 def _c2psa(plan, m, x: View, out=None):
     c = m.c
-    y = _conv(plan, m.cv1, x)
-    a, b = y.sub(0, c), y.sub(c, c)
     cat = plan.act(2 * c, x.H, x.W)
+    # eval plans: as in _psa, cv1's [a | b] lands in the concat and the last PSA block's output overwrites b there
+    y = _conv(plan, m.cv1, x, None if plan.training else cat)
+    a, b = y.sub(0, c), y.sub(c, c)
     blocks = list(m.m)
     for j, blk in enumerate(blocks):
         b = _psa(plan, blk, b, cat.sub(c, c) if j == len(blocks) - 1 else None)
-    plan.ops.append(Copy(plan, a, cat.sub(0, c)))
+    if plan.training:
+        plan.ops.append(Copy(plan, a, cat.sub(0, c)))
     return _conv(plan, m.cv2, cat, out)
 
 

@@ -42,19 +42,21 @@ def decode_nms(pred: torch.Tensor, img_size, conf: float, iou_thr: float):
     require_device(pred)
     from ._lib import lib
     p = pred.float()
-    if p.stride(-1) != 1:
+    if p.stride(-1) < 1:
         p = p.contiguous()
     B, N, W = p.shape
     C = W - 4
     dev = p.device
     ws_bytes = lib().ym_nms_workspace_size(B, max(N, 1))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+    cnt = torch.empty(B, dtype=torch.int32, device=dev)          # every count is written by the launch
     boxes = torch.empty(B, N, 4, dtype=torch.float32, device=dev)
     scores = torch.empty(B, N, dtype=torch.float32, device=dev)
     labels = torch.empty(B, N, dtype=torch.int64, device=dev)
     index = torch.empty(B, N, dtype=torch.int64, device=dev)
-    call("ym_decode_nms", ptr(p), B, N, C, p.stride(1), p.stride(0), float(conf), float(iou_thr), float(img_size),
-         ptr(ws), ws_bytes, ptr(cnt), ptr(boxes), ptr(scores), ptr(labels), ptr(index), stream_ptr(dev))
+    # a row's elements may be strided (the anchor-major view y.transpose(1, 2) of the eval output): read in place
+    call("ym_decode_nms_strided", ptr(p), B, N, C, p.stride(1), p.stride(0), p.stride(2), float(conf), float(iou_thr),
+         float(img_size), ptr(ws), ws_bytes, ptr(cnt), ptr(boxes), ptr(scores), ptr(labels), ptr(index),
+         stream_ptr(dev))
     counts = cnt.cpu().tolist()                      # the single host sync of the batch
     return [{"boxes": boxes[b, :k], "scores": scores[b, :k], "labels": labels[b, :k]} for b, k in enumerate(counts)]
