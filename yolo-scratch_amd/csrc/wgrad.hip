@@ -586,6 +586,9 @@ struct WgPlan {
     bool deep;         // wgrad3: two register sets (units t + 1, t + 2 in flight)
 };
 
+// workgroups per weight-gradient launch (ym_wgrad_set_target; the 512 of the stride-1 3x3 rule scales with it)
+int g_wg_target = 256;
+
 WgPlan wg_plan(const ym_conv_desc* d) {
     WgPlan p{};
     const int64_t M = int64_t(d->n) * d->oh * d->ow;
@@ -623,12 +626,12 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     // workgroups per launch: 256 measured best in the training step (2800 img/s vs 2767 at 512 and
     // 2725 at 1024): the weight gradients run on the side stream beside the data gradients, and
     // fewer, longer split-K blocks leave the main stream room and halve the partials to reduce
-    int64_t target = 256;
+    int64_t target = g_wg_target;
     // stride-1 3x3 layers with few units per channel tile (20x20 maps, 256-channel 40x40): 512 workgroups of
     // >= 6 units — the larger partials cost less than half the CUs idling (s@640 bs64, same-process A/B:
     // 128->128 20x20 34.7 -> 30.2 us, 256->128 40x40 84.8 -> 76.1 us; the stride-2 20x20 layers and
     // 128-channel 40x40 ones measured slower, so they keep 256)
-    if (p.kind == 3 && d->stride == 1 && p.units / cols < 256) { target = 512; min_units = 6; }
+    if (p.kind == 3 && d->stride == 1 && p.units / cols < 256) { target = 2 * g_wg_target; min_units = 6; }
     // the second register set pays where a split runs many units (maps >= 64 wide: 80x80 128->128
     // 152.8 -> 147.6 us); below that the extra VGPRs (120 -> 166: one workgroup per CU) cost as much
     p.deep = p.kind == 3 && d->ow >= 64;
@@ -641,6 +644,14 @@ WgPlan wg_plan(const ym_conv_desc* d) {
 }
 
 }  // namespace
+
+extern "C" int ym_wgrad_set_target(int wgs) {
+    // workgroups per weight-gradient launch the split-K plan aims for (default 256; <= 0 restores it); returns the
+    // previous setting
+    const int prev = g_wg_target;
+    g_wg_target = wgs <= 0 ? 256 : wgs;
+    return prev;
+}
 
 int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len) {
     const WgPlan p = wg_plan(d);

@@ -73,6 +73,7 @@ SIGNATURES = {
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
+    "ym_wgrad_set_target": (R, [INT]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
     "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_conv_first_fwd_eval": (R, [P, P, P, P, INT, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, P]),
