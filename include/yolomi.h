@@ -301,6 +301,9 @@ int ym_conv_set_eval_split(int max_tiles);
 /* The K-split's K-stage threshold (split layers of >= min_stages 64-deep stages; default 12; <0 restores it) and the
  * tile count at or below which an eval conv the halo kernel would take runs the 2-stage GEMM instead (default 0). */
 int ym_conv_set_eval_split_nk(int min_stages);
+/* Layers the pipelined implicit GEMM takes (>= 256 tiles: large maps / batches) run its eval instance (1, default;
+ * <0 restores it) or, with 0, are not eval-epilogue cases (ym_conv_fwd + ym_bn_apply). */
+int ym_conv_set_eval_pipe(int on);
 int ym_conv_set_eval_gemm_tiles(int max_tiles);
 int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
                      const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* y,

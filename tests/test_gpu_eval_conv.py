@@ -2,7 +2,8 @@
 shift -> SiLU -> + residual, yolo11_modules.py:21-47 in eval mode) — vs a PyTorch fp32 reference of the same op, and
 the eval forward of a whole model with it vs without it.
 
-Kernel cases: the halo-staged 3x3 kernel's C4 tile (20x20 / 10x10 maps, channel counts off the 32-channel chunk) and
+Kernel cases: the pipelined implicit GEMM's eval instance (>= 256 tiles), the halo-staged 3x3 kernel's C4 tile (20x20 /
+10x10 maps, channel counts off the 32-channel chunk) and
 the 2-stage implicit GEMM on 128x64 tiles (1x1, 3x3 stride 2, outputs narrower than the tile), each with the workspace
 (the small-grid K-split: fp32 slices + a fold launch, where the policy splits) and without it (one launch), with and
 without SiLU and a residual (its own strides at n > 1); the output is a
@@ -32,7 +33,10 @@ CASES = [
     (2, 20, 20, 64, 40, 1, 1),
     (1, 20, 20, 136, 64, 3, 1),       # K-split: 27 K stages in 6 slices, slices starting inside a tap
     (1, 10, 10, 1024, 64, 1, 1),      # K-split of a 1x1: 16 stages in 4 slices
+    (4, 128, 128, 64, 64, 1, 1),      # >= 256 tiles: the pipelined forward's eval instance (256 x 64 tile)
+    (4, 128, 128, 128, 128, 3, 1),    # ... its 256 x 128 tile
 ]
+PIPE_CASES = {(4, 128, 128, 64, 64, 1, 1), (4, 128, 128, 128, 128, 3, 1)}
 
 
 def _desc(n, h, w, cin, cout, k, s, ld):
@@ -55,6 +59,7 @@ def test_conv_fwd_eval_vs_torch(case, act, with_res, split):
     ld = cout + 24                                   # output / residual: channel slices of wider buffers
     d, oh, ow = _desc(n, h, w, cin, cout, k, s, ld)
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1, case
+    assert (lib().ym_conv_algo(ctypes.byref(d), 0) == 2) == (case in PIPE_CASES), case
     g = torch.Generator().manual_seed(hash((case, act, with_res)) & 0xFFFF)
     x = torch.randn(n, h, w, cin, generator=g).half()
     wt = (torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5).half()

@@ -1363,11 +1363,24 @@ static int eval_ks(const ym_conv_desc* d) {
     return ks >= 2 && M * (d->cout / 8) < (int64_t(1) << 31) ? int(ks) : 1;
 }
 
+// the pipelined forward's eval instance for layers of >= 256 tiles (ym_conv_set_eval_pipe; 0: those layers run
+// ym_conv_fwd + ym_bn_apply)
+static int g_eval_pipe = 1;
+
+extern "C" int ym_conv_set_eval_pipe(int on) {
+    // the pipelined forward's eval instance on (1, default; -1 restores it) or off (0); returns the previous setting
+    const int prev = g_eval_pipe;
+    g_eval_pipe = on < 0 ? 1 : (on ? 1 : 0);
+    return prev;
+}
+
 static bool eval_layout_ok(const ym_conv_desc* d) {
     if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return false;
     if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return false;
     if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return false;
-    return !(direct_plan(d, 0).ok || hpipe_plan(d, 0).ok || pipe_plan(d, 0).ok);   // no eval epilogue there
+    if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok) return false;   // no eval epilogue there
+    const PipePlan pp = pipe_plan(d, 0);
+    return !pp.ok || (g_eval_pipe && pipe_eval_ok(pp, d));          // the pipelined forward's eval instance
 }
 
 // the eval forward runs the halo kernel's eval instance (not the GEMM) for d
@@ -1377,6 +1390,7 @@ static bool eval_halo(const ym_conv_desc* d, const HaloPlan& hp) {
 
 extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
     if (!eval_layout_ok(d)) return 0;
+    if (pipe_plan(d, 0).ok) return 1;
     if (eval_ks(d) > 1 || (eval_tiles(d) <= g_eval_gemm_tiles && eval_gemm_fits(d))) return 1;
     const HaloPlan hp = halo_plan(d, 0);
     if (hp.ok) return hp.cfg == 1 ? 1 : 0;
@@ -1412,6 +1426,12 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
         ev.part = static_cast<float*>(workspace);
     }
     hipStream_t st = as_stream(stream);
+    const PipePlan pp = pipe_plan(d, 0);
+    if (pp.ok) {                                  // large maps (>= 256 tiles): the pipelined forward's eval instance
+        YM_CHECK_ARG(pipe_launch_eval(pp, d, x, w, y, ev, st) == 0, "ym_conv_fwd_eval: pipelined launch refused");
+        YM_LAUNCH_CHECK("ym_conv_fwd_eval (pipe)");
+        return YM_OK;
+    }
     const HaloPlan hp = halo_plan(d, 0);
     if (ks == 1 && eval_halo(d, hp)) {
         YM_CHECK_ARG(halo_launch(hp, d, 0, x, w, y, nullptr, nullptr, nullptr, st, nullptr, &ev) == 0,

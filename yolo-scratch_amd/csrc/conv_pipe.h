@@ -23,5 +23,10 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);
 // fold: the BatchNorm finalize as the launch's tail (ym_conv_fwd_bn; forward with statistics only) or null
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
                 const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold = nullptr);
+// the eval-mode Conv block instance (ym_conv_fwd_eval): d's forward with the running-statistics BatchNorm / SiLU /
+// residual e in the epilogue, into the fp16 y view (pipe_eval_ok: the plan's single-class forward); 0 on success
+bool pipe_eval_ok(const PipePlan& p, const ym_conv_desc* d);
+int pipe_launch_eval(const PipePlan& p, const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y,
+                     const EvalArgs& e, hipStream_t st);
 
 }  // namespace ym

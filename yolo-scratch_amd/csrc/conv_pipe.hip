@@ -342,8 +342,12 @@ struct Issuer {
 // fetched), 2 no MFMAs (fragments still read), 4 only the gathered input's DMAs out of range, 8 only the weights'
 // C1: one output class on maps of >= BM pixels (Issuer's fast path; the stride-2 data gradient's four classes and tiny
 // maps take the generic one)
-template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false>
-__global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) {
+// EV: the eval-mode Conv block instance (ym_conv_fwd_eval at large batches: running-statistics BatchNorm / SiLU /
+// residual in the register epilogue, conv_epi.h EvalEpi; a C1 forward without statistics; e is not read otherwise)
+template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false,
+          bool EV = false>
+__global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, EvalArgs e) {
+    static_assert(!EV || (C1 && MODE == PF && ABL == 0), "the eval instance is a single-class forward");
     // NS: LDS ring of K stages — stage g computing, g+1 .. g+NS-1 in flight (3; 2 for the 64-KB+ stages of the
     // 256-channel / 512-pixel tiles)
     static_assert(NS == 2 || NS == 3, "ring depth");
@@ -552,8 +556,22 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a) 
                 if constexpr (C1) return c_m0 + wc * (BM / WN) + qp < Mtot;
                 return m0 + wc * (BM / WN) + qp < cc.Mc;
             };
-            epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
-                                  a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
+            if constexpr (EV) {
+                const EvalEpi ee{e.sc, e.sh, e.act, make_rsrc(e.res, e.res ? e.res_bytes : 0), e.res != nullptr};
+                auto res_off = [&](int qp) -> uint32_t {     // pix_off's C1 pixel walk on the residual view's strides
+                    const int q = wc * (BM / WN) + qp;
+                    if (c_m0 + q >= Mtot) return OOB;
+                    uint32_t pix = c_tp + uint32_t(q);
+                    int n = c_tn;
+                    if (pix >= is.ohw) { pix -= is.ohw; ++n; }
+                    return uint32_t((int64_t(n) * e.r_bs + int64_t(pix) * e.r_ld + wch0) * 2);
+                };
+                epilogue_regs_x<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
+                                        &ee, res_off);
+            } else {
+                epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
+                                      a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
+            }
         }
     }
 
@@ -613,25 +631,32 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     const bool c1 = a.ncls == 1 && int64_t(a.OH) * a.OW >= kCfg[cfg].bm && g_pipe_exp != 20;
     if (cfg == 0 && g_pipe_exp >= 10 && g_pipe_exp < 20) {
         switch (g_pipe_exp) {
-            case 10: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 1, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
-            case 11: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 2, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
-            case 12: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 4, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
-            default: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 8, true><<<dim3(grid), dim3(1024), 0, st>>>(a); return;
+            case 10: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 1, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
+            case 11: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 2, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
+            case 12: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 4, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
+            default: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 8, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
         }
     }
     if (c1) {
         switch (cfg) {
-            case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(1024), 0, st>>>(a); break;
-            case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a); break;
-            default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+            case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
+            case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+            default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
         }
         return;
     }
     switch (cfg) {
-        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2><<<dim3(grid), dim3(1024), 0, st>>>(a); break;
-        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a); break;
-        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a); break;
+        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
+        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
     }
+}
+
+// the eval instance (EV): cfg 1 / 2 tiles on 8 waves (the 16-wave 256 x 128 tile's 127 VGPRs leave no room for the
+// eval epilogue at four waves per SIMD; cfg 0 runs as the 8-wave cfg 2)
+void launch_eval(int cfg, const PipeArgs& a, const EvalArgs& e, int grid, hipStream_t st) {
+    if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
+    else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
 }
 
 void launch_cfg(int mode, int cfg, const PipeArgs& a, int grid, hipStream_t st) {
@@ -728,6 +753,34 @@ int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint1
     if (!dgrad && st_sum) a.fold = bn_fold_args(fold);
     launch_cfg(dgrad ? PD : PF, p.cfg, a, p.grid, st);
     return YM_OK;
+}
+
+bool pipe_eval_ok(const PipePlan& p, const ym_conv_desc* d) {
+    // the eval instance is the single-class (C1) forward: maps of >= BM pixels, the shipped control path
+    return p.ok && int64_t(d->oh) * d->ow >= kCfg[p.cfg].bm && g_pipe_exp != 20 && d->out_f32 == 2 && !d->accumulate;
+}
+
+int pipe_launch_eval(const PipePlan& p, const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, uint16_t* y,
+                     const EvalArgs& e, hipStream_t st) {
+    if (!pipe_eval_ok(p, d)) return 1;
+    PipeArgs a{};
+    a.x = x; a.x_bs = d->x_bs; a.x_ld = d->x_ld;
+    a.y = y; a.y_bs = d->y_bs; a.y_ld = d->y_ld;
+    a.GH = d->h; a.GW = d->w; a.Kin = d->cin;
+    a.OH = d->oh; a.OW = d->ow; a.Nout = d->cout;
+    a.os = 1;
+    a.out_f32 = 2;
+    a.w = w;
+    a.KH = d->k; a.KW = d->k; a.stride = d->stride; a.pad = d->pad; a.N = d->n;
+    // cfg 0 runs as the 8-wave 256 x 128 instance (same tile, grid and rows)
+    const int cfg = p.cfg == 1 ? 1 : 2;
+    const int bm = kCfg[cfg].bm, bn = kCfg[cfg].bn;
+    a.ntiles = (a.Nout + bn - 1) / bn;
+    a.ncls = 1;
+    a.mt_pre[0] = 0;
+    a.mt_pre[1] = int((int64_t(a.N) * a.OH * a.OW + bm - 1) / bm);
+    launch_eval(cfg, a, e, p.grid, st);
+    return 0;
 }
 
 }  // namespace ym
