@@ -7,7 +7,7 @@ O=$GRAFT_REPO_ROOT/gpurun_out/r05_benchset
 rm -rf $O; mkdir -p $O
 cd $GRAFT_REPO_ROOT
 mapfile -t CFGS < "$1"
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
 for i in "${!CFGS[@]}"; do
   c="${CFGS[$i]}"; [ "$c" = "-" ] && c=""
   lib=""; envs=()

@@ -586,8 +586,11 @@ struct WgPlan {
     bool deep;         // wgrad3: two register sets (units t + 1, t + 2 in flight)
 };
 
-// workgroups per weight-gradient launch (ym_wgrad_set_target; the 512 of the stride-1 3x3 rule scales with it)
-int g_wg_target = 256;
+// workgroups per weight-gradient launch (ym_wgrad_set_target; the stride-1 3x3 rule's doubled target scales with it):
+// 160 since round 5 — in the step, 160 / 192 / 224 / 256 measured 3392 / 3389 / 3379 / 3384 img/s (three same-box
+// runs each, profiles/r05/wgrad_target_streams_ab.txt): the weight gradients share the GPU with the data gradients,
+// and fewer split-K blocks leave the other streams room and halve the partials to reduce
+int g_wg_target = 160;
 
 WgPlan wg_plan(const ym_conv_desc* d) {
     WgPlan p{};
@@ -623,12 +626,10 @@ WgPlan wg_plan(const ym_conv_desc* d) {
     // enough K units per workgroup to amortise writing its fp32 partial tile (64x64x9 floats for
     // 3x3: 147 KB, about the input an 8x8-pixel unit moves 12 times)
     int64_t min_units = p.kind == 3 ? 12 : 8;
-    // workgroups per launch: 256 measured best in the training step (2800 img/s vs 2767 at 512 and
-    // 2725 at 1024): the weight gradients run on the side stream beside the data gradients, and
-    // fewer, longer split-K blocks leave the main stream room and halve the partials to reduce
+    // workgroups per launch (g_wg_target above; round 1: 256 vs 512 / 1024 in the step)
     int64_t target = g_wg_target;
-    // stride-1 3x3 layers with few units per channel tile (20x20 maps, 256-channel 40x40): 512 workgroups of
-    // >= 6 units — the larger partials cost less than half the CUs idling (s@640 bs64, same-process A/B:
+    // stride-1 3x3 layers with few units per channel tile (20x20 maps, 256-channel 40x40): twice the target (512 when it
+    // was 256) in workgroups of >= 6 units — the larger partials cost less than half the CUs idling (s@640 bs64, same-process A/B:
     // 128->128 20x20 34.7 -> 30.2 us, 256->128 40x40 84.8 -> 76.1 us; the stride-2 20x20 layers and
     // 128-channel 40x40 ones measured slower, so they keep 256)
     if (p.kind == 3 && d->stride == 1 && p.units / cols < 256) { target = 2 * g_wg_target; min_units = 6; }
@@ -649,7 +650,7 @@ extern "C" int ym_wgrad_set_target(int wgs) {
     // workgroups per weight-gradient launch the split-K plan aims for (default 256; <= 0 restores it); returns the
     // previous setting
     const int prev = g_wg_target;
-    g_wg_target = wgs <= 0 ? 256 : wgs;
+    g_wg_target = wgs <= 0 ? 160 : wgs;
     return prev;
 }
 

@@ -995,6 +995,8 @@ class Plan:
 
     def _run(self, ops, phase, after=None):
         K = self._nstreams()
+        if phase == "fwd" and os.environ.get("YM_FWD_STREAMS"):
+            K = max(1, int(os.environ["YM_FWD_STREAMS"]))      # A/B runs: the forward's stream count alone
         self._alloc_bn_ws(K)
         if K == 1:
             st = stream_ptr(self.dev)
