@@ -304,6 +304,10 @@ int ym_conv_set_eval_split_nk(int min_stages);
 /* Layers the pipelined implicit GEMM takes (>= 256 tiles: large maps / batches) run its eval instance (1, default;
  * <0 restores it) or, with 0, are not eval-epilogue cases (ym_conv_fwd + ym_bn_apply). */
 int ym_conv_set_eval_pipe(int on);
+/* Layers whose training kernel has no eval instance, run through one anyway (bit mask; default 0; <0 restores it):
+ * bit 0 the halo kernel's 8-wave tile -> the 2-stage GEMM's eval instance, bit 1 the halo-pipelined 3x3 kernel ->
+ * the halo C4 / 2-stage GEMM eval instances.  Returns the previous setting. */
+int ym_conv_set_eval_route(int mask);
 int ym_conv_set_eval_gemm_tiles(int max_tiles);
 int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
                      const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* y,

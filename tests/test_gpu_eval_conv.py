@@ -96,9 +96,19 @@ def test_conv_fwd_eval_vs_torch(case, act, with_res, split):
 
 
 def test_conv_fwd_eval_ok_scope():
-    """Not eval-epilogue cases: a map the direct kernel takes, an accumulating or non-fp16 output."""
+    """Not eval-epilogue cases at the default routing: a layer the halo-pipelined kernel takes, an accumulating or
+    non-fp16 output."""
     from yolomi._lib import lib
-    d, _, _ = _desc(8, 160, 160, 64, 64, 3, 1, 64)              # >= 1 M output pixels: direct kernel
+    prev = lib().ym_conv_set_eval_route(-1)
+    try:
+        _ok_scope_default(lib())
+    finally:
+        lib().ym_conv_set_eval_route(prev)
+
+
+def _ok_scope_default(L):
+    lib = lambda: L                                             # noqa: E731
+    d, _, _ = _desc(8, 160, 160, 64, 64, 3, 1, 64)              # the halo-pipelined 3x3 kernel (no eval instance)
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 0
     d, _, _ = _desc(1, 20, 20, 64, 32, 1, 1, 32)                # 2-stage GEMM, 32 output channels (masked tile half)
     assert lib().ym_conv_fwd_eval_ok(ctypes.byref(d)) == 1

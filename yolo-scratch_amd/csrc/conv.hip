@@ -1374,11 +1374,24 @@ extern "C" int ym_conv_set_eval_pipe(int on) {
     return prev;
 }
 
+// layers whose training kernel has no eval instance, routed to an eval instance anyway (ym_conv_set_eval_route):
+// bit 0 the halo kernel's 8-wave tile (C8: its eval instance spills) -> the 2-stage GEMM's; bit 1 the halo-pipelined
+// 3x3 kernel -> the halo C4 / GEMM eval instances
+static int g_eval_route = 0;
+
+extern "C" int ym_conv_set_eval_route(int mask) {
+    // see g_eval_route (-1: default 0); returns the previous setting
+    const int prev = g_eval_route;
+    g_eval_route = mask < 0 ? 0 : (mask & 3);
+    return prev;
+}
+
 static bool eval_layout_ok(const ym_conv_desc* d) {
     if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return false;
     if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return false;
     if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return false;
-    if (direct_plan(d, 0).ok || hpipe_plan(d, 0).ok) return false;   // no eval epilogue there
+    if (direct_plan(d, 0).ok) return false;                          // no eval epilogue there
+    if (hpipe_plan(d, 0).ok && !((g_eval_route & 2) && eval_gemm_fits(d))) return false;
     const PipePlan pp = pipe_plan(d, 0);
     return !pp.ok || (g_eval_pipe && pipe_eval_ok(pp, d));          // the pipelined forward's eval instance
 }
@@ -1393,7 +1406,7 @@ extern "C" int ym_conv_fwd_eval_ok(const ym_conv_desc* d) {
     if (pipe_plan(d, 0).ok) return 1;
     if (eval_ks(d) > 1 || (eval_tiles(d) <= g_eval_gemm_tiles && eval_gemm_fits(d))) return 1;
     const HaloPlan hp = halo_plan(d, 0);
-    if (hp.ok) return hp.cfg == 1 ? 1 : 0;
+    if (hp.ok) return hp.cfg == 1 ? 1 : ((g_eval_route & 1) && eval_gemm_fits(d) ? 1 : 0);
     return eval_gemm_fits(d) ? 1 : 0;
 }
 

@@ -98,6 +98,7 @@ SIGNATURES = {
     "ym_conv_set_eval_split": (R, [INT]),
     "ym_conv_set_eval_split_nk": (R, [INT]),
     "ym_conv_set_eval_pipe": (R, [INT]),
+    "ym_conv_set_eval_route": (R, [INT]),
     "ym_conv_set_eval_gemm_tiles": (R, [INT]),
     "ym_conv_fwd_eval": (R, [P, P, P, P, P, INT, P, I64, I64, P, P, SZ, P]),
     "ym_bn_finalize": (R, [P, P, INT, INT, F64, P, P, P, P, P, F32, F32, P, P, P, P, P, P]),
