@@ -192,7 +192,7 @@ int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt,
  * `workspace` (ym_conv_wgrad_workspace_size bytes) and are reduced by the library: no atomics
  * into, and no zero-fill of, dw_oihw.  dz bf16 with the y_* view, x fp16 with the x_* view. */
 size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d);
-/* Workgroups per weight-gradient launch the split-K plan aims for (default 160, tuned in the training step where
+/* Workgroups per weight-gradient launch the split-K plan aims for (default 256, tuned in the training step where
  * the weight gradients share the GPU with the data gradients; <= 0 restores it).  Returns the previous setting.
  * Process-wide, like ym_conv_set_halo; a workspace size queried under one setting serves only that setting. */
 int ym_wgrad_set_target(int wgs);

@@ -586,11 +586,11 @@ struct WgPlan {
     bool deep;         // wgrad3: two register sets (units t + 1, t + 2 in flight)
 };
 
-// workgroups per weight-gradient launch (ym_wgrad_set_target; the stride-1 3x3 rule's doubled target scales with it):
-// 160 since round 5 — in the step, 160 / 192 / 224 / 256 measured 3392 / 3389 / 3379 / 3384 img/s (three same-box
-// runs each, profiles/r05/wgrad_target_streams_ab.txt): the weight gradients share the GPU with the data gradients,
-// and fewer split-K blocks leave the other streams room and halve the partials to reduce
-int g_wg_target = 160;
+// workgroups per weight-gradient launch (ym_wgrad_set_target; the stride-1 3x3 rule's doubled target scales with it).
+// Round 5: 160 measured +0.2 % img/s in the step (three same-box pairs, profiles/r05/wgrad_target_streams_ab.txt) but
+// each launch ran longer alone (the 3x3 family's single-stream roofline fraction 0.2107 -> 0.1974, wgrad 0.199 ->
+// 0.161, profiles/r05/at_589d336): kept at 256, the gain inside the run-to-run spread
+int g_wg_target = 256;
 
 WgPlan wg_plan(const ym_conv_desc* d) {
     WgPlan p{};
@@ -650,7 +650,7 @@ extern "C" int ym_wgrad_set_target(int wgs) {
     // workgroups per weight-gradient launch the split-K plan aims for (default 256; <= 0 restores it); returns the
     // previous setting
     const int prev = g_wg_target;
-    g_wg_target = wgs <= 0 ? 160 : wgs;
+    g_wg_target = wgs <= 0 ? 256 : wgs;
     return prev;
 }
 
