@@ -846,6 +846,12 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
 // crosses entries walks the table element by element.  (Round 3's one-element-per-thread kernel with a
 // binary search per element: 168 us per step on s@640.)
 constexpr int PREP_PER = 16, PREP_CHUNK = 256 * PREP_PER;
+// the forward-only launch (ym_prep_weights_fwd): smaller chunks — more workgroups in flight; round 5, s@640's table:
+// 16 / 8 elements per thread 32.8 / 27.1 us (the two-pass launch keeps 16: 8 measured 66.5 -> 72.4 us)
+#ifndef YM_PREP_PER_FWD
+#define YM_PREP_PER_FWD 8
+#endif
+constexpr int PREP_PER_FWD = YM_PREP_PER_FWD;
 constexpr int PREP_LDS = 8192;                               // floats of the transposed pass's tile
 
 __device__ __forceinline__ void prep_one(const ym_wprep_entry& t, int j, int pass) {
@@ -868,7 +874,8 @@ __device__ __forceinline__ void prep_one(const ym_wprep_entry& t, int j, int pas
 template <bool FWD_ONLY>
 __global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry* __restrict__ tab, int n_entries,
                                                            int64_t total) {
-    const int64_t c0 = int64_t(blockIdx.x) * PREP_CHUNK, c1 = min(c0 + PREP_CHUNK, total);
+    constexpr int PER = FWD_ONLY ? PREP_PER_FWD : PREP_PER, CHUNK = 256 * PER;
+    const int64_t c0 = int64_t(blockIdx.x) * CHUNK, c1 = min(c0 + CHUNK, total);
     const int pass = FWD_ONLY ? 0 : int(blockIdx.y);
     // the chunk's first entry (the last with elem_offset <= c0; offsets ascending): a two-level 64-ary search, each level
     // one load per lane + a ballot (every wave repeats it: no LDS, no barrier) — 2 memory round trips for <= 4096
@@ -924,10 +931,10 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry*
                 return;
             }
         }
-        float v[PREP_PER];
-        int64_t di[PREP_PER];
+        float v[PER];
+        int64_t di[PER];
 #pragma unroll
-        for (int k = 0; k < PREP_PER; ++k) {
+        for (int k = 0; k < PER; ++k) {
             const int j = min(jb + k * 256, nj - 1);
             int64_t si;
             if (pass == 0) {
@@ -944,7 +951,7 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const ym_wprep_entry*
             v[k] = t.src[si];
         }
 #pragma unroll
-        for (int k = 0; k < PREP_PER; ++k) {
+        for (int k = 0; k < PER; ++k) {
             if (jb + k * 256 >= nj) break;
             dst[di[k]] = pass == 0 ? f2h(v[k]) : f2bf(v[k]);
         }
@@ -1660,7 +1667,8 @@ extern "C" int ym_prep_weights(const ym_wprep_entry* table_dev, int n_entries, i
 
 extern "C" int ym_prep_weights_fwd(const ym_wprep_entry* table_dev, int n_entries, int64_t total_elems, void* stream) {
     if (total_elems == 0) return YM_OK;
-    hipLaunchKernelGGL(prep_weights_kernel<true>, dim3(unsigned((total_elems + PREP_CHUNK - 1) / PREP_CHUNK)), dim3(256),
+    constexpr int CHUNK = 256 * PREP_PER_FWD;
+    hipLaunchKernelGGL(prep_weights_kernel<true>, dim3(unsigned((total_elems + CHUNK - 1) / CHUNK)), dim3(256),
                        0, as_stream(stream), table_dev, n_entries, total_elems);
     YM_LAUNCH_CHECK("ym_prep_weights_fwd");
     return YM_OK;
