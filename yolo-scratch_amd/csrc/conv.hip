@@ -535,27 +535,30 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
     }
 }
 
-// eval-mode stem Conv block in one launch (ym_conv_first_fwd_eval): the same per-(pixel, 8 channels) conv, then the
-// running-statistics BatchNorm + SiLU on the fp32 sum (EvalEpi's arithmetic) and one 16-B store into the activation
-// view; no statistics, no fp16 z, no apply launch
+// eval-mode stem Conv block in one launch (ym_conv_first_fwd_eval): one thread per output pixel and ALL its channels
+// (the weights, scale and shift broadcast from LDS), the running-statistics BatchNorm + SiLU on the fp32 sums
+// (EvalEpi's arithmetic, the training kernel's summation order) and 16-B stores of the pixel's contiguous channel
+// run — a wave writes 64 whole pixel rows; the 9 image reads are made once per pixel, not once per 8 channels.
+// No statistics, no fp16 z, no apply launch.  Cout % 8 == 0, Cout <= 512.
 __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                               const float* __restrict__ sc, const float* __restrict__ sh,
                                                               int act, uint16_t* __restrict__ y, int64_t y_bs,
                                                               int64_t y_ld, int N, int H, int W, int OH, int OW,
                                                               int Cout, int stride, int pad) {
-    const int G = Cout >> 3;
-    const int g = threadIdx.x % G;
-    float wr[8][9], s[8], h[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-#pragma unroll
-        for (int t = 0; t < 9; ++t) wr[r][t] = w[(g * 8 + r) * 9 + t];
-        s[r] = sc[g * 8 + r];
-        h[r] = sh[g * 8 + r];
+    // weights tap-major in LDS ([t][c]: 8 channels of one tap = two 16-B broadcast reads)
+    __shared__ __attribute__((aligned(16))) float wl[512 * 9];
+    __shared__ __attribute__((aligned(16))) float sl[512], hl[512];
+    for (int i = threadIdx.x; i < Cout * 9; i += 256) {
+        const int c = i / 9, t = i - c * 9;
+        wl[t * Cout + c] = w[i];
     }
+    for (int i = threadIdx.x; i < Cout; i += 256) {
+        sl[i] = sc[i];
+        hl[i] = sh[i];
+    }
+    __syncthreads();
     const int M = N * OH * OW, OHW = OH * OW;
-    const int step = gridDim.x * (256 / G);
-    for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
+    for (int m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
         const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
         float patch[9];
 #pragma unroll
@@ -566,21 +569,33 @@ __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __res
                 patch[kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
                                          ? img[(n * H + ih) * W + iw] : 0.f;
             }
-        float v[8];
+        uint16_t* yp = y + int64_t(n) * y_bs + int64_t(pix) * y_ld;
+        for (int c0 = 0; c0 < Cout; c0 += 8) {
+            float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            float a = 0.f;
+            for (int t = 0; t < 9; ++t) {                        // tap order per channel: the training kernel's sum
+                const float4 w0 = *reinterpret_cast<const float4*>(wl + t * Cout + c0);
+                const float4 w1 = *reinterpret_cast<const float4*>(wl + t * Cout + c0 + 4);
+                const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
-            for (int t = 0; t < 9; ++t) a += wr[r][t] * patch[t];
-            const float u = fmaf(a, s[r], h[r]);
-            v[r] = act ? silu_f(u) : u;
+                for (int r = 0; r < 8; ++r) v[r] += wv[r] * patch[t];
+            }
+            const float4 s0 = *reinterpret_cast<const float4*>(sl + c0), s1 = *reinterpret_cast<const float4*>(sl + c0 + 4);
+            const float4 h0 = *reinterpret_cast<const float4*>(hl + c0), h1 = *reinterpret_cast<const float4*>(hl + c0 + 4);
+            const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float u = fmaf(v[r], sv[r], hv[r]);
+                v[r] = act ? silu_f(u) : u;
+            }
+            uint4 o;
+            o.x = pk2h(v[0], v[1]);
+            o.y = pk2h(v[2], v[3]);
+            o.z = pk2h(v[4], v[5]);
+            o.w = pk2h(v[6], v[7]);
+            *reinterpret_cast<uint4*>(yp + c0) = o;
         }
-        uint4 o;
-        o.x = pk2h(v[0], v[1]);
-        o.y = pk2h(v[2], v[3]);
-        o.z = pk2h(v[4], v[5]);
-        o.w = pk2h(v[6], v[7]);
-        *reinterpret_cast<uint4*>(y + int64_t(n) * y_bs + int64_t(pix) * y_ld + g * 8) = o;
     }
 }
 
@@ -1563,16 +1578,16 @@ extern "C" int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, con
                                       int act, uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh,
                                       int ow, int cout, int stride, int pad, void* stream) {
     YM_CHECK_ARG(img && w_oihw && scale && shift && y, "ym_conv_first_fwd_eval: null argument");
-    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd_eval: cout=%d unsupported",
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512, "ym_conv_first_fwd_eval: cout=%d unsupported",
                  cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd_eval: too many pixels");
     YM_CHECK_ARG(y_ld % 8 == 0 && y_bs % 8 == 0 && y_ld >= cout && y_bs >= int64_t(oh) * ow * y_ld &&
                      reinterpret_cast<uintptr_t>(y) % 16 == 0,
                  "ym_conv_first_fwd_eval: output view not 16-byte aligned");
-    const int64_t threads = int64_t(n) * oh * ow * (cout / 8);
+    const int64_t threads = int64_t(n) * oh * ow;                 // one per output pixel
     if (threads == 0) return YM_OK;
-    const int blocks = int(std::min<int64_t>((threads + 255) / 256, 4096));
+    const int blocks = int(std::min<int64_t>((threads + 255) / 256, 8192));
     hipLaunchKernelGGL(conv_first_eval_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, scale,
                        shift, act, y, y_bs, y_ld, n, h, w, oh, ow, cout, stride, pad);
     YM_LAUNCH_CHECK("ym_conv_first_fwd_eval");
