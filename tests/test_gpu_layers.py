@@ -306,14 +306,15 @@ def teacher_forced(scale, imgsz, bs, seed):
     return R
 
 
-@pytest.mark.parametrize("scale,imgsz,bs,select", [("s", 640, 2, 64), ("m", 256, 1, 0)])
+@pytest.mark.parametrize("scale,imgsz,bs,select", [("s", 640, 2, 64), ("m", 256, 1, 0), ("x", 128, 1, 0)])
 def test_teacher_forced_every_layer(scale, imgsz, bs, select):
     """select = 64: every conv kernel choice (kernel, template instance, tile) is made as for the bench's
     s@640 bs64 step (ym_conv_set_select_batch) while the batch is 2, so this test checks, op by op, exactly
     the kernels the benchmarked step runs — the direct / quad kernels on the persistent grids of the 160x160
     stem stage, the halo-pipelined, pipelined, halo and implicit-GEMM instances and every weight-gradient
     instance.  The set of (op, direction, kernel) the bs64 plan selects is computed from the plan's own
-    descriptors and every element of it must have been checked.  select = 0: m@256 bs1 at its own sizes."""
+    descriptors and every element of it must have been checked.  select = 0: m@256 bs1 and x@128 bs1 at their own
+    sizes (x: the 96-channel stem and the 384-channel depthwise pe run as channel pieces 64 + 32 / 256 + 128)."""
     from yolomi._lib import lib
     torch.set_num_threads(min(16, torch.get_num_threads()))
     prev = lib().ym_conv_set_select_batch(select)

@@ -476,10 +476,14 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
 // ------------------------------------------------------------------ stem conv (Cin = 1), fp32 image input
 // one thread per (output pixel, 8 channels), the 8x9 weights in registers, 32-bit index math
 // (N*OH*OW and N*H*W < 2^31, checked on the host).  HBM-bound: writes the fp16 z (2 B/elem).
+// Channel pieces (these small VALU kernels): a launch covers channels c_base .. c_base + Cout of a Ct-channel layer,
+// Cout / 8 a power of two <= 64 (the lane-group reductions); a width like the x-scale stem's 96 runs as pieces 64 + 32
+// (ch_pieces below), rows / partial rows strided by Ct.
 __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                              uint16_t* __restrict__ y, float* __restrict__ st_sum,
                                                              float* __restrict__ st_sq, int N, int H, int W, int OH,
-                                                             int OW, int Cout, int stride, int pad) {
+                                                             int OW, int Cout, int stride, int pad, int c_base,
+                                                             int Ct) {
     __shared__ float red[2][512];
     const int G = Cout >> 3;                 // channel groups (divides 64)
     const int g = threadIdx.x % G;
@@ -487,7 +491,7 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-        for (int t = 0; t < 9; ++t) wr[r][t] = w[(g * 8 + r) * 9 + t];
+        for (int t = 0; t < 9; ++t) wr[r][t] = w[(c_base + g * 8 + r) * 9 + t];
     float ls[8], lq[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ls[r] = lq[r] = 0.f;
@@ -519,7 +523,7 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
         o.y = pk2h(v[2], v[3]);
         o.z = pk2h(v[4], v[5]);
         o.w = pk2h(v[6], v[7]);
-        if (y) *reinterpret_cast<uint4*>(y + size_t(m) * Cout + g * 8) = o;   // null: statistics only
+        if (y) *reinterpret_cast<uint4*>(y + size_t(m) * Ct + c_base + g * 8) = o;   // null: statistics only
     }
     // lanes with the same channel group: xor-reduce over the other lane bits, then the waves in order
 #pragma unroll
@@ -530,8 +534,8 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < Cout; c += 256) {
-        st_sum[int64_t(blockIdx.x) * Cout + c] = red[0][c];
-        st_sq[int64_t(blockIdx.x) * Cout + c] = red[1][c];
+        st_sum[int64_t(blockIdx.x) * Ct + c_base + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * Ct + c_base + c] = red[1][c];
     }
 }
 
@@ -603,7 +607,8 @@ __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __res
 // image needs no gradient); dW += the rows summed in order (colsum_kernel)
 __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __restrict__ dz, const float* __restrict__ img,
                                                                float* __restrict__ part, int N, int H, int W, int OH,
-                                                               int OW, int Cout, int stride, int pad) {
+                                                               int OW, int Cout, int stride, int pad, int c_base,
+                                                               int Ct) {
     __shared__ float red[128 * 9];
     const int G = Cout >> 3;
     const int g = threadIdx.x % G;
@@ -622,7 +627,7 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
         for (int u = 0; u < 2; ++u) {
             const int m = m0 + u * step < M ? m0 + u * step : m0;
             const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
-            d[u] = *reinterpret_cast<const uint4*>(dz + size_t(m) * Cout + g * 8);
+            d[u] = *reinterpret_cast<const uint4*>(dz + size_t(m) * Ct + c_base + g * 8);
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -654,7 +659,7 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
     ordered_wave_add72(red, acc, g, G);
-    for (int i = threadIdx.x; i < Cout * 9; i += 256) part[int64_t(blockIdx.x) * Cout * 9 + i] = red[i];
+    for (int i = threadIdx.x; i < Cout * 9; i += 256) part[int64_t(blockIdx.x) * Ct * 9 + c_base * 9 + i] = red[i];
 }
 
 // ------------------------------------------------------------------ depthwise 3x3, stride 1, pad 1
@@ -663,9 +668,10 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
 struct DwArgs {
     const bf16_t* x; int64_t x_bs, x_ld; int gsz, gstride, goff;
     const float* w;            // fp32 [C][9]
-    bf16_t* y;                 // dense (N, H, W, C) (fwd) / dx view (bwd)
+    bf16_t* y;                 // dense (N, H, W, Ct) (fwd) / dx view (bwd)
     int64_t y_bs, y_ld;
-    int N, H, W, C;
+    int N, H, W, C;            // C: this launch's channels (a piece of Ct, from c_base; see conv_first_fwd_kernel)
+    int c_base, Ct;
 };
 
 // one thread per (pixel, 8 channels): 16-B loads, the 8x9 weights in registers, statistics and
@@ -683,7 +689,7 @@ __device__ __forceinline__ void unpack8(uint4 u, float* f, bool half) {
 __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum, float* st_sq) {
     __shared__ float red[2][512];
     const int G = a.C >> 3, g = threadIdx.x % G;
-    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    const int c0 = a.c_base + g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
     float wr[8][9];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -715,7 +721,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
         o.y = pk2h(s[2], s[3]);
         o.z = pk2h(s[4], s[5]);
         o.w = pk2h(s[6], s[7]);
-        *reinterpret_cast<uint4*>(a.y + size_t(m) * a.C + c0) = o;
+        *reinterpret_cast<uint4*>(a.y + size_t(m) * a.Ct + c0) = o;
 #pragma unroll
         for (int r = 0; r < 8; ++r) { ls[r] += s[r]; lq[r] += s[r] * s[r]; }
     }
@@ -727,8 +733,8 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_kernel(DwArgs a, float* st_sum,
         }
     ordered_wave_add8(red[0], red[1], ls, lq, g, G);
     for (int c = threadIdx.x; c < a.C; c += 256) {
-        st_sum[int64_t(blockIdx.x) * a.C + c] = red[0][c];
-        st_sq[int64_t(blockIdx.x) * a.C + c] = red[1][c];
+        st_sum[int64_t(blockIdx.x) * a.Ct + a.c_base + c] = red[0][c];
+        st_sq[int64_t(blockIdx.x) * a.Ct + a.c_base + c] = red[1][c];
     }
 }
 
@@ -740,7 +746,7 @@ __global__ void __launch_bounds__(256) dw3x3_fwd_eval_kernel(DwArgs a, const flo
                                                              const uint16_t* __restrict__ res, int64_t r_bs,
                                                              int64_t r_ld) {
     const int G = a.C >> 3, g = threadIdx.x % G;
-    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    const int c0 = a.c_base + g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
     float wr[8][9], s8[8], h8[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -796,7 +802,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
                                                         int accumulate) {
     __shared__ float red[512 * 9];
     const int G = a.C >> 3, g = threadIdx.x % G;
-    const int c0 = g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
+    const int c0 = a.c_base + g * 8, sc0 = (c0 / a.gsz) * a.gstride + a.goff + c0 % a.gsz;
     float wr[8][9], acc[8][9];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
@@ -810,7 +816,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
     for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
         const int n = m / HW, pix = m - n * HW, h = pix / a.W, wc = pix - h * a.W;
         float d0[8], gx[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        unpack8(*reinterpret_cast<const uint4*>(dz + size_t(m) * a.C + c0), d0, false);
+        unpack8(*reinterpret_cast<const uint4*>(dz + size_t(m) * a.Ct + c0), d0, false);
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh)
 #pragma unroll
@@ -819,7 +825,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
                 const int oh = h + 1 - kh, ow = wc + 1 - kw;
                 if (unsigned(oh) < unsigned(a.H) && unsigned(ow) < unsigned(a.W)) {
                     float dv[8];
-                    unpack8(*reinterpret_cast<const uint4*>(dz + size_t(n * HW + oh * a.W + ow) * a.C + c0), dv, false);
+                    unpack8(*reinterpret_cast<const uint4*>(dz + size_t(n * HW + oh * a.W + ow) * a.Ct + c0), dv, false);
 #pragma unroll
                     for (int r = 0; r < 8; ++r) gx[r] += wr[r][kh * 3 + kw] * dv[r];
                 }
@@ -849,7 +855,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
     ordered_wave_add72(red, acc, g, G);
-    for (int i = threadIdx.x; i < 9 * a.C; i += 256) part[int64_t(blockIdx.x) * 9 * a.C + i] = red[i];
+    for (int i = threadIdx.x; i < 9 * a.C; i += 256) part[int64_t(blockIdx.x) * 9 * a.Ct + 9 * a.c_base + i] = red[i];
 }
 
 // ------------------------------------------------------------------ weight preparation
@@ -1561,15 +1567,31 @@ extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     return YM_OK;
 }
 
+// channel pieces of a c-channel layer for the lane-group kernels (stem, depthwise): powers of two of 8-channel groups,
+// largest first, at most max_groups each — f(c_base, channels) per launch (64 + 32 for the x-scale stem's 96)
+template <class F>
+static void ch_pieces(int c, int max_groups, F f) {
+    int base = 0, groups = c / 8;
+    while (groups > 0) {
+        int p = 1;
+        while (p * 2 <= groups && p * 2 <= max_groups) p *= 2;
+        f(base * 8, p * 8);
+        base += p;
+        groups -= p;
+    }
+}
+
 extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
                                  int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
                                  void* stream) {
-    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512 && 64 % (cout / 8) == 0, "ym_conv_first_fwd: cout=%d unsupported", cout);
+    YM_CHECK_ARG(cout % 8 == 0 && cout > 0 && cout <= 4096, "ym_conv_first_fwd: cout=%d unsupported", cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd: too many pixels");
     YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_conv_first_fwd: statistics buffers / blocks");
-    hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
-                       stat_sum, stat_sq, n, h, w, oh, ow, cout, stride, pad);
+    ch_pieces(cout, 64, [&](int c_base, int c) {
+        hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
+                           stat_sum, stat_sq, n, h, w, oh, ow, c, stride, pad, c_base, cout);
+    });
     YM_LAUNCH_CHECK("ym_conv_first_fwd");
     return YM_OK;
 }
@@ -1601,34 +1623,37 @@ extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
 extern "C" int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh,
                                    int ow, int cout, int stride, int pad, float* workspace, size_t workspace_bytes,
                                    void* stream) {
-    YM_CHECK_ARG(cout % 8 == 0 && cout <= 128 && 64 % (cout / 8) == 0, "ym_conv_first_wgrad: cout=%d unsupported",
-                 cout);
+    YM_CHECK_ARG(cout % 8 == 0 && cout > 0 && cout <= 4096, "ym_conv_first_wgrad: cout=%d unsupported", cout);
     YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
                  "ym_conv_first_wgrad: too many pixels");
     YM_CHECK_ARG(workspace && workspace_bytes >= ym_conv_first_wgrad_workspace_size(cout),
                  "ym_conv_first_wgrad: workspace too small");
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dz, img, workspace, n, h, w, oh,
-                       ow, cout, stride, pad);
+    ch_pieces(cout, 16, [&](int c_base, int c) {             // <= 128 channels a piece (the kernel's LDS rows)
+        hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dz, img, workspace, n, h, w,
+                           oh, ow, c, stride, pad, c_base, cout);
+    });
     colsum_launch(workspace, PARTIAL_BLOCKS, cout * 9, int64_t(cout) * 9, dw_oihw, 1, st);
     YM_LAUNCH_CHECK("ym_conv_first_wgrad");
     return YM_OK;
 }
 
+// any C % 8 == 0 (run as ch_pieces of <= 512 channels); 8-channel aligned channel map and views
 static bool dw_shape_ok(int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff, int c) {
-    const int G = c / 8;
-    return c % 8 == 0 && G >= 1 && G <= 64 && (G & (G - 1)) == 0 && gsz % 8 == 0 && gstride % 8 == 0 &&
-           goff % 8 == 0 && x_bs % 8 == 0 && x_ld % 8 == 0;
+    return c % 8 == 0 && c > 0 && c <= 8192 && gsz % 8 == 0 && gstride % 8 == 0 && goff % 8 == 0 && x_bs % 8 == 0 &&
+           x_ld % 8 == 0;
 }
 
 extern "C" int ym_dw3x3_fwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int gsz, int gstride, int goff,
                             const float* w, uint16_t* y, float* stat_sum, float* stat_sq, int n, int h, int wd, int c,
                             int blocks, void* stream) {
     YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
-                 "ym_dw3x3_fwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+                 "ym_dw3x3_fwd: unsupported shape (C %% 8 != 0 or channel map / views not 8-channel aligned)");
     YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_dw3x3_fwd: statistics buffers / blocks");
-    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
+    ch_pieces(c, 64, [&](int c_base, int cp) {
+        const DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, 0, 0, n, h, wd, cp, c_base, c};
+        hipLaunchKernelGGL(dw3x3_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), a, stat_sum, stat_sq);
+    });
     YM_LAUNCH_CHECK("ym_dw3x3_fwd");
     return YM_OK;
 }
@@ -1639,15 +1664,17 @@ extern "C" int ym_dw3x3_fwd_eval(const uint16_t* x, int64_t x_bs, int64_t x_ld, 
                                  int wd, int c, void* stream) {
     YM_CHECK_ARG(x && w && scale && shift && y, "ym_dw3x3_fwd_eval: null argument");
     YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && int64_t(n) * h * wd < (int64_t(1) << 31),
-                 "ym_dw3x3_fwd_eval: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+                 "ym_dw3x3_fwd_eval: unsupported shape (C %% 8 != 0 or channel map / views not 8-channel aligned)");
     YM_CHECK_ARG(y_bs % 8 == 0 && y_ld % 8 == 0 && reinterpret_cast<uintptr_t>(y) % 16 == 0 &&
                      (!res || (r_bs % 4 == 0 && r_ld % 4 == 0 && reinterpret_cast<uintptr_t>(res) % 8 == 0)),
                  "ym_dw3x3_fwd_eval: output / residual view alignment");
-    const int64_t threads = int64_t(n) * h * wd * (c / 8);
-    if (threads == 0) return YM_OK;
-    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, y_bs, y_ld, n, h, wd, c};
-    hipLaunchKernelGGL(dw3x3_fwd_eval_kernel, dim3(unsigned(std::min<int64_t>((threads + 255) / 256, 4096))), dim3(256),
-                       0, as_stream(stream), a, scale, shift, act, res, r_bs, r_ld);
+    if (int64_t(n) * h * wd == 0) return YM_OK;
+    ch_pieces(c, 64, [&](int c_base, int cp) {
+        const int64_t threads = int64_t(n) * h * wd * (cp / 8);
+        const DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, y, y_bs, y_ld, n, h, wd, cp, c_base, c};
+        hipLaunchKernelGGL(dw3x3_fwd_eval_kernel, dim3(unsigned(std::min<int64_t>((threads + 255) / 256, 4096))),
+                           dim3(256), 0, as_stream(stream), a, scale, shift, act, res, r_bs, r_ld);
+    });
     YM_LAUNCH_CHECK("ym_dw3x3_fwd_eval");
     return YM_OK;
 }
@@ -1662,11 +1689,13 @@ extern "C" int ym_dw3x3_bwd(const uint16_t* x, int64_t x_bs, int64_t x_ld, int g
                             void* stream) {
     YM_CHECK_ARG(dw_shape_ok(x_bs, x_ld, gsz, gstride, goff, c) && dx_bs % 8 == 0 && dx_ld % 8 == 0 &&
                      int64_t(n) * h * wd < (int64_t(1) << 31),
-                 "ym_dw3x3_bwd: unsupported shape (C/8 a power of two <= 64, 8-channel aligned views)");
+                 "ym_dw3x3_bwd: unsupported shape (C %% 8 != 0 or channel map / views not 8-channel aligned)");
     YM_CHECK_ARG(workspace && workspace_bytes >= ym_dw3x3_bwd_workspace_size(c), "ym_dw3x3_bwd: workspace too small");
-    DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, dx, dx_bs, dx_ld, n, h, wd, c};
     hipStream_t st = as_stream(stream);
-    hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, a, dz, workspace, accumulate);
+    ch_pieces(c, 64, [&](int c_base, int cp) {
+        const DwArgs a{x, x_bs, x_ld, gsz, gstride, goff, w, dx, dx_bs, dx_ld, n, h, wd, cp, c_base, c};
+        hipLaunchKernelGGL(dw3x3_bwd_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, a, dz, workspace, accumulate);
+    });
     colsum_launch(workspace, PARTIAL_BLOCKS, c * 9, int64_t(c) * 9, dw, 1, st);
     YM_LAUNCH_CHECK("ym_dw3x3_bwd");
     return YM_OK;
