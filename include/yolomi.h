@@ -172,7 +172,8 @@ int ym_conv_set_halo(int mode);
  * Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_pipe(int mode);
 /* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
- * layers) for later calls: -1 default, 0 never, 1 maps of >= 1 M output pixels (default), 2 any size.
+ * layers) for later calls: -1 default, 0 never, 1 maps of >= 1 M output pixels (default), 2 any size, 3 >= 200 k
+ * output pixels.
  * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_direct(int mode);
 /* Selection policy of the halo-staged pipelined 3x3 stride-1 kernel (conv_hpipe.hip: 16x16-pixel tiles,
@@ -290,6 +291,9 @@ int ym_conv_fwd_eval_ok(const ym_conv_desc* d);
 /* Stage / ring configuration of ym_conv_fwd_eval's implicit GEMM (0: 32-deep K stages x 3, 1: 64 x 3 (default),
  * 2: 64 x 4); <0 restores the default.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
 int ym_conv_set_eval_cfg(int cfg);
+/* Eval GEMM outputs of <= 32 channels on a 128 x 32 tile (1, default; <0 restores it) or the 128 x 64 one (0).
+ * Returns the previous setting. */
+int ym_conv_set_eval_narrow(int on);
 /* Small grids (a bs-1 forward's late layers: a few dozen tiles, each walking a long K serially) run as a K-split: the
  * GEMM launch writes ks fp32 partial slices into the caller's workspace and a second launch applies BatchNorm / SiLU /
  * residual to their sum.  ym_conv_fwd_eval_workspace_size(d) is the workspace that takes (0: one launch); with a

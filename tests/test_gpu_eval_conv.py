@@ -33,6 +33,8 @@ CASES = [
     (2, 20, 20, 64, 40, 1, 1),
     (1, 20, 20, 136, 64, 3, 1),       # K-split: 27 K stages in 6 slices, slices starting inside a tap
     (1, 10, 10, 1024, 64, 1, 1),      # K-split of a 1x1: 16 stages in 4 slices
+    (2, 40, 40, 48, 16, 3, 1),        # <= 32 output channels: the 128 x 32 eval tile (1 x 4 waves)
+    (1, 20, 20, 256, 24, 3, 1),       # ... a ragged width on it, K-split (36 stages in 9 slices)
     (4, 128, 128, 64, 64, 1, 1),      # >= 256 tiles: the pipelined forward's eval instance (256 x 64 tile)
     (4, 128, 128, 128, 128, 3, 1),    # ... its 256 x 128 tile
 ]

@@ -1151,9 +1151,9 @@ extern "C" int ym_conv_set_pipe(int mode) {
 
 extern "C" int ym_conv_set_direct(int mode) {
     // selection policy of the direct register-weight kernel: -1 default, 0 never, 1 maps of
-    // >= 1 M output pixels (default), 2 any size; returns the previous setting
+    // >= 1 M output pixels (default), 2 any size, 3 >= 200 k output pixels; returns the previous setting
     const int prev = g_direct_force;
-    g_direct_force = mode < -1 || mode > 2 ? -1 : mode;
+    g_direct_force = mode < -1 || mode > 3 ? -1 : mode;
     return prev;
 }
 
@@ -1332,6 +1332,15 @@ extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const ui
 // 1: 64-deep x 3, 2: 64-deep x 4 — at bs 1 a launch covers a few tiles and walks its whole K serially, so deeper
 // stages halve its DMA round trips (128-deep x 3, one workgroup per CU, measured slower: profiles/r05/eval_split_ab.txt)
 static int g_eval_cfg = 1;
+static int g_eval_narrow = 1;
+
+extern "C" int ym_conv_set_eval_narrow(int on) {
+    // eval GEMM outputs of <= 32 channels on the 128 x 32 tile (1, default; <0 restores it) or the 128 x 64 (0);
+    // returns the previous setting
+    const int prev = g_eval_narrow;
+    g_eval_narrow = on < 0 ? 1 : (on ? 1 : 0);
+    return prev;
+}
 
 extern "C" int ym_conv_set_eval_cfg(int cfg) {
     // the eval GEMM's stage / ring configuration (0..2, -1 default 1); returns the previous setting
@@ -1492,7 +1501,10 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
     a.N = d->n;
     a.ostep = 1;
     a.ep_lds = 1;
-    if (g_eval_cfg == 0) launch_gemm<128, 64, 2, 2, 32, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
+    // outputs of <= 32 channels: the 128 x 32 tile on 4 waves along the pixels (1 x 4: 32 channels per wave, the
+    // register epilogue's minimum) instead of half-masking the 128 x 64 tile (ym_conv_set_eval_narrow)
+    if (g_eval_narrow && d->cout <= 32) launch_gemm<128, 32, 1, 4, 64, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
+    else if (g_eval_cfg == 0) launch_gemm<128, 64, 2, 2, 32, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     else if (g_eval_cfg == 1) launch_gemm<128, 64, 2, 2, 64, 3, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     else launch_gemm<128, 64, 2, 2, 64, 4, MODE_FWD, true>(a, FWD_STAT_BLOCKS, st, ev);
     if (ks > 1) {

@@ -446,6 +446,10 @@ const Variant kVariants[] = {
 };
 #undef DIR_VARIANT
 
+// default 1 (>= 1 M output pixels).  Round 5: mode 3 (>= 200 k) measured the s@640 inference at bs 8 / 32 +0-2 / +3-4 %
+// and the bs64 step unchanged in sum, but it moves the 80x80 layers of the bs64 step to this kernel and the largest
+// of them (128 -> 128 3x3 s2, the bench line's probe) ran 0.174 -> 0.203 ms: kept at 1
+// (profiles/r05/direct_threshold_ab.txt)
 int direct_mode() { return g_direct_force >= 0 ? g_direct_force : 1; }
 
 // workgroups of variant i the whole chip holds at once (CUs x the kernel's occupancy), cached per device and
@@ -488,6 +492,7 @@ DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
     const int OH = dgrad ? d->h : d->oh, OW = dgrad ? d->w : d->ow;
     const int64_t M = select_n(d) * OH * OW;
     if (mode == 1 && M < (int64_t(1) << 20)) return p;
+    if (mode == 3 && M < 200000) return p;          // >= 200 k: the 160x160 stage from 8 images up
     for (int i = 0; i < int(sizeof(kVariants) / sizeof(kVariants[0])); ++i) {
         const Variant& v = kVariants[i];
         if (v.mode != dgrad || v.ks != d->k || v.s != d->stride || v.kc * 32 != kin) continue;

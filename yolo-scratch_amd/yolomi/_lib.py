@@ -94,6 +94,7 @@ SIGNATURES = {
     "ym_conv_set_fold": (R, [INT]),
     "ym_conv_fwd_eval_ok": (R, [P]),
     "ym_conv_set_eval_cfg": (R, [INT]),
+    "ym_conv_set_eval_narrow": (R, [INT]),
     "ym_conv_fwd_eval_workspace_size": (SZ, [P]),
     "ym_conv_set_eval_split": (R, [INT]),
     "ym_conv_set_eval_split_nk": (R, [INT]),
