@@ -1261,7 +1261,7 @@ static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_
                int64_t(d->n) * d->y_bs * 2 < (int64_t(1) << 31) && reinterpret_cast<uintptr_t>(y) % 16 == 0;
     if (a.M == 0) return YM_OK;
     // the direct and halo-pipelined kernels have no bias term: a conv with bias takes the kernels below
-    const DirectPlan dp = bias ? DirectPlan{} : direct_plan(d, 0);
+    const DirectPlan dp = bias ? DirectPlan{} : direct_plan(d, 0, stat_sum == nullptr);
     if (dp.ok) {
         direct_launch(dp, d, 0, x, w, y, stat_sum, stat_sq, as_stream(stream));
         YM_LAUNCH_CHECK("ym_conv_fwd (direct)");
@@ -1427,7 +1427,7 @@ static bool eval_layout_ok(const ym_conv_desc* d) {
     if (!d || d->cin % 8 || d->cout % 8 || d->k < 1 || d->k > 3 || d->out_f32 != 2 || d->accumulate) return false;
     if (d->x_ld % 8 || d->x_bs % 8 || d->y_ld % 8 || d->y_bs % 8) return false;
     if (int64_t(d->n) * d->y_bs * 2 >= (int64_t(1) << 31)) return false;
-    if (direct_plan(d, 0).ok) return false;                          // no eval epilogue there
+    if (direct_plan(d, 0, true).ok) return false;                    // no eval epilogue there
     if (hpipe_plan(d, 0).ok && !((g_eval_route & 2) && eval_gemm_fits(d))) return false;
     const PipePlan pp = pipe_plan(d, 0);
     return !pp.ok || (g_eval_pipe && pipe_eval_ok(pp, d));          // the pipelined forward's eval instance

@@ -14,7 +14,9 @@ struct DirectPlan {
 // -1: default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size
 extern int g_direct_force;
 
-DirectPlan direct_plan(const ym_conv_desc* d, int dgrad);
+// inference: a forward without BatchNorm statistics (the eval path) — under the default policy it takes the kernel from
+// 200 k output pixels (the 160x160 stage from 8 images up) instead of 1 M
+DirectPlan direct_plan(const ym_conv_desc* d, int dgrad, bool inference = false);
 int direct_launch(const DirectPlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w,
                   void* y, float* st_sum, float* st_sq, hipStream_t st);
 

@@ -474,9 +474,12 @@ int resident_blocks(int i) {
 
 }  // namespace
 
-DirectPlan direct_plan(const ym_conv_desc* d, int dgrad) {
+DirectPlan direct_plan(const ym_conv_desc* d, int dgrad, bool inference) {
     DirectPlan p{};
-    const int mode = direct_mode();
+    int mode = direct_mode();
+    // the inference forward (no statistics): mode 3's threshold under the default policy (s@640 bs 8 / 32 +0-2 / +3-4 %,
+    // profiles/r05/direct_threshold_ab.txt; the training step keeps 1 M: its 80x80 layers ran slower here)
+    if (inference && !dgrad && mode == 1 && g_direct_force < 0) mode = 3;
     if (!d || mode == 0) return p;
     if (d->k != 1 && d->k != 3) return p;
     if (d->pad != d->k / 2 || (d->stride != 1 && d->stride != 2)) return p;
