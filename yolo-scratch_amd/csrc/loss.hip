@@ -212,6 +212,12 @@ __global__ void __launch_bounds__(256) assign_scan_kernel(Src src, int64_t A, co
         if (lane == 0 && pos) atomicAdd(&s_cnt[g], int(__popcll(pos)));
         // wave max of the packed (iou, ~a) key: the first anchor of the best IoU
         uint32_t hi = live ? __float_as_uint(iou) : 0u, lo = live ? 0xffffffffu - uint32_t(a) : 0u;
+        // most (wave, gt) pairs overlap nowhere: every key's iou bits are then 0 and the wave max is lane 0's
+        // (the lowest anchor; lane 0 is live whenever any lane is), so the 12 shuffles are skipped
+        if (!__ballot(hi != 0u)) {
+            if (lane == 0 && live) atomicMax(&s_amax[g], uint64_t(lo));
+            continue;
+        }
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             const uint32_t h2 = __shfl_xor(hi, o, 64), l2 = __shfl_xor(lo, o, 64);
@@ -390,13 +396,33 @@ __device__ __forceinline__ float bce(float x, float t) {
     return (1.0f - t) * x + mv + logf(expf(-mv) + expf(-x - mv));
 }
 
-// one thread per anchor; block partials (double) of cls, box, dfl, tss
+// one thread per anchor; block partials (double) of cls, box, dfl, tss.  The workgroup's class logits (a contiguous run
+// of 256 head rows) are staged through LDS by coalesced loads first (round 5: each lane read its own 20 B at a 276-B
+// row stride); every thread's arithmetic and summation order is unchanged.
+constexpr int LOSS_NC_LDS = 16;                 // class counts staged through LDS (larger ones read the rows directly)
 __global__ void __launch_bounds__(256) loss_partial_kernel(const float* __restrict__ head, int64_t A, int no, int nc,
                                                            Levels L, const float4* __restrict__ gt_box,
                                                            const float* __restrict__ gt_lab, int M, AssignWs w) {
     __shared__ double red[5][256];
+    __shared__ float s_cls[256 * LOSS_NC_LDS];
     const int b = blockIdx.y;
-    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const int64_t a0 = int64_t(blockIdx.x) * blockDim.x;
+    const int64_t a = a0 + threadIdx.x;
+    const bool staged = nc <= LOSS_NC_LDS;
+    if (staged) {
+        const int na = int(min(int64_t(blockDim.x), A - a0));
+        const float* xr = head + (int64_t(b) * A + a0) * no;
+        // element e of the run's class block = (row aa, class c); (aa, c) stepped without a division per element
+        const int q = int(blockDim.x) / nc, r = int(blockDim.x) - q * nc;
+        int aa = threadIdx.x / nc, c = threadIdx.x - aa * nc;
+        for (int e = threadIdx.x; e < na * nc; e += blockDim.x) {
+            s_cls[e] = xr[int64_t(aa) * no + 64 + c];
+            c += r;
+            aa += q;
+            if (c >= nc) { c -= nc; ++aa; }
+        }
+        __syncthreads();
+    }
     double lc = 0, lb = 0, ld = 0, ts = 0, nf = 0;
     if (a < A) {
         const int64_t i = int64_t(b) * A + a;
@@ -405,9 +431,10 @@ __global__ void __launch_bounds__(256) loss_partial_kernel(const float* __restri
         const float nm = w.norm[i];
         int lab = 0;
         if (f) lab = int(gt_lab[b * M + w.tgi[i]]);
+        const float* xc = staged ? s_cls + threadIdx.x * nc : x + 64;
         for (int c = 0; c < nc; ++c) {
             float t = (f && c == lab) ? nm : 0.f;
-            lc += bce(x[64 + c], t);
+            lc += bce(xc[c], t);
         }
         if (f) {
             ts = nm;
@@ -478,30 +505,56 @@ __global__ void loss_final_kernel(int nparts, int B, AssignWs w) {
     }
 }
 
-// d loss / d head rows; gscale = d(total)/d(loss) (autograd's incoming grad, device scalar)
+// d loss / d head rows; gscale = d(total)/d(loss) (autograd's incoming grad, device scalar).
+// A workgroup's 256 anchors are one contiguous run of 256 x no floats of head / dhead: the background rows' zero DFL
+// gradients are stored a row (256 B) per wave instruction and the class-logit gradients element by element over the
+// run (round 5 — the thread-per-row form stored 4 B per lane at a 276-B row stride), then each foreground anchor's
+// thread writes its 64 DFL / box gradients (2-3 % of the rows).  Same arithmetic per element.
 __global__ void __launch_bounds__(256) loss_bwd_kernel(const float* __restrict__ head, int64_t A, int no, int nc, int B,
                                                        Levels L, const float4* __restrict__ gt_box,
                                                        const float* __restrict__ gt_lab, int M, AssignWs w,
                                                        const float* __restrict__ gout, float* __restrict__ dhead) {
+    __shared__ int s_f[256], s_lab[256];
+    __shared__ float s_nm[256];
     const int b = blockIdx.y;
-    const int64_t a = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (a >= A) return;
+    const int64_t a0 = int64_t(blockIdx.x) * blockDim.x;
+    const int na = int(min(int64_t(blockDim.x), A - a0));
+    const int tid = threadIdx.x;
+    const float k = gout[0] * float(B) / w.out[4];
+    if (tid < na) {
+        const int64_t i = int64_t(b) * A + a0 + tid;
+        const int f = w.fg[i];
+        s_f[tid] = f;
+        s_nm[tid] = w.norm[i];
+        s_lab[tid] = f ? int(gt_lab[b * M + w.tgi[i]]) : 0;
+    }
+    __syncthreads();
+    {
+        const int64_t r0 = (int64_t(b) * A + a0) * no;
+        const float* xr = head + r0;
+        float* dr = dhead + r0;
+        // background rows' 64 zero DFL gradients: wave wv stores rows wv*64 .. wv*64+63, one row per store
+        // instruction, skipping foreground rows by a wave-uniform bit of a ballot (no memory read in the loop)
+        const int wv = tid >> 6, lane = tid & 63, rb = wv * 64;
+        const unsigned long long bg = __ballot(rb + lane < na && !s_f[rb + lane]);
+        for (int r = 0; r < 64; ++r)
+            if ((bg >> r) & 1ull) dr[int64_t(rb + r) * no + lane] = 0.f;
+        // class-logit gradients, element e = (row aa, class c) of the run's class block, stepped without divisions
+        const int q = int(blockDim.x) / nc, rr = int(blockDim.x) - q * nc;
+        int aa = tid / nc, c = tid - aa * nc;
+        for (int e = tid; e < na * nc; e += blockDim.x, c += rr, aa += q) {
+            if (c >= nc) { c -= nc; ++aa; }
+            const int64_t o = int64_t(aa) * no + 64 + c;
+            const float t = (s_f[aa] && c == s_lab[aa]) ? s_nm[aa] : 0.f;
+            dr[o] = 0.5f * k * (sigm(xr[o]) - t);
+        }
+    }
+    if (tid >= na || !s_f[tid]) return;
+    const int64_t a = a0 + tid;
     const int64_t i = int64_t(b) * A + a;
     const float* x = head + i * no;
     float* dx = dhead + i * no;
-    const float k = gout[0] * float(B) / w.out[4];
-    const int f = w.fg[i];
-    const float nm = w.norm[i];
-    int lab = 0;
-    if (f) lab = int(gt_lab[b * M + w.tgi[i]]);
-    for (int c = 0; c < nc; ++c) {
-        float t = (f && c == lab) ? nm : 0.f;
-        dx[64 + c] = 0.5f * k * (sigm(x[64 + c]) - t);
-    }
-    if (!f) {
-        for (int j = 0; j < 64; ++j) dx[j] = 0.f;
-        return;
-    }
+    const float nm = s_nm[tid];
     float ax, ay, s;
     anchor_of(L, a, ax, ay, s);
     float4 gb = gt_box[b * M + w.tgi[i]];
