@@ -301,6 +301,7 @@ class _LossFn(torch.autograd.Function):
         loss = lc.out[0].clone()
         items = lc.out[1:4].clone()
         ctx.mark_non_differentiable(items)
+        ctx.set_materialize_grads(False)      # items' gradient stays None: no zero-filled (3,) tensor per backward
         return loss, items
 
     @staticmethod
