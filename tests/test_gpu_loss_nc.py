@@ -1,0 +1,49 @@
+"""The fused loss (ym_loss_fwd / ym_loss_bwd) at class counts other than the crater config's 5: 1, 16 (the largest
+count loss_partial stages through LDS), 17 (the first it reads from the rows directly) and 80 (COCO), against the
+CPU oracle's v8_loss (oracle/loss.py, following yolo_v8_loss.py:372-499) on the same fp32 head maps — assignment
+decisions exact, loss / items within 1e-4, head-map gradients within 1e-3 (the golden assigner test's bounds)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nc", [1, 16, 17, 80])
+def test_fused_loss_class_counts_vs_oracle(nc):
+    import torch.nn as nn
+    from models import Detect
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    from oracle import loss as ol
+
+    class Stub(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.det = Detect(nc, (64, 128, 256))
+            self.det.stride = torch.tensor([8.0, 16.0, 32.0])
+
+    B, imgsz = 3, 256
+    b = synth_batch(B, imgsz, seed=100 + nc, nc=nc)
+    batch = {k: b[k] for k in ("batch_idx", "cls", "bboxes")}
+    g = torch.Generator().manual_seed(nc)
+    feats = [torch.randn(B, 64 + nc, imgsz // s, imgsz // s, generator=g) * 2.0 for s in (8, 16, 32)]
+
+    crit = v8DetectionLoss(Stub().cuda())
+    fd = [f.cuda().requires_grad_(True) for f in feats]
+    loss, items = crit(fd, {k: v.cuda() for k, v in batch.items()})
+    tgi, fg, nm = crit.assignment()
+    loss.backward()
+
+    fr = [f.clone().requires_grad_(True) for f in feats]
+    rl, ri, inter = ol.v8_loss(fr, batch, nc=nc, return_internals=True)
+    rl.backward()
+
+    assert int(inter["fg"].sum()) > 0
+    np.testing.assert_array_equal(fg.cpu().numpy().astype(bool), inter["fg"].numpy())
+    fgm = inter["fg"]
+    np.testing.assert_array_equal(tgi.cpu()[fgm].numpy(), inter["tgi"][fgm].numpy())
+    torch.testing.assert_close(items.cpu(), ri, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(loss.detach().cpu(), rl.detach(), rtol=1e-4, atol=1e-6)
+    for a, r in zip(fd, fr):
+        torch.testing.assert_close(a.grad.cpu(), r.grad, rtol=1e-3, atol=1e-6)

@@ -821,7 +821,7 @@ extern "C" int ym_loss_fwd(const float* head, int64_t B, int64_t A, int nc, int 
                            void* workspace, size_t workspace_bytes, float* gt_box, float* gt_lab, int* gt_valid,
                            float* out, void* stream) {
     YM_CHECK_ARG(nl >= 1 && nl <= MAXLV, "ym_loss_fwd: 1..4 levels");
-    YM_CHECK_ARG(nc >= 1 && nc <= 64, "ym_loss_fwd: nc");
+    YM_CHECK_ARG(nc >= 1 && nc <= 1024, "ym_loss_fwd: nc=%d out of range (1..1024)", nc);
     YM_CHECK_ARG(M >= 0 && M <= 4096, "ym_loss_fwd: M=%d out of range", M);
     hipStream_t st = as_stream(stream);
     Levels L = make_levels(nl, level_h, level_w, strides);
@@ -969,7 +969,7 @@ extern "C" int ym_tal_assign(const float* pd_scores, const float* pd_bboxes, con
                              float* target_bboxes, float* target_scores, uint8_t* fg_mask, int64_t* target_gt_idx,
                              void* stream) {
     YM_CHECK_ARG(M >= 1 && M <= 4096, "ym_tal_assign: M=%d out of range (1..4096)", M);
-    YM_CHECK_ARG(nc >= 1 && nc <= 64, "ym_tal_assign: nc");
+    YM_CHECK_ARG(nc >= 1 && nc <= 1024, "ym_tal_assign: nc=%d out of range (1..1024)", nc);
     YM_CHECK_ARG((reinterpret_cast<uintptr_t>(gt_bboxes) & 15) == 0, "ym_tal_assign: gt_bboxes not 16-B aligned");
     YM_CHECK_ARG((reinterpret_cast<uintptr_t>(target_bboxes) & 15) == 0, "ym_tal_assign: target_bboxes not 16-B aligned");
     hipStream_t st = as_stream(stream);
@@ -1002,7 +1002,7 @@ extern "C" int ym_bbox_loss_fwd(const float* pred_dist, const float* pred_bboxes
                                 const float* target_bboxes, const float* target_scores, const float* tss,
                                 const uint8_t* fg_mask, int64_t B, int64_t A, int nc, void* workspace,
                                 size_t workspace_bytes, float* out, void* stream) {
-    YM_CHECK_ARG(nc >= 1 && nc <= 64, "ym_bbox_loss_fwd: nc");
+    YM_CHECK_ARG(nc >= 1 && nc <= 1024, "ym_bbox_loss_fwd: nc=%d out of range (1..1024)", nc);
     YM_CHECK_ARG(workspace_bytes >= ym_bbox_loss_workspace_size(B, A), "ym_bbox_loss_fwd: workspace too small");
     hipStream_t st = as_stream(stream);
     BoxIn in{pred_dist, pred_bboxes, anchor_points, target_bboxes, target_scores, fg_mask, A, nc};
