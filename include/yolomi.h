@@ -397,7 +397,7 @@ int ym_view_to_f32(const uint16_t* x, int64_t bs, int64_t ld, float* y, int64_t 
 int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t ld, int64_t m, int c, int hw, int accumulate,
                    void* stream);
 /* dhead (B, A, 64+nc) fp32 rows of one pyramid level -> bf16 dz for the box / cls 1x1 convs
- * (cls zero-padded to 8 channels) and bias grads (+=). */
+ * (cls zero-padded to a multiple of 8 channels, dz_cls rows of round_up(nc, 8)) and bias grads (+=); nc 1..1024. */
 size_t ym_head_grad_workspace_size(void);
 int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc, uint16_t* dz_box,
                  uint16_t* dz_cls, float* dbias_box, float* dbias_cls, float* workspace, size_t workspace_bytes,

@@ -47,3 +47,44 @@ def test_fused_loss_class_counts_vs_oracle(nc):
     torch.testing.assert_close(loss.detach().cpu(), rl.detach(), rtol=1e-4, atol=1e-6)
     for a, r in zip(fd, fr):
         torch.testing.assert_close(a.grad.cpu(), r.grad, rtol=1e-3, atol=1e-6)
+
+
+def test_model_80_classes_train_step_and_eval():
+    """An 80-class model through the HIP path (ym_head_grad's class rows padded to 8-channel groups): the fused loss
+    on the network's own heads equals the oracle's v8_loss on the same heads (1e-4), every gradient is finite, and the
+    eval forward decodes (B, 4 + 80, A) finite rows.  Input stays 1-channel, as every reference entry point builds
+    it (yolo11_model.py:23, :258 ch=1); a 3-channel image is refused loudly by the stem."""
+    ch = 1
+    import yaml
+    from pathlib import Path
+    from models import build_yolo11
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    from datasets import prepare_batch
+    from oracle import loss as ol
+    root = Path(__file__).resolve().parents[1] / "yolo-scratch_amd"
+    cfg = yaml.safe_load((root / "configs" / "yolo11n_crater.yaml").read_text())
+    cfg["scale"] = "s"
+    torch.manual_seed(8)
+    nc = 80
+    m = build_yolo11(cfg, ch=ch, nc=nc).cuda().train()
+    crit = v8DetectionLoss(m, tal_topk=10)
+    b = prepare_batch(synth_batch(2, 160, seed=9, nc=nc, ch=ch), torch.device("cuda"))
+    heads = m(b["img"])
+    loss, items = crit(heads, b)
+    loss.backward()
+    torch.cuda.synchronize()
+    cpu_b = {k: b[k].cpu() for k in ("batch_idx", "cls", "bboxes")}
+    rl, ri = ol.v8_loss([h.detach().float().cpu() for h in heads], cpu_b, nc=nc)
+    torch.testing.assert_close(items.cpu(), ri, rtol=1e-4, atol=1e-6)
+    bad = [n for n, p in m.named_parameters() if p.grad is None or not torch.isfinite(p.grad).all()]
+    assert not [n for n in bad if "dfl" not in n], bad[:5]
+    m.eval()
+    with torch.no_grad():
+        y, _ = m(b["img"])
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (2, 4 + nc, 20 * 20 + 10 * 10 + 5 * 5) and torch.isfinite(y).all(), y.shape
+    from yolomi._lib import YolomiError
+    m3 = build_yolo11(cfg, ch=3, nc=nc).cuda().train()
+    with pytest.raises(YolomiError, match="ch=1"):
+        m3(torch.rand(1, 3, 64, 64, device="cuda"))

@@ -489,18 +489,20 @@ __global__ void view_axpy_kernel(const bf16_t* __restrict__ x, int64_t x_bs, int
 
 // ------------------------------------------------------------------ Detect head gradient split
 // dhead (B, A, 64+nc) fp32 rows for one level (anchor offset `aoff`, HW anchors per image) ->
-// dz_box bf16 [M][64], dz_cls bf16 [M][8] (nc <= 8, zero padded), and per-block bias-gradient
-// partials part[blockIdx.x][72] (summed in a fixed order by colsum_kernel; no atomics).
-// Thread t < 252 owns 8-channel group g = t % 9 of pixel slot t / 9 (28 pixels per block pass).
+// dz_box bf16 [M][64], dz_cls bf16 [M][ncp] (ncp = nc rounded up to 8, zero padded), and per-block bias-gradient
+// partials part[blockIdx.x][64 + ncp] (summed in a fixed order by colsum_kernel; no atomics).
+// A pixel is G = 8 + ncp / 8 groups of 8 channels; thread t < S * G (S = 256 / G pixel slots per block pass) owns
+// group t % G of slot t / G (nc <= 8: G 9, S 28).
 __global__ void __launch_bounds__(256) head_grad_kernel(const float* __restrict__ dh, int64_t A, int64_t aoff, int HW,
                                                         int64_t M, int nc, bf16_t* __restrict__ dbox,
                                                         bf16_t* __restrict__ dcls, float* __restrict__ part) {
-    __shared__ float red[252][9];            // [thread][8 sums] (+1 pad)
-    const int t = threadIdx.x, g = t % 9, slot = t / 9;
+    __shared__ float red[256][9];            // [thread][8 sums] (+1 pad)
+    const int ncp = (nc + 7) & ~7, G = 8 + ncp / 8, S = 256 / G, ncol = 64 + ncp;
+    const int t = threadIdx.x, g = t % G, slot = t / G;
     const int no = 64 + nc;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (t < 252) {
-        for (int64_t m = int64_t(blockIdx.x) * 28 + slot; m < M; m += int64_t(gridDim.x) * 28) {
+    if (t < S * G) {
+        for (int64_t m = int64_t(blockIdx.x) * S + slot; m < M; m += int64_t(gridDim.x) * S) {
             const int64_t n = m / HW, pix = m - n * HW;
             const float* row = dh + (n * A + aoff + pix) * no;
             float v[8];
@@ -509,9 +511,10 @@ __global__ void __launch_bounds__(256) head_grad_kernel(const float* __restrict_
                 for (int k = 0; k < 8; ++k) v[k] = row[g * 8 + k];     // rows of 64+nc floats: 4-B aligned
                 *reinterpret_cast<uint4*>(dbox + m * 64 + g * 8) = pack8(v);
             } else {
+                const int c0 = (g - 8) * 8;
 #pragma unroll
-                for (int k = 0; k < 8; ++k) v[k] = k < nc ? row[64 + k] : 0.f;
-                *reinterpret_cast<uint4*>(dcls + m * 8) = pack8(v);
+                for (int k = 0; k < 8; ++k) v[k] = c0 + k < nc ? row[64 + c0 + k] : 0.f;
+                *reinterpret_cast<uint4*>(dcls + m * ncp + c0) = pack8(v);
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) acc[k] += v[k];
@@ -520,11 +523,11 @@ __global__ void __launch_bounds__(256) head_grad_kernel(const float* __restrict_
         for (int k = 0; k < 8; ++k) red[t][k] = acc[k];
     }
     __syncthreads();
-    if (t < 72) {                            // column t = g * 8 + k: sum the 28 slots in order
-        const int gg = t >> 3, k = t & 7;
+    for (int col = t; col < ncol; col += blockDim.x) {     // column = group * 8 + k: sum the S slots in order
+        const int gg = col >> 3, k = col & 7;
         float s = 0.f;
-        for (int sl = 0; sl < 28; ++sl) s += red[sl * 9 + gg][k];
-        part[int64_t(blockIdx.x) * 72 + t] = s;
+        for (int sl = 0; sl < S; ++sl) s += red[sl * G + gg][k];
+        part[int64_t(blockIdx.x) * ncol + col] = s;
     }
 }
 
@@ -705,18 +708,23 @@ extern "C" int ym_f32_to_view(const float* x, uint16_t* y, int64_t bs, int64_t l
     return YM_OK;
 }
 
-extern "C" size_t ym_head_grad_workspace_size(void) { return size_t(PARTIAL_BLOCKS) * 72 * sizeof(float); }
+constexpr int HEAD_GRAD_MAX_NC = 1024;
+// sized for the largest class count (512 x 1088 floats, 2.2 MB)
+extern "C" size_t ym_head_grad_workspace_size(void) {
+    return size_t(PARTIAL_BLOCKS) * (64 + HEAD_GRAD_MAX_NC) * sizeof(float);
+}
 
 extern "C" int ym_head_grad(const float* dhead, int64_t a_total, int64_t a_off, int hw, int64_t m, int nc,
                             uint16_t* dz_box, uint16_t* dz_cls, float* dbias_box, float* dbias_cls, float* workspace,
                             size_t workspace_bytes, void* stream) {
-    YM_CHECK_ARG(nc >= 1 && nc <= 8, "ym_head_grad: nc must be in [1, 8]");
+    YM_CHECK_ARG(nc >= 1 && nc <= HEAD_GRAD_MAX_NC, "ym_head_grad: nc=%d out of range (1..1024)", nc);
     YM_CHECK_ARG(workspace && workspace_bytes >= ym_head_grad_workspace_size(), "ym_head_grad: workspace too small");
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(head_grad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dhead, a_total, a_off, hw, m, nc,
                        dz_box, dz_cls, workspace);
-    if (dbias_box) colsum_launch(workspace, PARTIAL_BLOCKS, 64, 72, dbias_box, 1, st);
-    if (dbias_cls) colsum_launch(workspace + 64, PARTIAL_BLOCKS, nc, 72, dbias_cls, 1, st);
+    const int ncol = 64 + ((nc + 7) & ~7);
+    if (dbias_box) colsum_launch(workspace, PARTIAL_BLOCKS, 64, ncol, dbias_box, 1, st);
+    if (dbias_cls) colsum_launch(workspace + 64, PARTIAL_BLOCKS, nc, ncol, dbias_cls, 1, st);
     YM_LAUNCH_CHECK("ym_head_grad");
     return YM_OK;
 }

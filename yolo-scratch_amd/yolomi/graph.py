@@ -717,10 +717,11 @@ class HeadLevel:
         self.nc = no - 64
         self.HW, self.M = xb.H * xb.W, B * xb.H * xb.W
         self.wb_f, self.wb_t = plan.weights.add(box_conv.weight, need_t=True)
-        self.wc_f, self.wc_t = plan.weights.add(cls_conv.weight, need_t=True, cout_t=8)
+        ncp = (self.nc + 7) // 8 * 8          # class gradient rows padded to 8 channels (ym_head_grad)
+        self.wc_f, self.wc_t = plan.weights.add(cls_conv.weight, need_t=True, cout_t=ncp)
         self.dzb = torch.empty(self.M, 64, dtype=BF16, device=plan.dev)
-        self.dzc = torch.empty(self.M, 8, dtype=BF16, device=plan.dev)
-        self.wsc = torch.empty(8, xc.c, dtype=F32, device=plan.dev)
+        self.dzc = torch.empty(self.M, ncp, dtype=BF16, device=plan.dev)
+        self.wsc = torch.empty(ncp, xc.c, dtype=F32, device=plan.dev)
 
         def desc(x, cout, y_bs, y_ld, out_f32):
             d = ConvDesc()
@@ -731,7 +732,7 @@ class HeadLevel:
         self.fb = desc(xb, 64, A * no, no, 1)
         self.fc = desc(xc, self.nc, A * no, no, 1)
         self.bb = desc(xb, 64, self.HW * 64, 64, 0)
-        self.bc = desc(xc, 8, self.HW * 8, 8, 0)
+        self.bc = desc(xc, ncp, self.HW * ncp, ncp, 0)
         plan.need_wgrad_ws(self.bb)
         plan.need_wgrad_ws(self.bc)
 
