@@ -84,6 +84,9 @@ def test_model_80_classes_train_step_and_eval():
         y, _ = m(b["img"])
     torch.cuda.synchronize()
     assert tuple(y.shape) == (2, 4 + nc, 20 * 20 + 10 * 10 + 5 * 5) and torch.isfinite(y).all(), y.shape
+    from yolomi.post import decode_nms
+    dets = decode_nms(y.transpose(1, 2), 160, 0.001, 0.7)      # 80 class columns through the batched decode + NMS
+    assert len(dets) == 2
     from yolomi._lib import YolomiError
     m3 = build_yolo11(cfg, ch=3, nc=nc).cuda().train()
     with pytest.raises(YolomiError, match="ch=1"):
