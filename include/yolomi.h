@@ -12,9 +12,10 @@
  *  - All pointers are DEVICE pointers unless stated; buffers are allocated by
  *    the caller (PyTorch caching allocator); the library never allocates or
  *    frees caller memory and keeps no TENSOR state between calls.  The only
- *    process-wide state is configuration: the conv kernel selection policies
- *    (ym_conv_set_halo / ym_conv_set_pipe / ym_conv_set_direct); it never changes a result
- *    beyond fp32 summation order.  The library reads no environment variables.
+ *    process-wide state is configuration: the kernel selection policies, whose
+ *    override setters live in yolomi_experimental.h (tests / tuning only, atomic, see the contract
+ *    there); a policy never changes a result beyond fp32 summation order.  The library reads no
+ *    environment variables.
  *  - `stream` is a hipStream_t (0 = legacy default stream); every call is
  *    asynchronous on it and performs no device-wide synchronisation.
  *  - Activations are NHWC.  An "activation view" is (base pointer, batch
@@ -156,30 +157,6 @@ int ym_conv_algo(const ym_conv_desc* d, int dgrad);
  * returns an id (algo x 1000 + template instance; weight gradients >= 10000; -1 for a bad argument) and,
  * if name != NULL, writes its name (e.g. "direct v3", "pipe 256x128", "wgrad3 s2 64x64 8x8 deep"). */
 int ym_conv_kernel(const ym_conv_desc* d, int dir, char* name, int name_len);
-/* Kernel selection as if the batch held n images (0: the real batch, the default): every size rule
- * and tile choice below evaluates at n, the launch geometry at the real batch — a small-batch parity
- * test runs the kernel instances of a large-batch step.  Returns the previous setting.  Process-wide;
- * not for use while other threads plan or launch convolutions. */
-int ym_conv_set_select_batch(int n);
-/* Selection policy of the halo-staged kernel for later calls: -1 default, 0 never, 1 wherever it
- * applies, 2 maps <= 24 wide, 3 (default) maps <= 48 wide or <= 64 output channels.  Returns the
- * previous setting.  Process-wide; not for use while other threads launch convolutions. */
-int ym_conv_set_halo(int mode);
-/* Selection policy of the persistent pipelined implicit GEMM (conv_pipe.hip) for later calls: -1
- * default, 0 never, 1 layers of >= 1024 256-pixel tiles with >= 128 output channels, 2 every eligible
- * layer of >= 256 tiles, 3 (default) every 1x1 and the 3x3 with >= 128 output channels (forward: or
- * inputs) at >= 256 tiles, never a stride-2 data gradient.  Returns the previous setting.
- * Process-wide, like ym_conv_set_halo. */
-int ym_conv_set_pipe(int mode);
-/* Selection policy of the direct register-weight kernel (conv_direct.hip: 32-128-channel 1x1 / 3x3
- * layers) for later calls: -1 default, 0 never, 1 maps of >= 1 M output pixels (default), 2 any size, 3 >= 200 k
- * output pixels.
- * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
-int ym_conv_set_direct(int mode);
-/* Selection policy of the halo-staged pipelined 3x3 stride-1 kernel (conv_hpipe.hip: 16x16-pixel tiles,
- * each 64-channel chunk of the 18x18 input halo staged once for all nine taps): -1 default, 0 never,
- * 1 the weight-resident 64 -> 64 layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
-int ym_conv_set_hpipe(int mode);
 /* y = conv(x, w) (+bias), x fp16 NHWC view, w fp16 [cout][kh][kw][cin], k in 1..3; optional per-block
  * channel sum / sum-of-squares partials [ym_conv_fwd_stat_rows(d)][cout] for training BatchNorm
  * (BatchNorm2d batch stats; not together with a bias).  accumulate is not supported for fp16 output
@@ -193,26 +170,23 @@ int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt,
  * `workspace` (ym_conv_wgrad_workspace_size bytes) and are reduced by the library: no atomics
  * into, and no zero-fill of, dw_oihw.  dz bf16 with the y_* view, x fp16 with the x_* view. */
 size_t ym_conv_wgrad_workspace_size(const ym_conv_desc* d);
-/* Workgroups per weight-gradient launch the split-K plan aims for (default 256, tuned in the training step where
- * the weight gradients share the GPU with the data gradients; <= 0 restores it).  Returns the previous setting.
- * Process-wide, like ym_conv_set_halo; a workspace size queried under one setting serves only that setting. */
-int ym_wgrad_set_target(int wgs);
 int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* x, void* workspace,
                   size_t workspace_bytes, float* dw_oihw, int accumulate, void* stream);
-/* Stem conv (cin = 1, 3x3) on the fp32 image (model.0, yaml row 0); y = NULL: statistics only. */
+/* Stem conv (3x3) on the fp32 NCHW image of ch = 1..4 planes (model.0, yaml row 0: Conv(ch, c, 3, 2); the reference's
+ * build_yolo11(ch=...), models/yolo11_model.py:23, 258); y = NULL: statistics only. */
 int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq, int n,
-                      int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks, void* stream);
+                      int h, int w, int oh, int ow, int cout, int stride, int pad, int ch, int blocks, void* stream);
 /* Eval-mode stem Conv block in one launch (inference): the stem conv, BatchNorm with the running-statistics scale /
  * shift, SiLU if act, written into the fp16 activation view y (strides y_bs / y_ld, multiples of 8, y 16-B aligned)
  * — what ym_conv_first_fwd + ym_bn_apply compute, without the statistics, the fp16 z and the apply launch. */
 int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, const float* scale, const float* shift, int act,
                            uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh, int ow, int cout,
-                           int stride, int pad, void* stream);
-/* dW (+)= stem weight gradient; per-workgroup partials in `workspace`
- * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). cout <= 128. */
-size_t ym_conv_first_wgrad_workspace_size(int cout);
+                           int stride, int pad, int ch, void* stream);
+/* dW (+)= stem weight gradient (ch image planes); per-workgroup partials in `workspace`
+ * (ym_conv_first_wgrad_workspace_size bytes), summed in a fixed order (bit-reproducible). */
+size_t ym_conv_first_wgrad_workspace_size(int cout, int ch);
 int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh, int ow,
-                        int cout, int stride, int pad, float* workspace, size_t workspace_bytes, void* stream);
+                        int cout, int stride, int pad, int ch, float* workspace, size_t workspace_bytes, void* stream);
 size_t ym_stem_bwd_wgrad_workspace_size(int cout);
 /* Stored-z stem backward: dz = BatchNorm-backward apply of dy on the STORED fp16 z (dense
  * [m][cout]) straight into the weight-gradient partials (dz never written) — replaces
@@ -273,9 +247,6 @@ typedef struct {
 int ym_conv_fwd_bn_fused(const ym_conv_desc* d);
 int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, float* stat_sum,
                    float* stat_sq, const ym_bn_fold* bn, void* stream);
-/* Fold policy of ym_conv_fwd_bn for later calls: -1 default (on), 0 never (conv, then ym_bn_finalize), 1 on.
- * Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
-int ym_conv_set_fold(int mode);
 int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c, double count, const float* gamma,
                    const float* beta, float* running_mean, float* running_var, int64_t* num_batches_tracked,
                    float momentum, float eps, float* scale, float* shift, float* mean, float* rstd, void* workspace,
@@ -288,31 +259,12 @@ int ym_bn_finalize(const float* part_sum, const float* part_sq, int parts, int c
  * of 4).  ym_conv_fwd_eval_ok(d) is 1 where the kernel this conv selects has the eval epilogue (the halo-staged 3x3
  * kernel's 4-wave tile, the 2-stage implicit GEMM); elsewhere run ym_conv_fwd + ym_bn_apply.  Bias-free convs only. */
 int ym_conv_fwd_eval_ok(const ym_conv_desc* d);
-/* Stage / ring configuration of ym_conv_fwd_eval's implicit GEMM (0: 32-deep K stages x 3, 1: 64 x 3 (default),
- * 2: 64 x 4); <0 restores the default.  Returns the previous setting.  Process-wide, like ym_conv_set_halo. */
-int ym_conv_set_eval_cfg(int cfg);
-/* Eval GEMM outputs of <= 32 channels on a 128 x 32 tile (1, default; <0 restores it) or the 128 x 64 one (0).
- * Returns the previous setting. */
-int ym_conv_set_eval_narrow(int on);
 /* Small grids (a bs-1 forward's late layers: a few dozen tiles, each walking a long K serially) run as a K-split: the
  * GEMM launch writes ks fp32 partial slices into the caller's workspace and a second launch applies BatchNorm / SiLU /
  * residual to their sum.  ym_conv_fwd_eval_workspace_size(d) is the workspace that takes (0: one launch); with a
- * NULL or smaller workspace the call runs unsplit.  ym_conv_set_eval_split(max_tiles): split layers of <= max_tiles
- * 128x64 tiles and >= 12 K stages (default 64; 0 never; <0 restores the default); returns the previous setting.
- * Process-wide, like ym_conv_set_halo; a workspace size queried under one setting serves only that setting. */
+ * NULL or smaller workspace the call runs unsplit.  By default layers of <= 64 128x64 tiles and >= 12 K stages split
+ * (yolomi_experimental.h ym_conv_set_eval_split); a workspace size holds for the policy it was queried under. */
 size_t ym_conv_fwd_eval_workspace_size(const ym_conv_desc* d);
-int ym_conv_set_eval_split(int max_tiles);
-/* The K-split's K-stage threshold (split layers of >= min_stages 64-deep stages; default 12; <0 restores it) and the
- * tile count at or below which an eval conv the halo kernel would take runs the 2-stage GEMM instead (default 0). */
-int ym_conv_set_eval_split_nk(int min_stages);
-/* Layers the pipelined implicit GEMM takes (>= 256 tiles: large maps / batches) run its eval instance (1, default;
- * <0 restores it) or, with 0, are not eval-epilogue cases (ym_conv_fwd + ym_bn_apply). */
-int ym_conv_set_eval_pipe(int on);
-/* Layers whose training kernel has no eval instance, run through one anyway (bit mask; default 0; <0 restores it):
- * bit 0 the halo kernel's 8-wave tile -> the 2-stage GEMM's eval instance, bit 1 the halo-pipelined 3x3 kernel ->
- * the halo C4 / 2-stage GEMM eval instances.  Returns the previous setting. */
-int ym_conv_set_eval_route(int mask);
-int ym_conv_set_eval_gemm_tiles(int max_tiles);
 int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, const float* scale,
                      const float* shift, int act, const uint16_t* res, int64_t r_bs, int64_t r_ld, uint16_t* y,
                      void* workspace, size_t workspace_bytes, void* stream);
@@ -347,10 +299,6 @@ int ym_bn_bwd_reduce_fold(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const 
                           const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                           float* part_sum, float* part_dot, const float* gamma, float* dgamma, float* dbeta,
                           int accumulate, float* coef, void* workspace, void* stream);
-/* Policy of the fused backward statistics + finalize for later calls: -1 default (= 2), 0 never, 1 on maps up
- * to 25600 pixels (20x20 x 64 images), 2 up to 102400 (40x40 x 64).  Returns the previous setting.  Process-wide,
- * like ym_conv_set_halo. */
-int ym_bn_set_bwd_fold(int mode);
 int ym_bn_bwd_apply(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c, int hw,
                     const float* scale, const float* shift, const float* mean, const float* rstd, int act,
                     const float* coef, uint16_t* dz, void* stream);

@@ -188,14 +188,16 @@ def test_eval_forward_one_launch_blocks_vs_unfused(scale_name, imgsz, bs, monkey
         assert err <= 2e-2 * mag + 1e-2, (err, mag)
 
 
-@pytest.mark.parametrize("n,h,w,cout,act", [(1, 64, 64, 32, 1), (2, 37, 41, 16, 1), (1, 20, 20, 64, 0), (1, 30, 30, 96, 1)])
-def test_conv_first_fwd_eval_vs_torch(n, h, w, cout, act):
-    """ym_conv_first_fwd_eval — the stem Conv block (ch 1 -> cout, 3x3 s2 on the fp32 image) with the eval BatchNorm and
-    SiLU in one launch, into a channel slice of a wider buffer, vs torch fp32 (fp16 output rounding)."""
+@pytest.mark.parametrize("n,h,w,cout,act,ch", [(1, 64, 64, 32, 1, 1), (2, 37, 41, 16, 1, 1), (1, 20, 20, 64, 0, 1),
+                                               (1, 30, 30, 96, 1, 1), (2, 33, 40, 32, 1, 3), (1, 24, 24, 256, 0, 4),
+                                               (1, 17, 19, 16, 1, 2)])
+def test_conv_first_fwd_eval_vs_torch(n, h, w, cout, act, ch):
+    """ym_conv_first_fwd_eval — the stem Conv block (ch image planes -> cout, 3x3 s2 on the fp32 NCHW image) with the
+    eval BatchNorm and SiLU in one launch, into a channel slice of a wider buffer, vs torch fp32 (fp16 output rounding)."""
     from yolomi._lib import call, stream_ptr
     g = torch.Generator().manual_seed(n * 1000 + h + cout)
-    img = torch.rand(n, 1, h, w, generator=g)
-    wt = torch.randn(cout, 1, 3, 3, generator=g) / 3
+    img = torch.rand(n, ch, h, w, generator=g)
+    wt = torch.randn(cout, ch, 3, 3, generator=g) / (3 * ch ** 0.5)
     scale = torch.rand(cout, generator=g) + 0.5
     shift = torch.randn(cout, generator=g) * 0.2
     ref = F.conv2d(img, wt, stride=2, padding=1).permute(0, 2, 3, 1) * scale + shift
@@ -208,7 +210,7 @@ def test_conv_first_fwd_eval_vs_torch(n, h, w, cout, act):
     imgd, wd, scd, shd = img.to(dev), wt.to(dev), scale.to(dev), shift.to(dev)
     torch.cuda.synchronize()
     call("ym_conv_first_fwd_eval", imgd.data_ptr(), wd.data_ptr(), scd.data_ptr(), shd.data_ptr(), act,
-         buf[..., 8:].data_ptr(), oh * ow * ld, ld, n, h, w, oh, ow, cout, 2, 1, stream_ptr(dev))
+         buf[..., 8:].data_ptr(), oh * ow * ld, ld, n, h, w, oh, ow, cout, 2, 1, ch, stream_ptr(dev))
     torch.cuda.synchronize()
     out = buf.float().cpu()
     assert torch.all(out[..., :8] == 7.0) and torch.all(out[..., 8 + cout:] == 7.0), "channels outside the view written"

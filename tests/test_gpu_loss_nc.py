@@ -52,8 +52,9 @@ def test_fused_loss_class_counts_vs_oracle(nc):
 def test_model_80_classes_train_step_and_eval():
     """An 80-class model through the HIP path (ym_head_grad's class rows padded to 8-channel groups): the fused loss
     on the network's own heads equals the oracle's v8_loss on the same heads (1e-4), every gradient is finite, and the
-    eval forward decodes (B, 4 + 80, A) finite rows.  Input stays 1-channel, as every reference entry point builds
-    it (yolo11_model.py:23, :258 ch=1); a 3-channel image is refused loudly by the stem."""
+    eval forward decodes (B, 4 + 80, A) finite rows (gradients vs the oracle at nc = 80: test_gpu_network.py
+    test_model_80_classes_train_step_vs_oracle).  An image whose plane count differs from the model's ch is refused
+    with the reference's Conv2d message."""
     ch = 1
     import yaml
     from pathlib import Path
@@ -88,6 +89,5 @@ def test_model_80_classes_train_step_and_eval():
     dets = decode_nms(y.transpose(1, 2), 160, 0.001, 0.7)      # 80 class columns through the batched decode + NMS
     assert len(dets) == 2
     from yolomi._lib import YolomiError
-    m3 = build_yolo11(cfg, ch=3, nc=nc).cuda().train()
-    with pytest.raises(YolomiError, match="ch=1"):
-        m3(torch.rand(1, 3, 64, 64, device="cuda"))
+    with pytest.raises(YolomiError, match="to have 1 channels, but got 3 channels"):
+        m(torch.rand(1, 3, 64, 64, device="cuda"))

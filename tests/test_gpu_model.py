@@ -76,12 +76,12 @@ def _batch(d, dev="cuda"):
             "cls": torch.from_numpy(d["cls"]).to(dev), "bboxes": torch.from_numpy(d["bboxes"]).to(dev)}
 
 
-def _seeded_model(scale):
+def _seeded_model(scale, nc=5, ch=1):
     from oracle import model as om
     from models import build_yolo11
     cfg = om.load_cfg(scale)
-    layers, save, P = om.build(cfg)
-    m = build_yolo11(cfg, ch=1, nc=5)
+    layers, save, P = om.build(cfg, ch=ch, nc=nc)
+    m = build_yolo11(cfg, ch=ch, nc=nc)
     m.load_state_dict(P)
     return m.cuda()
 
@@ -290,10 +290,10 @@ def test_sppf_fused_chain_bit_identical(H, W, C, B):
     assert torch.equal(gbuf, gref)
 
 
-def _emulated_heads(scale, img):
+def _emulated_heads(scale, img, nc=5, ch=1):
     from oracle import model as om
     from oracle.precision import hip_storage_rounding
-    layers, save, P = om.build(om.load_cfg(scale))
+    layers, save, P = om.build(om.load_cfg(scale), ch=ch, nc=nc)
     with torch.no_grad(), hip_storage_rounding():
         return om.forward(P, layers, save, torch.as_tensor(img), training=True)
 

@@ -189,3 +189,44 @@ def test_two_forwards_before_one_backward():
         keep = y1.clone()
         m(b1["img"] * 0.5)
     assert torch.equal(y1, keep)                       # eval outputs are not overwritten by the next forward
+
+
+class _BatchSet(torch.utils.data.Dataset):
+    """Whole synthetic batches as dataset items (a DataLoader with batch_size=None hands them over as they are)."""
+
+    def __init__(self, n, batch, imgsz, seed):
+        self.n, self.batch, self.imgsz, self.seed = n, batch, imgsz, seed
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        from datasets.synthetic import synth_batch
+        return synth_batch(self.batch, self.imgsz, self.seed + i)
+
+
+def test_validate_through_pinned_worker_loader_with_eval_graph():
+    """validate() as main() runs it: a DataLoader with worker processes, pin_memory=True and persistent workers
+    (make_loaders, train_yolo11_cuda.py:226) whose pin-memory thread is live while the eval forward is captured as a
+    HIP graph on the 2nd batch and replayed on the 3rd-5th (yolomi/graph.py Plan._replay, thread_local capture mode).
+    The metrics and the loss equal validate() over the same batches with the graph off (eager every batch)."""
+    import os
+    import train_yolo11_cuda as T
+    from losses import v8DetectionLoss
+    m = _model()
+    crit = v8DetectionLoss(m)
+    ds = _BatchSet(5, 2, 256, seed=60)
+    loader = torch.utils.data.DataLoader(ds, batch_size=None, num_workers=2, pin_memory=True, persistent_workers=True,
+                                         prefetch_factor=2)
+    dev = torch.device("cuda")
+    got = T.validate(m, loader, crit, dev, conf_threshold=1e-7, iou_threshold=0.45)
+    plan = next(p for k, v in m.__dict__["_ym_plans"].items() if not k[-1] for p in v)
+    assert "fwd" in plan.__dict__.get("_graphs", {}), "the eval forward was not captured inside validate()"
+    got2 = T.validate(m, loader, crit, dev, conf_threshold=1e-7, iou_threshold=0.45)     # replay only
+    os.environ["YM_EVAL_GRAPH"] = "0"
+    try:
+        want = T.validate(m, torch.utils.data.DataLoader(ds, batch_size=None), crit, dev, conf_threshold=1e-7,
+                          iou_threshold=0.45)
+    finally:
+        os.environ.pop("YM_EVAL_GRAPH", None)
+    assert got == want and got2 == want, (got, got2, want)

@@ -597,7 +597,7 @@ extern "C" int ym_bn_bwd_finalize(const float* part_sum, const float* part_dot, 
 }
 
 // fused backward statistics + finalize policy (ym_bn_set_bwd_fold): -1 default (= 2), 0 off, 1 / 2 on (map size caps)
-static int g_bwd_fold = -1;
+static Policy g_bwd_fold{-1};
 // the maps it takes: whole 64-channel groups and at most 25600 pixels = 20x20 x 64 images on 64 workgroups per group
 // (on larger maps 64 workgroups per group streamed the tensor slower than the streaming kernel's 512 full-width ones:
 // 40x40 -0.5 %, profiles/r04/bn_bwd_fold_ab.txt); by default (round 5) it also takes <= 102400 pixels (40x40 x 64
@@ -619,9 +619,7 @@ extern "C" int ym_bn_bwd_fold_ok(int64_t m, int c) {
 extern "C" int ym_bn_set_bwd_fold(int mode) {
     // fused backward statistics + finalize: -1 default (= 2), 0 off, 1 on up to 25600 pixels, 2 up to 102400;
     // returns the previous setting
-    const int prev = g_bwd_fold;
-    g_bwd_fold = mode < -1 || mode > 2 ? -1 : mode;
-    return prev;
+    return g_bwd_fold.set(mode < -1 || mode > 2 ? -1 : mode);
 }
 
 extern "C" int ym_bn_bwd_reduce_fold(const uint16_t* dy, int64_t d_bs, int64_t d_ld, const uint16_t* z, int64_t m, int c,

@@ -6,7 +6,10 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <atomic>
+
 #include "../../include/yolomi.h"
+#include "../../include/yolomi_experimental.h"
 
 namespace ym {
 
@@ -32,11 +35,27 @@ void set_error(const char* fmt, ...);
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// A process-wide selection policy behind a yolomi_experimental.h setter: an atomic int (a setter racing a launch
+// is a data race no more — the launch sees the old or the new value, whole); every store bumps g_policy_gen, so a
+// caller that caches a policy-dependent answer (ym_conv_fwd_eval_ok, a workspace size) can tell it went stale
+// (ym_policy_generation).  Reads are relaxed: a policy orders nothing but itself.
+extern std::atomic<unsigned> g_policy_gen;
+struct Policy {
+    std::atomic<int> v;
+    explicit constexpr Policy(int x) : v(x) {}
+    operator int() const { return v.load(std::memory_order_relaxed); }
+    int set(int x) {
+        const int prev = v.exchange(x, std::memory_order_relaxed);
+        g_policy_gen.fetch_add(1, std::memory_order_relaxed);
+        return prev;
+    }
+};
+
 // Conv kernel selection batch (ym_conv_set_select_batch): when > 0 the selection rules of every conv
 // kernel (size thresholds, tile shapes) evaluate as if the batch held this many images, while the
 // launch geometry still follows the real batch — so a small-batch parity test runs exactly the kernel
 // instances a large-batch training step selects.  0 (the default): the real batch.
-extern int g_select_n;
+extern Policy g_select_n;
 static inline int64_t select_n(const ym_conv_desc* d) { return g_select_n > 0 ? int64_t(g_select_n) : int64_t(d->n); }
 
 // the weight-gradient kernel instance ym_conv_wgrad runs for d (wgrad.hip; ym_conv_kernel dir 2)

@@ -38,7 +38,8 @@
 #include "tile.h"
 
 namespace ym {
-int g_select_n = 0;
+Policy g_select_n{0};
+std::atomic<unsigned> g_policy_gen{0};
 
 namespace {
 
@@ -473,25 +474,44 @@ conv_gemm_kernel(GemmArgs a, EvalArgs e) {
     }
 }
 
-// ------------------------------------------------------------------ stem conv (Cin = 1), fp32 image input
-// one thread per (output pixel, 8 channels), the 8x9 weights in registers, 32-bit index math
-// (N*OH*OW and N*H*W < 2^31, checked on the host).  HBM-bound: writes the fp16 z (2 B/elem).
+// ------------------------------------------------------------------ stem conv (Cin = CH image planes), fp32 image input
+// one thread per (output pixel, 8 channels), the 8 x 9CH weights in registers, 32-bit index math
+// (N*OH*OW and N*CH*H*W < 2^31, checked on the host).  HBM-bound: writes the fp16 z (2 B/elem).
+// The image is the reference's NCHW (B, CH, H, W) fp32 tensor; tap t = ci * 9 + kh * 3 + kw is the OIHW weight order,
+// and the sum runs over t in that order (CH = 1: the crater config's single plane).
 // Channel pieces (these small VALU kernels): a launch covers channels c_base .. c_base + Cout of a Ct-channel layer,
 // Cout / 8 a power of two <= 64 (the lane-group reductions); a width like the x-scale stem's 96 runs as pieces 64 + 32
 // (ch_pieces below), rows / partial rows strided by Ct.
+template <int CH>
+__device__ __forceinline__ void stem_patch(const float* __restrict__ img, int n, int H, int W, int oh, int ow,
+                                           int stride, int pad, float* patch) {
+#pragma unroll
+    for (int ci = 0; ci < CH; ++ci)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
+                patch[ci * 9 + kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
+                                                  ? img[((n * CH + ci) * H + ih) * W + iw] : 0.f;
+            }
+}
+
+template <int CH>
 __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                              uint16_t* __restrict__ y, float* __restrict__ st_sum,
                                                              float* __restrict__ st_sq, int N, int H, int W, int OH,
                                                              int OW, int Cout, int stride, int pad, int c_base,
                                                              int Ct) {
+    constexpr int T = 9 * CH;
     __shared__ float red[2][512];
     const int G = Cout >> 3;                 // channel groups (divides 64)
     const int g = threadIdx.x % G;
-    float wr[8][9];
+    float wr[8][T];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-        for (int t = 0; t < 9; ++t) wr[r][t] = w[(c_base + g * 8 + r) * 9 + t];
+        for (int t = 0; t < T; ++t) wr[r][t] = w[(c_base + g * 8 + r) * T + t];
     float ls[8], lq[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) ls[r] = lq[r] = 0.f;
@@ -499,21 +519,14 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
     const int step = gridDim.x * (256 / G);
     for (int m = (blockIdx.x * 256 + threadIdx.x) / G; m < M; m += step) {
         const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
-        float patch[9];
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                patch[kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
-                                         ? img[(n * H + ih) * W + iw] : 0.f;
-            }
+        float patch[T];
+        stem_patch<CH>(img, n, H, W, oh, ow, stride, pad, patch);
         float v[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
             float s = 0.f;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) s += wr[r][t] * patch[t];
+            for (int t = 0; t < T; ++t) s += wr[r][t] * patch[t];
             v[r] = s;
             ls[r] += s;
             lq[r] += s * s;
@@ -542,18 +555,20 @@ __global__ void __launch_bounds__(256) conv_first_fwd_kernel(const float* __rest
 // eval-mode stem Conv block in one launch (ym_conv_first_fwd_eval): one thread per output pixel and ALL its channels
 // (the weights, scale and shift broadcast from LDS), the running-statistics BatchNorm + SiLU on the fp32 sums
 // (EvalEpi's arithmetic, the training kernel's summation order) and 16-B stores of the pixel's contiguous channel
-// run — a wave writes 64 whole pixel rows; the 9 image reads are made once per pixel, not once per 8 channels.
-// No statistics, no fp16 z, no apply launch.  Cout % 8 == 0, Cout <= 512.
+// run — a wave writes 64 whole pixel rows; the 9 CH image reads are made once per pixel, not once per 8 channels.
+// No statistics, no fp16 z, no apply launch.  Cout % 8 == 0, Cout <= 512 (CH = 1, 2), <= 256 (CH = 3, 4).
+template <int CH>
 __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __restrict__ img, const float* __restrict__ w,
                                                               const float* __restrict__ sc, const float* __restrict__ sh,
                                                               int act, uint16_t* __restrict__ y, int64_t y_bs,
                                                               int64_t y_ld, int N, int H, int W, int OH, int OW,
                                                               int Cout, int stride, int pad) {
+    constexpr int T = 9 * CH;
     // weights tap-major in LDS ([t][c]: 8 channels of one tap = two 16-B broadcast reads)
-    __shared__ __attribute__((aligned(16))) float wl[512 * 9];
+    __shared__ __attribute__((aligned(16))) float wl[(CH <= 2 ? 512 : 256) * T];
     __shared__ __attribute__((aligned(16))) float sl[512], hl[512];
-    for (int i = threadIdx.x; i < Cout * 9; i += 256) {
-        const int c = i / 9, t = i - c * 9;
+    for (int i = threadIdx.x; i < Cout * T; i += 256) {
+        const int c = i / T, t = i - c * T;
         wl[t * Cout + c] = w[i];
     }
     for (int i = threadIdx.x; i < Cout; i += 256) {
@@ -564,20 +579,13 @@ __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __res
     const int M = N * OH * OW, OHW = OH * OW;
     for (int m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
         const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
-        float patch[9];
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-            for (int kw = 0; kw < 3; ++kw) {
-                const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                patch[kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
-                                         ? img[(n * H + ih) * W + iw] : 0.f;
-            }
+        float patch[T];
+        stem_patch<CH>(img, n, H, W, oh, ow, stride, pad, patch);
         uint16_t* yp = y + int64_t(n) * y_bs + int64_t(pix) * y_ld;
         for (int c0 = 0; c0 < Cout; c0 += 8) {
             float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {                        // tap order per channel: the training kernel's sum
+            for (int t = 0; t < T; ++t) {                        // tap order per channel: the training kernel's sum
                 const float4 w0 = *reinterpret_cast<const float4*>(wl + t * Cout + c0);
                 const float4 w1 = *reinterpret_cast<const float4*>(wl + t * Cout + c0 + 4);
                 const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
@@ -605,37 +613,32 @@ __global__ void __launch_bounds__(256) conv_first_eval_kernel(const float* __res
 
 // part[block][co*9 + t] = sum over the block's pixels p of dz[p][co] * patch(p)[t]  (no dgrad: the
 // image needs no gradient); dW += the rows summed in order (colsum_kernel)
+template <int CH>
 __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __restrict__ dz, const float* __restrict__ img,
                                                                float* __restrict__ part, int N, int H, int W, int OH,
                                                                int OW, int Cout, int stride, int pad, int c_base,
                                                                int Ct) {
-    __shared__ float red[128 * 9];
+    constexpr int T = 9 * CH;
+    __shared__ float red[128 * T];
     const int G = Cout >> 3;
     const int g = threadIdx.x % G;
-    float acc[8][9];
+    float acc[8][T];
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-        for (int t = 0; t < 9; ++t) acc[r][t] = 0.f;
+        for (int t = 0; t < T; ++t) acc[r][t] = 0.f;
     const int M = N * OH * OW, OHW = OH * OW;
     const int step = gridDim.x * (256 / G);
     // two pixels per iteration (loads of both first); accumulation order unchanged (m, m + step, ...)
     for (int m0 = (blockIdx.x * 256 + threadIdx.x) / G; m0 < M; m0 += 2 * step) {
         uint4 d[2];
-        float xv[2][9];
+        float xv[2][T];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int m = m0 + u * step < M ? m0 + u * step : m0;
             const int n = m / OHW, pix = m - n * OHW, oh = pix / OW, ow = pix - oh * OW;
             d[u] = *reinterpret_cast<const uint4*>(dz + size_t(m) * Ct + c_base + g * 8);
-#pragma unroll
-            for (int kh = 0; kh < 3; ++kh)
-#pragma unroll
-                for (int kw = 0; kw < 3; ++kw) {
-                    const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-                    xv[u][kh * 3 + kw] = (unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W))
-                                             ? img[(n * H + ih) * W + iw] : 0.f;
-                }
+            stem_patch<CH>(img, n, H, W, oh, ow, stride, pad, xv[u]);
         }
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
@@ -648,7 +651,7 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
                 gv[2 * e + 1] = bf2f(bf16_t(dd[e] >> 16));
             }
 #pragma unroll
-            for (int t = 0; t < 9; ++t)
+            for (int t = 0; t < T; ++t)
 #pragma unroll
                 for (int r = 0; r < 8; ++r) acc[r][t] += gv[r] * xv[u][t];
         }
@@ -656,10 +659,10 @@ __global__ void __launch_bounds__(256) conv_first_wgrad_kernel(const bf16_t* __r
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
+        for (int t = 0; t < T; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
-    ordered_wave_add72(red, acc, g, G);
-    for (int i = threadIdx.x; i < Cout * 9; i += 256) part[int64_t(blockIdx.x) * Ct * 9 + c_base * 9 + i] = red[i];
+    ordered_wave_add_taps<T>(red, acc, g, G);
+    for (int i = threadIdx.x; i < Cout * T; i += 256) part[int64_t(blockIdx.x) * Ct * T + c_base * T + i] = red[i];
 }
 
 // ------------------------------------------------------------------ depthwise 3x3, stride 1, pad 1
@@ -854,7 +857,7 @@ __global__ void __launch_bounds__(256) dw3x3_bwd_kernel(DwArgs a, const bf16_t* 
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
-    ordered_wave_add72(red, acc, g, G);
+    ordered_wave_add_taps<9>(red, acc, g, G);
     for (int i = threadIdx.x; i < 9 * a.C; i += 256) part[int64_t(blockIdx.x) * 9 * a.Ct + 9 * a.c_base + i] = red[i];
 }
 
@@ -1127,42 +1130,32 @@ extern "C" int ym_conv_stat_blocks(int64_t M, int Cout) {
 
 extern "C" int ym_conv_set_select_batch(int n) {
     // kernel selection as if the batch held n images (0: the real batch); returns the previous setting
-    const int prev = g_select_n;
-    g_select_n = n > 0 ? n : 0;
-    return prev;
+    return g_select_n.set(n > 0 ? n : 0);
 }
 
 extern "C" int ym_conv_set_halo(int mode) {
     // selection policy of the halo-staged 3x3 kernel: -1 default, 0 never, 1 wherever it applies,
     // 2 where it measured faster in the step (the default), 3 the wider per-layer rule; returns the
     // previous setting
-    const int prev = g_halo_force;
-    g_halo_force = mode < -1 || mode > 3 ? -1 : mode;
-    return prev;
+    return g_halo_force.set(mode < -1 || mode > 3 ? -1 : mode);
 }
 
 extern "C" int ym_conv_set_pipe(int mode) {
     // selection policy of the pipelined implicit GEMM: -1 default, 0 never, 1 layers of >= 1024
     // tiles (default), 2 >= 256 tiles; returns the previous setting
-    const int prev = g_pipe_force;
-    g_pipe_force = mode < -1 || mode > 3 ? -1 : mode;
-    return prev;
+    return g_pipe_force.set(mode < -1 || mode > 3 ? -1 : mode);
 }
 
 extern "C" int ym_conv_set_direct(int mode) {
     // selection policy of the direct register-weight kernel: -1 default, 0 never, 1 maps of
     // >= 1 M output pixels (default), 2 any size, 3 >= 200 k output pixels; returns the previous setting
-    const int prev = g_direct_force;
-    g_direct_force = mode < -1 || mode > 3 ? -1 : mode;
-    return prev;
+    return g_direct_force.set(mode < -1 || mode > 3 ? -1 : mode);
 }
 
 extern "C" int ym_conv_set_hpipe(int mode) {
     // selection policy of the halo-staged pipelined 3x3 kernel: -1 default, 0 never, 1 eligible layers of
     // >= 512 tiles (default), 2 every eligible layer; returns the previous setting
-    const int prev = g_hpipe_force;
-    g_hpipe_force = mode < -1 || mode > 2 ? -1 : mode;
-    return prev;
+    return g_hpipe_force.set(mode < -1 || mode > 2 ? -1 : mode);
 }
 
 extern "C" int ym_conv_algo(const ym_conv_desc* d, int dgrad) {
@@ -1230,7 +1223,7 @@ extern "C" int ym_conv_fwd_stat_rows(const ym_conv_desc* d) {
 }
 
 // ym_conv_fwd_bn's fold policy (ym_conv_set_fold): -1 default (on), 0 off, 1 on
-static int g_fold_mode = -1;
+static Policy g_fold_mode{-1};
 
 // fold: the BatchNorm finalize as the pipelined kernel's tail (ym_conv_fwd_bn), null elsewhere
 static int conv_fwd_impl(const ym_conv_desc* d, const uint16_t* x, const uint16_t* w, void* y, const float* bias,
@@ -1331,22 +1324,18 @@ extern "C" int ym_conv_fwd_bn(const ym_conv_desc* d, const uint16_t* x, const ui
 // the eval GEMM's K stage x ring (ym_conv_set_eval_cfg): 0: 32-deep stages, 3-stage ring (the training 128x64 tile's),
 // 1: 64-deep x 3, 2: 64-deep x 4 — at bs 1 a launch covers a few tiles and walks its whole K serially, so deeper
 // stages halve its DMA round trips (128-deep x 3, one workgroup per CU, measured slower: profiles/r05/eval_split_ab.txt)
-static int g_eval_cfg = 1;
-static int g_eval_narrow = 1;
+static Policy g_eval_cfg{1};
+static Policy g_eval_narrow{1};
 
 extern "C" int ym_conv_set_eval_narrow(int on) {
     // eval GEMM outputs of <= 32 channels on the 128 x 32 tile (1, default; <0 restores it) or the 128 x 64 (0);
     // returns the previous setting
-    const int prev = g_eval_narrow;
-    g_eval_narrow = on < 0 ? 1 : (on ? 1 : 0);
-    return prev;
+    return g_eval_narrow.set(on < 0 ? 1 : (on ? 1 : 0));
 }
 
 extern "C" int ym_conv_set_eval_cfg(int cfg) {
     // the eval GEMM's stage / ring configuration (0..2, -1 default 1); returns the previous setting
-    const int prev = g_eval_cfg;
-    g_eval_cfg = cfg < 0 || cfg > 2 ? 1 : cfg;
-    return prev;
+    return g_eval_cfg.set(cfg < 0 || cfg > 2 ? 1 : cfg);
 }
 
 // K-split on small grids (ym_conv_set_eval_split): a bs-1 late layer is a few dozen 128x64 tiles, each walking a K of
@@ -1354,28 +1343,22 @@ extern "C" int ym_conv_set_eval_cfg(int cfg) {
 // partial slab (EvalArgs.part) and eval_fold_kernel applies BatchNorm / SiLU / residual to the slices' sum — one
 // extra launch (~4 us) for a K walk ks times shorter.  Split where the layer has <= g_eval_split tiles and >= 12 K
 // stages: ks = min(stages / 4, 256 / tiles, 16) (>= 4 stages a slice, <= ~one workgroup per CU).
-static int g_eval_split = 64, g_eval_split_nk = 12, g_eval_gemm_tiles = 0;
+static Policy g_eval_split{64}, g_eval_split_nk{12}, g_eval_gemm_tiles{0};
 
 extern "C" int ym_conv_set_eval_split(int max_tiles) {
     // the eval K-split's tile threshold (0: never split, -1: default 64); returns the previous setting
-    const int prev = g_eval_split;
-    g_eval_split = max_tiles < 0 ? 64 : max_tiles;
-    return prev;
+    return g_eval_split.set(max_tiles < 0 ? 64 : max_tiles);
 }
 
 extern "C" int ym_conv_set_eval_split_nk(int min_stages) {
     // the eval K-split's K-stage threshold (-1: default 12); returns the previous setting
-    const int prev = g_eval_split_nk;
-    g_eval_split_nk = min_stages < 0 ? 12 : min_stages;
-    return prev;
+    return g_eval_split_nk.set(min_stages < 0 ? 12 : min_stages);
 }
 
 extern "C" int ym_conv_set_eval_gemm_tiles(int max_tiles) {
     // eval convs of <= max_tiles 128x64 tiles take the 2-stage GEMM where the halo kernel would run (0: never,
     // -1: default 0); returns the previous setting
-    const int prev = g_eval_gemm_tiles;
-    g_eval_gemm_tiles = max_tiles < 0 ? 0 : max_tiles;
-    return prev;
+    return g_eval_gemm_tiles.set(max_tiles < 0 ? 0 : max_tiles);
 }
 
 static int64_t eval_tiles(const ym_conv_desc* d) {
@@ -1393,7 +1376,9 @@ static int eval_ks(const ym_conv_desc* d) {
     if (g_eval_split == 0 || !eval_gemm_fits(d)) return 1;
     const int64_t M = int64_t(d->n) * d->oh * d->ow;
     const int64_t tiles = ((M + 127) / 128) * ((d->cout + 63) / 64);
-    const int KB = g_eval_cfg == 0 ? 32 : 64;
+    // K stages of the instance ym_conv_fwd_eval launches: the narrow (<= 32-channel) 128 x 32 tile always runs
+    // 64-deep stages, the 128 x 64 one 32-deep under eval cfg 0
+    const int KB = (g_eval_narrow && d->cout <= 32) || g_eval_cfg != 0 ? 64 : 32;
     const int nk = d->k * d->k * ((d->cin + KB - 1) / KB);
     if (tiles > g_eval_split || nk < g_eval_split_nk) return 1;
     const int64_t ks = std::min<int64_t>(std::min<int64_t>(nk / 4, std::max<int64_t>(1, 256 / tiles)), 16);
@@ -1402,25 +1387,21 @@ static int eval_ks(const ym_conv_desc* d) {
 
 // the pipelined forward's eval instance for layers of >= 256 tiles (ym_conv_set_eval_pipe; 0: those layers run
 // ym_conv_fwd + ym_bn_apply)
-static int g_eval_pipe = 1;
+static Policy g_eval_pipe{1};
 
 extern "C" int ym_conv_set_eval_pipe(int on) {
     // the pipelined forward's eval instance on (1, default; -1 restores it) or off (0); returns the previous setting
-    const int prev = g_eval_pipe;
-    g_eval_pipe = on < 0 ? 1 : (on ? 1 : 0);
-    return prev;
+    return g_eval_pipe.set(on < 0 ? 1 : (on ? 1 : 0));
 }
 
 // layers whose training kernel has no eval instance, routed to an eval instance anyway (ym_conv_set_eval_route):
 // bit 0 the halo kernel's 8-wave tile (C8: its eval instance spills) -> the 2-stage GEMM's; bit 1 the halo-pipelined
 // 3x3 kernel -> the halo C4 / GEMM eval instances
-static int g_eval_route = 0;
+static Policy g_eval_route{0};
 
 extern "C" int ym_conv_set_eval_route(int mask) {
     // see g_eval_route (-1: default 0); returns the previous setting
-    const int prev = g_eval_route;
-    g_eval_route = mask < 0 ? 0 : (mask & 3);
-    return prev;
+    return g_eval_route.set(mask < 0 ? 0 : (mask & 3));
 }
 
 static bool eval_layout_ok(const ym_conv_desc* d) {
@@ -1519,9 +1500,7 @@ extern "C" int ym_conv_fwd_eval(const ym_conv_desc* d, const uint16_t* x, const 
 
 extern "C" int ym_conv_set_fold(int mode) {
     // ym_conv_fwd_bn's fold policy: -1 default (on), 0 off, 1 on; returns the previous setting
-    const int prev = g_fold_mode;
-    g_fold_mode = mode < -1 || mode > 1 ? -1 : mode;
-    return prev;
+    return g_fold_mode.set(mode < -1 || mode > 1 ? -1 : mode);
 }
 
 extern "C" int ym_conv_dgrad(const ym_conv_desc* d, const uint16_t* dz, const uint16_t* wt, uint16_t* dx, void* stream) {
@@ -1593,16 +1572,27 @@ static void ch_pieces(int c, int max_groups, F f) {
     }
 }
 
+// the stem kernels' instance for `ch` image planes (1..4: the reference builds ch = 1 for its crater config and any
+// ch through build_yolo11(ch=...), models/yolo11_model.py:23, 258; RGB is 3)
+#define YM_STEM_CH_SWITCH(ch, KERNEL, ...)                                                                         \
+    switch (ch) {                                                                                                  \
+        case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                                                 \
+        case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                                                 \
+        case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                                                 \
+        default: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                                                \
+    }
+
 extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t* y, float* stat_sum, float* stat_sq,
-                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int blocks,
+                                 int n, int h, int w, int oh, int ow, int cout, int stride, int pad, int ch, int blocks,
                                  void* stream) {
     YM_CHECK_ARG(cout % 8 == 0 && cout > 0 && cout <= 4096, "ym_conv_first_fwd: cout=%d unsupported", cout);
-    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+    YM_CHECK_ARG(ch >= 1 && ch <= 4, "ym_conv_first_fwd: ch=%d image planes unsupported (1..4)", ch);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * ch * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd: too many pixels");
     YM_CHECK_ARG(blocks >= 1 && stat_sum && stat_sq, "ym_conv_first_fwd: statistics buffers / blocks");
     ch_pieces(cout, 64, [&](int c_base, int c) {
-        hipLaunchKernelGGL(conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
-                           stat_sum, stat_sq, n, h, w, oh, ow, c, stride, pad, c_base, cout);
+        YM_STEM_CH_SWITCH(ch, conv_first_fwd_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, y,
+                          stat_sum, stat_sq, n, h, w, oh, ow, c, stride, pad, c_base, cout)
     });
     YM_LAUNCH_CHECK("ym_conv_first_fwd");
     return YM_OK;
@@ -1610,11 +1600,11 @@ extern "C" int ym_conv_first_fwd(const float* img, const float* w_oihw, uint16_t
 
 extern "C" int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, const float* scale, const float* shift,
                                       int act, uint16_t* y, int64_t y_bs, int64_t y_ld, int n, int h, int w, int oh,
-                                      int ow, int cout, int stride, int pad, void* stream) {
+                                      int ow, int cout, int stride, int pad, int ch, void* stream) {
     YM_CHECK_ARG(img && w_oihw && scale && shift && y, "ym_conv_first_fwd_eval: null argument");
-    YM_CHECK_ARG(cout % 8 == 0 && cout <= 512, "ym_conv_first_fwd_eval: cout=%d unsupported",
-                 cout);
-    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+    YM_CHECK_ARG(ch >= 1 && ch <= 4, "ym_conv_first_fwd_eval: ch=%d image planes unsupported (1..4)", ch);
+    YM_CHECK_ARG(cout % 8 == 0 && cout <= (ch <= 2 ? 512 : 256), "ym_conv_first_fwd_eval: cout=%d unsupported", cout);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * ch * h * w < (int64_t(1) << 31),
                  "ym_conv_first_fwd_eval: too many pixels");
     YM_CHECK_ARG(y_ld % 8 == 0 && y_bs % 8 == 0 && y_ld >= cout && y_bs >= int64_t(oh) * ow * y_ld &&
                      reinterpret_cast<uintptr_t>(y) % 16 == 0,
@@ -1622,30 +1612,31 @@ extern "C" int ym_conv_first_fwd_eval(const float* img, const float* w_oihw, con
     const int64_t threads = int64_t(n) * oh * ow;                 // one per output pixel
     if (threads == 0) return YM_OK;
     const int blocks = int(std::min<int64_t>((threads + 255) / 256, 8192));
-    hipLaunchKernelGGL(conv_first_eval_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, scale,
-                       shift, act, y, y_bs, y_ld, n, h, w, oh, ow, cout, stride, pad);
+    YM_STEM_CH_SWITCH(ch, conv_first_eval_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), img, w_oihw, scale,
+                      shift, act, y, y_bs, y_ld, n, h, w, oh, ow, cout, stride, pad)
     YM_LAUNCH_CHECK("ym_conv_first_fwd_eval");
     return YM_OK;
 }
 
-extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout) {
-    return size_t(PARTIAL_BLOCKS) * size_t(cout > 0 ? cout : 0) * 9 * sizeof(float);
+extern "C" size_t ym_conv_first_wgrad_workspace_size(int cout, int ch) {
+    return size_t(PARTIAL_BLOCKS) * size_t(cout > 0 ? cout : 0) * 9 * size_t(ch > 0 ? ch : 0) * sizeof(float);
 }
 
 extern "C" int ym_conv_first_wgrad(const uint16_t* dz, const float* img, float* dw_oihw, int n, int h, int w, int oh,
-                                   int ow, int cout, int stride, int pad, float* workspace, size_t workspace_bytes,
-                                   void* stream) {
+                                   int ow, int cout, int stride, int pad, int ch, float* workspace,
+                                   size_t workspace_bytes, void* stream) {
     YM_CHECK_ARG(cout % 8 == 0 && cout > 0 && cout <= 4096, "ym_conv_first_wgrad: cout=%d unsupported", cout);
-    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * h * w < (int64_t(1) << 31),
+    YM_CHECK_ARG(ch >= 1 && ch <= 4, "ym_conv_first_wgrad: ch=%d image planes unsupported (1..4)", ch);
+    YM_CHECK_ARG(int64_t(n) * oh * ow < (int64_t(1) << 31) && int64_t(n) * ch * h * w < (int64_t(1) << 31),
                  "ym_conv_first_wgrad: too many pixels");
-    YM_CHECK_ARG(workspace && workspace_bytes >= ym_conv_first_wgrad_workspace_size(cout),
+    YM_CHECK_ARG(workspace && workspace_bytes >= ym_conv_first_wgrad_workspace_size(cout, ch),
                  "ym_conv_first_wgrad: workspace too small");
     hipStream_t st = as_stream(stream);
     ch_pieces(cout, 16, [&](int c_base, int c) {             // <= 128 channels a piece (the kernel's LDS rows)
-        hipLaunchKernelGGL(conv_first_wgrad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dz, img, workspace, n, h, w,
-                           oh, ow, c, stride, pad, c_base, cout);
+        YM_STEM_CH_SWITCH(ch, conv_first_wgrad_kernel, dim3(PARTIAL_BLOCKS), dim3(256), 0, st, dz, img, workspace, n, h,
+                          w, oh, ow, c, stride, pad, c_base, cout)
     });
-    colsum_launch(workspace, PARTIAL_BLOCKS, cout * 9, int64_t(cout) * 9, dw_oihw, 1, st);
+    colsum_launch(workspace, PARTIAL_BLOCKS, cout * 9 * ch, int64_t(cout) * 9 * ch, dw_oihw, 1, st);
     YM_LAUNCH_CHECK("ym_conv_first_wgrad");
     return YM_OK;
 }

@@ -12,7 +12,7 @@ struct DirectPlan {
 };
 
 // -1: default policy; 0 never; 1 maps of >= 1 M output pixels; 2 any size
-extern int g_direct_force;
+extern Policy g_direct_force;
 
 // inference: a forward without BatchNorm statistics (the eval path) — under the default policy it takes the kernel from
 // 200 k output pixels (the 160x160 stage from 8 images up) instead of 1 M

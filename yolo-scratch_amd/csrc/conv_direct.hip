@@ -29,7 +29,7 @@
 
 namespace ym {
 
-int g_direct_force = -1;
+Policy g_direct_force{-1};
 
 namespace {
 

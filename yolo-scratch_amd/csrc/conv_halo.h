@@ -16,7 +16,7 @@ struct HaloPlan {
 
 // -1: default policy (3); 0 never; 1 wherever it applies; 2 maps <= 24 wide; 3 maps <= 48
 // wide or <= 64 output channels (ym_conv_set_halo)
-extern int g_halo_force;
+extern Policy g_halo_force;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad);

@@ -429,7 +429,7 @@ static bool pick_rect(int OH, int OW, int tp, int hpad, int& TH, int& TW) {
 
 }  // namespace
 
-int g_halo_force = -1;
+Policy g_halo_force{-1};
 
 HaloPlan halo_plan(const ym_conv_desc* d, int dgrad) {
     HaloPlan p{};

@@ -14,7 +14,7 @@ struct HPipePlan {
 
 // selection policy (ym_conv_set_hpipe): -1 default (1); 0 never; 1 the weight-resident 64 -> 64 layers with >= 512 tiles;
 // 2 every eligible layer
-extern int g_hpipe_force;
+extern Policy g_hpipe_force;
 
 HPipePlan hpipe_plan(const ym_conv_desc* d, int dgrad);
 int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,

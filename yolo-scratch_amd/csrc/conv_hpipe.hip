@@ -33,7 +33,7 @@
 
 namespace ym {
 
-int g_hpipe_force = -1;
+Policy g_hpipe_force{-1};
 
 namespace {
 

@@ -16,7 +16,7 @@ struct PipePlan {
 
 // -1: default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
 // tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
-extern int g_pipe_force;
+extern Policy g_pipe_force;
 
 // dgrad = 0: forward conv described by d; 1: its data gradient
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);

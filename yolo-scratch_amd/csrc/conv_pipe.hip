@@ -40,10 +40,16 @@ namespace ym {
 // selection policy (ym_conv_set_pipe): -1 default (3); 0 never; 1 layers of >= 1024 tiles with >= 128
 // output channels, no stride-2 data gradient; 2 every eligible layer of >= 256 tiles; 3 (default) the
 // wider rule of pipe_plan (s@640 bs64 step: 2940 img/s vs 2902 for rule 1)
-int g_pipe_force = -1;
-// experiments (ym_pipe_set_exp, not in the header; tools/pipe_ab.py): 0 shipped; 1 the 8-wave 256 x 128 tile;
-// 10-13 ablations of the 16-wave tile (conv_pipe_kernel ABL 1, 2, 4, 8); 20 the generic (class-search) control path
-int g_pipe_exp = 0;
+Policy g_pipe_force{-1};
+// experiments (ym_pipe_set_exp, yolomi_experimental.h; tools/pipe_ab.py): 0 shipped; 1 the 8-wave 256 x 128 tile;
+// 10-13 ablations of the 16-wave tile (conv_pipe_kernel ABL 1, 2, 4, 8: wrong results by design); 20 the generic
+// (class-search) control path.  Built only into the measurement library (make exp: -DYM_EXPERIMENTS,
+// libyolomi_exp.so); the shipping libyolomi.so has neither the setter nor the ablation instances.
+#ifdef YM_EXPERIMENTS
+Policy g_pipe_exp{0};
+#else
+constexpr int g_pipe_exp = 0;
+#endif
 
 namespace {
 
@@ -629,6 +635,7 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}, {256, 128}};
 template <int MODE>
 void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     const bool c1 = a.ncls == 1 && int64_t(a.OH) * a.OW >= kCfg[cfg].bm && g_pipe_exp != 20;
+#ifdef YM_EXPERIMENTS
     if (cfg == 0 && g_pipe_exp >= 10 && g_pipe_exp < 20) {
         switch (g_pipe_exp) {
             case 10: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 1, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
@@ -637,6 +644,7 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
             default: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 8, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); return;
         }
     }
+#endif
     if (c1) {
         switch (cfg) {
             case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
@@ -711,11 +719,11 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     return p;
 }
 
+#ifdef YM_EXPERIMENTS
 extern "C" int ym_pipe_set_exp(int v) {
-    const int prev = g_pipe_exp;
-    g_pipe_exp = v;
-    return prev;
+    return g_pipe_exp.set(v);
 }
+#endif
 
 int pipe_launch(const PipePlan& p, const ym_conv_desc* d, int dgrad, const uint16_t* x, const uint16_t* w, void* y,
                 const float* bias, float* st_sum, float* st_sq, hipStream_t st, const ym_bn_fold* fold) {

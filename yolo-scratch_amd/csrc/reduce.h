@@ -28,7 +28,9 @@ __device__ __forceinline__ void ordered_wave_add8(float* rs, float* rq, const fl
         __syncthreads();
     }
 }
-__device__ __forceinline__ void ordered_wave_add72(float* red, const float (*acc)[9], int g, int G) {
+// 8 channels x T taps per lane group (the stem's weight-gradient rows: T = 9 x input channels)
+template <int T>
+__device__ __forceinline__ void ordered_wave_add_taps(float* red, const float (*acc)[T], int g, int G) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     __syncthreads();
     for (int w = 0; w < 4; ++w) {
@@ -36,7 +38,7 @@ __device__ __forceinline__ void ordered_wave_add72(float* red, const float (*acc
 #pragma unroll
             for (int r = 0; r < 8; ++r)
 #pragma unroll
-                for (int t = 0; t < 9; ++t) red[(g * 8 + r) * 9 + t] = (w ? red[(g * 8 + r) * 9 + t] : 0.f) + acc[r][t];
+                for (int t = 0; t < T; ++t) red[(g * 8 + r) * T + t] = (w ? red[(g * 8 + r) * T + t] : 0.f) + acc[r][t];
         __syncthreads();
     }
 }

@@ -17,3 +17,4 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* ym_last_error(void) { return ym::g_err; }
 extern "C" int ym_version(void) { return 1; }
+extern "C" unsigned ym_policy_generation(void) { return ym::g_policy_gen.load(std::memory_order_relaxed); }

@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(256) stem_bwd_wgrad_kernel(const bf16_t* __res
 #pragma unroll
         for (int t = 0; t < 9; ++t)
             for (int o = G; o < 64; o <<= 1) acc[r][t] += __shfl_xor(acc[r][t], o, 64);
-    ordered_wave_add72(red, acc, g, G);
+    ordered_wave_add_taps<9>(red, acc, g, G);
     for (int i = threadIdx.x; i < C * 9; i += 256) part[int64_t(blockIdx.x) * C * 9 + i] = red[i];
 }
 

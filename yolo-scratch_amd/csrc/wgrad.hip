@@ -160,8 +160,9 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
             for (int j = 0; j < TJ; ++j) acc[t][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     uint4 da[DI], xa[XI], db[DI], xb[XI];
-    auto load = [&](int64_t t, uint4 (&rdz)[DI], uint4 (&rx)[XI]) {
-        (void)t;                                   // == l_t
+    // stages unit l_t and steps it: no unit argument, so a call site cannot look as if it chose the unit (a reordered
+    // or prefetched call would stage the wrong unit silently) — units go in stream order, one per call
+    auto load = [&](uint4 (&rdz)[DI], uint4 (&rx)[XI]) {
         const bool live = l_t < t_end;             // past the split: zeros, no branch around the loads
         const int tw = l_tw, th = l_th, n = l_n;
         if (live) {
@@ -237,35 +238,35 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
         // units in pairs over the two register sets and the two LDS buffers: unit t + 1 is written into the
         // other buffer (its loads issued a unit ago) while unit t is multiplied, then unit t + 3's loads go out
         if (t_begin < t_end) {
-            load(t_begin, da, xa);
-            load(t_begin + 1, db, xb);
+            load(da, xa);
+            load(db, xb);
             store(0, da, xa);
             __syncthreads();
-            load(t_begin + 2, da, xa);
+            load(da, xa);
         }
         for (int64_t t = t_begin; t < t_end; t += 2) {
             compute(0);                       // unit t
             store(1, db, xb);                 // unit t + 1 into the other buffer (read two barriers ago)
-            load(t + 3, db, xb);
+            load(db, xb);
             __syncthreads();
             compute(1);                       // unit t + 1
             store(0, da, xa);                 // unit t + 2
-            load(t + 4, da, xa);
+            load(da, xa);
             __syncthreads();
         }
     } else if constexpr (DB) {
         if (t_begin < t_end) {
-            load(t_begin, da, xa);
+            load(da, xa);
             store(0, da, xa);
             __syncthreads();
-            load(t_begin + 1, da, xa);
+            load(da, xa);
         }
         int buf = 0;
         for (int64_t t = t_begin; t < t_end; ++t) {
             compute(buf);
             if (t + 1 < t_end) {
                 store(buf ^ 1, da, xa);
-                load(t + 2, da, xa);
+                load(da, xa);
             }
             __syncthreads();
             buf ^= 1;
@@ -275,31 +276,31 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
         // one unit of zeros at its end): the loop has one exit, so the accumulators are not copied
         // between the two bodies' register assignments
         if (t_begin < t_end) {
-            load(t_begin, da, xa);
-            load(t_begin + 1, db, xb);
+            load(da, xa);
+            load(db, xb);
             store(0, da, xa);
             __syncthreads();
-            load(t_begin + 2, da, xa);
+            load(da, xa);
         }
         for (int64_t t = t_begin; t < t_end; t += 2) {
             compute(0);                       // unit t (set a's, staged)
             __syncthreads();
             store(0, db, xb);
             __syncthreads();
-            load(t + 3, db, xb);
+            load(db, xb);
             compute(0);                       // unit t + 1
             __syncthreads();
             store(0, da, xa);
             __syncthreads();
-            load(t + 4, da, xa);
+            load(da, xa);
         }
     } else {
         // one register set: unit t + 1 in flight while unit t is multiplied
         if (t_begin < t_end) {
-            load(t_begin, da, xa);
+            load(da, xa);
             store(0, da, xa);
             __syncthreads();
-            load(t_begin + 1, da, xa);
+            load(da, xa);
         }
         for (int64_t t = t_begin; t < t_end; ++t) {
             compute(0);
@@ -307,7 +308,7 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
             if (t + 1 >= t_end) break;
             store(0, da, xa);
             __syncthreads();
-            load(t + 2, da, xa);
+            load(da, xa);
         }
     }
 
@@ -590,7 +591,7 @@ struct WgPlan {
 // Round 5: 160 measured +0.2 % img/s in the step (three same-box pairs, profiles/r05/wgrad_target_streams_ab.txt) but
 // each launch ran longer alone (the 3x3 family's single-stream roofline fraction 0.2107 -> 0.1974, wgrad 0.199 ->
 // 0.161, profiles/r05/at_589d336): kept at 256, the gain inside the run-to-run spread
-int g_wg_target = 256;
+Policy g_wg_target{256};
 
 WgPlan wg_plan(const ym_conv_desc* d) {
     WgPlan p{};
@@ -649,9 +650,7 @@ WgPlan wg_plan(const ym_conv_desc* d) {
 extern "C" int ym_wgrad_set_target(int wgs) {
     // workgroups per weight-gradient launch the split-K plan aims for (default 256; <= 0 restores it); returns the
     // previous setting
-    const int prev = g_wg_target;
-    g_wg_target = wgs <= 0 ? 256 : wgs;
-    return prev;
+    return g_wg_target.set(wgs <= 0 ? 256 : wgs);
 }
 
 int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len) {

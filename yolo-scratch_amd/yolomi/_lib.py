@@ -52,10 +52,12 @@ class BnFold(ctypes.Structure):
 
 
 R = _c.c_int
-# name -> (restype, argtypes); must match include/yolomi.h
+# name -> (restype, argtypes); must match include/yolomi.h + include/yolomi_experimental.h (its YM_EXPERIMENTS block
+# excepted: the measurement library's)
 SIGNATURES = {
     "ym_last_error": (_c.c_char_p, []),
     "ym_version": (R, []),
+    "ym_policy_generation": (_c.c_uint, []),
     "ym_iou_row": (R, [P, P, I64, P, P]),
     "ym_nms_workspace_size": (SZ, [I64, I64]),
     "ym_decode_nms": (R, [P, I64, I64, I64, I64, I64, F32, F32, F32, P, SZ, P, P, P, P, P, P]),
@@ -75,12 +77,12 @@ SIGNATURES = {
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
     "ym_wgrad_set_target": (R, [INT]),
     "ym_conv_wgrad": (R, [P, P, P, P, SZ, P, INT, P]),
-    "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_conv_first_fwd_eval": (R, [P, P, P, P, INT, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_fwd": (R, [P, P, P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
+    "ym_conv_first_fwd_eval": (R, [P, P, P, P, INT, P, I64, I64, INT, INT, INT, INT, INT, INT, INT, INT, INT, P]),
     "ym_stem_bwd_wgrad_workspace_size": (SZ, [INT]),
     "ym_stem_bwd_wgrad_stored": (R, [P, I64, I64, P, P, P, P, P, P, SZ, INT, INT, INT, INT, INT, INT, INT, INT, P]),
-    "ym_conv_first_wgrad_workspace_size": (SZ, [INT]),
-    "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
+    "ym_conv_first_wgrad_workspace_size": (SZ, [INT, INT]),
+    "ym_conv_first_wgrad": (R, [P, P, P, INT, INT, INT, INT, INT, INT, INT, INT, INT, P, SZ, P]),
     "ym_dw3x3_fwd": (R, [P, I64, I64, INT, INT, INT, P, P, P, P, INT, INT, INT, INT, INT, P]),
     "ym_dw3x3_fwd_eval": (R, [P, I64, I64, INT, INT, INT, P, P, P, INT, P, I64, I64, P, I64, I64, INT, INT, INT, INT,
                               P]),

@@ -311,12 +311,14 @@ class ConvBN:
         """ym_conv_fwd_eval arguments for this op's eval forward (conv + eval BatchNorm + SiLU + residual in one
         launch), or None: the selected kernel has no eval epilogue, a view is misaligned, or SPPF's pools need the
         fp32 copy.  YM_EVAL_FUSE=0 opts out."""
-        on = os.environ.get("YM_EVAL_FUSE", "1") != "0" and "out32" not in self.__dict__
+        # keyed on the library's policy generation too: ym_conv_fwd_eval_ok and the K-split workspace are answers of the
+        # selection policies in force (yolomi_experimental.h), re-asked after any setter call
+        on = (os.environ.get("YM_EVAL_FUSE", "1") != "0" and "out32" not in self.__dict__, lib().ym_policy_generation())
         f = self.__dict__.get("_evf")
         if f is None or f[0] != on:
             args = None
             r = self.res
-            if on and (r is None or (r.ptr() % 8 == 0 and r.ld % 4 == 0)) and self.y.ptr() % 16 == 0:
+            if on[0] and (r is None or (r.ptr() % 8 == 0 and r.ld % 4 == 0)) and self.y.ptr() % 16 == 0:
                 d = ConvDesc.from_buffer_copy(self.desc)
                 d.y_bs, d.y_ld, d.out_f32, d.accumulate = self.y.bs, self.y.ld, 2, 0
                 if lib().ym_conv_fwd_eval_ok(ctypes.byref(d)):
@@ -419,7 +421,8 @@ class ConvBN:
 
 
 class StemConvBN(ConvBN):
-    """model.0: Conv(ch=1 -> c, 3x3 s2) on the fp32 image (reference yaml backbone row 0)."""
+    """model.0: Conv(ch -> c, 3x3 s2) on the fp32 NCHW image of ch = 1..4 planes (reference yaml backbone row 0;
+    build_yolo11(ch=...), models/yolo11_model.py:23, 258)."""
 
     def rw(self, plan, phase):
         return ([], [_ka(self.y)]) if phase == "fwd" else ([_kg(self.y)], [_kg(self.y)])
@@ -428,7 +431,8 @@ class StemConvBN(ConvBN):
         w = m.conv.weight
         self.m, self.y, self.res, self.act, self.x = m, y, None, 1, None
         co, ci, k, _ = w.shape
-        assert ci == 1 and k == 3
+        if not (1 <= ci <= 4 and k == 3):
+            raise YolomiError(f"stem Conv({ci}, {co}, {k}): the stem kernels take 1..4 image planes and a 3x3 kernel")
         B, H, W = img_shape
         self.H, self.W, self.k, self.s, self.co, self.ci = H, W, k, s, co, ci
         oh, ow = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
@@ -454,24 +458,25 @@ class StemConvBN(ConvBN):
                 call("ym_bn_eval_coeff", self.co, _p(bn.weight), _p(bn.bias), _p(bn.running_mean),
                      _p(bn.running_var), float(bn.eps), sc, sh, st)
             call("ym_conv_first_fwd_eval", plan.img.data_ptr(), _p(self.m.conv.weight), sc, sh, self.act, y.ptr(),
-                 y.bs, y.ld, plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, st)
+                 y.bs, y.ld, plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.ci, st)
             return
         ss, sq = self.ps[0], self.ps[1]
         call("ym_conv_first_fwd", plan.img.data_ptr(), _p(self.m.conv.weight), self.z.data_ptr(), ss.data_ptr(),
-             sq.data_ptr(), plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.G, st)
+             sq.data_ptr(), plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.ci, self.G, st)
         self._bn_fwd(plan, st, ss, sq)
 
     def backward(self, plan, st):
         """Statistics pass + finalize as every Conv block, then the BatchNorm apply and the weight gradient in
         ONE pass over dy and the stored z (ym_stem_bwd_wgrad_stored: dz is never written and re-read; the
-        kernel covers 16 / 32 / 64 channels — the n / s / m-l stems; other widths: BN backward + a separate
-        weight gradient over the written dz)."""
+        kernel covers 16 / 32 / 64 channels of a 1-plane image — the n / s / m-l stems; other widths and multi-plane
+        images: BN backward + a separate weight gradient over the written dz)."""
         dy = self.y.grad_for_read(st)
-        if self.co not in (16, 32, 64):
+        if self.co not in (16, 32, 64) or self.ci != 1:
             self._bn_bwd(plan, st, dy)
-            ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co))
+            ws = plan.private_ws(self, lib().ym_conv_first_wgrad_workspace_size(self.co, self.ci))
             call("ym_conv_first_wgrad", self.z.data_ptr(), plan.img.data_ptr(), plan.gptr(self.m.conv.weight),
-                 plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, ws.data_ptr(), ws.numel() * 4, st)
+                 plan.B, self.H, self.W, self.oh, self.ow, self.co, self.s, 1, self.ci, ws.data_ptr(),
+                 ws.numel() * 4, st)
             plan.note_grad_write(plan._cur_stream)      # conv.weight: after the BN event _bn_bwd noted
             return
         bn = self.m.bn
@@ -1090,7 +1095,10 @@ class Plan:
             for mod in self.root.modules():
                 pairs += [(mod._parameters, n) for n in mod._parameters]
                 pairs += [(mod._buffers, n) for n in mod._buffers]
-        return tuple(t.data_ptr() if t is not None else 0 for t in (d.get(n) for d, n in pairs))
+        # + the library's policy generation: a graph captured under one kernel-selection policy is not replayed under
+        # another (yolomi_experimental.h)
+        return tuple(t.data_ptr() if t is not None else 0 for t in (d.get(n) for d, n in pairs)) + (
+            lib().ym_policy_generation(),)
 
     @property
     def graph_active(self):
@@ -1124,7 +1132,10 @@ class Plan:
                 setattr(self, name, statics[name])
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize(self.dev)
-            with torch.cuda.graph(g):
+            # thread_local: only THIS thread's HIP calls are checked against the capture — the DataLoader's
+            # pin-memory thread (validate(): the capture is the second val batch) and the process group's
+            # watchdog keep running during it instead of erroring or invalidating the capture
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 body()
             graphs[phase] = ent = (g, statics, key)
         g, statics, _ = ent
@@ -1498,7 +1509,7 @@ def run_block(module, x: torch.Tensor):
     plan = cache.get(key)
     if plan is None:
         plan = Plan(module, B, H, W, x.device, module.training)
-        if type(module).__name__ == "Conv" and module.conv.in_channels == 1:
+        if type(module).__name__ == "Conv" and module.conv.in_channels <= 4 and module.conv.kernel_size[0] == 3:
             # stem conv reads the fp32 image directly (no input gradient)
             plan.stem = True
             plan.input = None
@@ -1602,8 +1613,10 @@ def run_model(model, img: torch.Tensor):
     if not img.is_cuda:
         raise YolomiError("yolomi kernels run on the MI355X only (got a CPU tensor)")
     B, C, H, W = img.shape
-    if C != 1:
-        raise YolomiError(f"stem kernel supports ch=1 input (got {C})")
+    ch = model.model[0].conv.in_channels
+    if C != ch:
+        # what the reference's first nn.Conv2d raises for a wrong plane count
+        raise YolomiError(f"expected input[{B}, {C}, {H}, {W}] to have {ch} channels, but got {C} channels instead")
     key = ("model", B, H, W, model.training)
     cache = model.__dict__.setdefault("_ym_plans", {})
     pool = cache.setdefault(key, [])
