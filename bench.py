@@ -518,7 +518,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp16 fwd / bf16 bwd (fp32 accumulate, fp32 loss + optimizer)",
-        "data": "synthetic (640x640 uniform images, 1-20 log-uniform boxes/img, seeded per rank)",
+        "data": f"synthetic ({args.imgsz}x{args.imgsz} uniform images, 1-20 log-uniform boxes/img, seeded per rank)",
         "config": {"workload": f"YOLOv11-{args.scale} {args.imgsz}x{args.imgsz} train step "
                                f"(fwd+loss+bwd+allreduce+clip+AdamW)",
                    "global_batch": args.batch * world, "batch_per_gpu": args.batch, "imgsz": args.imgsz,

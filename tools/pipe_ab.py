@@ -1,6 +1,7 @@
 """Same-process A/B of an experimental conv_pipe configuration switch (an extern "C" setter that is NOT in
 the header) on the s@640 bs64 plan's layers, variants interleaved over rounds.
 usage: python tools/pipe_ab.py SETTER --only 6 10 34 --variants 0 1
+       python tools/pipe_ab.py SETTER --setter2 SETTER2 --variants 0:0 0:1 2:1   (value pairs for two setters)
 """
 import argparse
 import ctypes
@@ -17,7 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("setter")
     ap.add_argument("--only", type=int, nargs="+", required=True)
-    ap.add_argument("--variants", type=int, nargs="+", default=[0, 1])
+    ap.add_argument("--variants", nargs="+", default=["0", "1"])
+    ap.add_argument("--setter2", default=None, help="a second setter: variants are then 'v1:v2' pairs")
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--also", nargs="*", default=[], help="other setters applied first, NAME=VALUE")
@@ -40,7 +42,14 @@ def main():
     torch.cuda.synchronize()
     plan = model.__dict__["_ym_last_plan"]
     st = stream_ptr(dev)
-    setter = getattr(lib(), args.setter)
+    s1 = getattr(lib(), args.setter)
+    s2 = getattr(lib(), args.setter2) if args.setter2 else None
+
+    def setter(v):
+        parts = str(v).split(":")
+        s1(int(parts[0]))
+        if s2 is not None:
+            s2(int(parts[1]) if len(parts) > 1 else 0)
     for kv in args.also:
         name, val = kv.split("=")
         getattr(lib(), name)(int(val))

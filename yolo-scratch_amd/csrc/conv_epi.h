@@ -191,6 +191,108 @@ __device__ __forceinline__ void epilogue_regs_x(f32x4 (&acc)[TM][TN], float (&ss
     }
 }
 
+// The same epilogue for 32x32 MFMA accumulators (v_mfma_f32_32x32x16): acc[i][j][r] is channel
+// wch0 + i*32 + 8*(r>>2) + 4*h + (r&3) of wave-local pixel q = j*32 + p (h = lane>>5, p = lane&31): each register group
+// g = r>>2 holds 4 consecutive channels of one pixel, the other 4 of that 8-channel run in the partner lane l ^ 32.
+// Groups (2k, 2k+1) are exchanged between the lane halves with v_permlane32_swap (the upper half of 2k's packed values
+// <-> the lower half of 2k+1's), after which lane l holds channels i*32 + 8*(2k + h) .. +7 of pixel j*32 + p: one 16-B
+// store per lane and group pair, 32 pixels x 2 runs per instruction, TM * TN * 2 stores per lane.  Statistics: ssum /
+// ssq[i][r] for the 16 channels the lane's registers hold (summed over the lane's pixels; the caller reduces over p).
+template <int TM, int TN, class PixOff, class PixOk, class ResOff>
+__device__ __forceinline__ void epilogue_regs32_x(f32x16 (&acc)[TM][TN], float (&ssum)[TM][16], float (&ssq)[TM][16],
+                                                  bool stats, int lane, int wch0, int nout,
+                                                  __amdgpu_buffer_rsrc_t yres, bool half, bool accumulate,
+                                                  PixOff pix_off, PixOk pix_ok, const EvalEpi* ea, ResOff res_off) {
+    const int h = lane >> 5, p = lane & 31;
+    if (ea) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int cb = wch0 + i * 32 + 8 * g + 4 * h;
+                if (cb >= nout) continue;                              // nout % 8 == 0: all four or none
+                const float4 s4 = *reinterpret_cast<const float4*>(ea->sc + cb);
+                const float4 h4 = *reinterpret_cast<const float4*>(ea->sh + cb);
+                const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, hv[4] = {h4.x, h4.y, h4.z, h4.w};
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float t = fmaf(acc[i][j][4 * g + r], sv[r], hv[r]);
+                        acc[i][j][4 * g + r] = ea->act ? silu_f(t) : t;
+                    }
+            }
+        if (ea->res) {                                                 // + residual in fp32, one rounding (as ym_bn_apply)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const uint32_t b = res_off(j * 32 + p);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int co = i * 32 + 8 * g + 4 * h;
+                        const uint32_t off = b != OOB && wch0 + co < nout ? b + uint32_t(co) * 2u : OOB;
+                        const uint2 rv =
+                            __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ea->rres, off, 0, 0));
+                        acc[i][j][4 * g + 0] += h2f(uint16_t(rv.x & 0xffff));
+                        acc[i][j][4 * g + 1] += h2f(uint16_t(rv.x >> 16));
+                        acc[i][j][4 * g + 2] += h2f(uint16_t(rv.y & 0xffff));
+                        acc[i][j][4 * g + 3] += h2f(uint16_t(rv.y >> 16));
+                    }
+            }
+        }
+    }
+    if (stats) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if (!pix_ok(j * 32 + p)) continue;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (wch0 + i * 32 + 8 * g + 4 * h >= nout) continue;   // nout % 8 == 0: all four or none
+#pragma unroll
+                    for (int r = 4 * g; r < 4 * g + 4; ++r) {
+                        const float v = acc[i][j][r];
+                        ssum[i][r] += v;
+                        ssq[i][r] = fmaf(v, v, ssq[i][r]);
+                    }
+                }
+        }
+    }
+    auto pack = [&](float lo, float hi) -> uint32_t {
+        return half ? pk2h(lo, hi) : pk2bf(lo, hi);
+    };
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const uint32_t base = pix_off(j * 32 + p);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int ga = 8 * k, gb = 8 * k + 4;                  // registers of groups 2k and 2k + 1
+                const uint32_t x0 = pack(acc[i][j][ga], acc[i][j][ga + 1]), x1 = pack(acc[i][j][ga + 2], acc[i][j][ga + 3]);
+                const uint32_t y0 = pack(acc[i][j][gb], acc[i][j][gb + 1]), y1 = pack(acc[i][j][gb + 2], acc[i][j][gb + 3]);
+                const auto s0 = __builtin_amdgcn_permlane32_swap(x0, y0, false, false);
+                const auto s1 = __builtin_amdgcn_permlane32_swap(x1, y1, false, false);
+                uint4 v = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                const int co = i * 32 + 8 * (2 * k + h);               // channel offset within the wave
+                const uint32_t off = base != OOB && wch0 + co < nout ? base + uint32_t(co) * 2u : OOB;
+                if (accumulate) {                                      // gradient fan-in (bf16)
+                    const uint4 old = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yres, off, 0, 0));
+                    uint32_t ww[4] = {v.x, v.y, v.z, v.w}, oo[4] = {old.x, old.y, old.z, old.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        ww[e] = pk2bf(bf2f(bf16_t(ww[e] & 0xffff)) + bf2f(bf16_t(oo[e] & 0xffff)),
+                                      bf2f(bf16_t(ww[e] >> 16)) + bf2f(bf16_t(oo[e] >> 16)));
+                    v = make_uint4(ww[0], ww[1], ww[2], ww[3]);
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v),
+                                                       yres, off, 0, 0);
+            }
+    }
+}
+
 template <int TM, int TN, class PixOff, class PixOk>
 __device__ __forceinline__ void epilogue_regs(f32x4 (&acc)[TM][TN], float (&ssum)[TM][4], float (&ssq)[TM][4],
                                               bool stats, int lane, int wch0, int nout,

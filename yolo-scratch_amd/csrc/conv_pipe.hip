@@ -45,6 +45,11 @@ Policy g_pipe_force{-1};
 // 10-13 ablations of the 16-wave tile (conv_pipe_kernel ABL 1, 2, 4, 8: wrong results by design); 20 the generic
 // (class-search) control path.  Built only into the measurement library (make exp: -DYM_EXPERIMENTS,
 // libyolomi_exp.so); the shipping libyolomi.so has neither the setter nor the ablation instances.
+// MFMA shape of the pipelined kernel (ym_conv_set_pipe_mfma): 0 16x16x32 on the shipped tiles; 1 32x32x16 on the same
+// tiles; 2 32x32x16 with the 256 x 128 layers on 8 waves of 64 x 64 (cfg 2) instead of 16 of 32 x 64
+Policy g_pipe_mfma{0};
+// K-step issue order of the pipelined kernel's single-class instances (ym_conv_set_pipe_order; conv_pipe_kernel RO)
+Policy g_pipe_order{0};
 #ifdef YM_EXPERIMENTS
 Policy g_pipe_exp{0};
 #else
@@ -350,10 +355,19 @@ struct Issuer {
 // maps take the generic one)
 // EV: the eval-mode Conv block instance (ym_conv_fwd_eval at large batches: running-statistics BatchNorm / SiLU /
 // residual in the register epilogue, conv_epi.h EvalEpi; a C1 forward without statistics; e is not read otherwise)
+// MF: the MFMA shape — 16 (v_mfma_f32_16x16x32: 16x16 subtiles, one MFMA per 32-deep half and subtile pair) or 32
+// (v_mfma_f32_32x32x16, round 6: 32x32 subtiles, two 16-deep MFMAs per half; half the MFMA instructions for the same
+// FLOPs, a 32-cycle issue window per MFMA instead of 16, the same LDS fragment bytes; conv_epi.h epilogue_regs32_x)
+// RO: issue order inside a K step (round 6).  0: after the barrier the stage DMAs go out between the second half's MFMAs
+// and the next stage's first-half fragments are read two MFMAs before the end of the step (the compiler also floats the
+// second-half reads into the middle of the first half); 1: every fragment read is pinned ahead of the MFMAs it covers —
+// the second-half reads at the top of the step, the next stage's first-half reads right after the barrier, ahead of
+// the DMAs — so each read has a whole half (TM * TN * KS MFMAs per wave) of cover
 template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false,
-          bool EV = false>
+          bool EV = false, int MF = 16, int RO = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, EvalArgs e) {
     static_assert(!EV || (C1 && MODE == PF && ABL == 0), "the eval instance is a single-class forward");
+    static_assert(MF == 16 || MF == 32, "MFMA shape");
     // NS: LDS ring of K stages — stage g computing, g+1 .. g+NS-1 in flight (3; 2 for the 64-KB+ stages of the
     // 256-channel / 512-pixel tiles)
     static_assert(NS == 2 || NS == 3, "ring depth");
@@ -362,13 +376,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
     constexpr int AI = BN / 8 / NW;           // weight DMA instructions per wave per stage
     constexpr int BI = BM / 8 / NW;           // activation DMA instructions per wave per stage
     constexpr int DPS = AI + BI;              // DMAs per wave per stage (the vmcnt unit)
-    constexpr int TM = BN / WM / 16;          // 16-channel subtiles per wave
-    constexpr int TN = BM / WN / 16;          // 16-pixel subtiles per wave
+    constexpr int TM = BN / WM / MF;          // MF-channel subtiles per wave
+    constexpr int TN = BM / WN / MF;          // MF-pixel subtiles per wave
+    constexpr int KS = MF == 16 ? 1 : 2;      // MFMA K slices per 32-deep half (and fragment reads per subtile)
+    constexpr int NR = MF == 16 ? 4 : 16;     // accumulator registers per subtile and lane
+    typedef float AccT __attribute__((ext_vector_type(NR)));
     constexpr int STAGE = (BM + BN) * RB;
     static_assert(AI >= 1 && BI >= 1 && TM >= 1 && TN >= 1, "tile too small for 8-row DMA pieces");
     static_assert(EPI == 2, "register-only epilogue");
     constexpr int WCH = BN / WM;                          // channels per wave
-    constexpr int EPS = TM * TN / 2;                      // epilogue stores per lane
+    constexpr int EPS = MF == 16 ? TM * TN / 2 : TM * TN * 2;   // epilogue stores per lane
     // the ring; the statistics' cross-wave reduction reuses its first bytes after the last tile
     static_assert(NS * STAGE <= 160 * 1024 && 2 * (BM / (BM / WN)) * BN * 4 <= NS * STAGE, "LDS budget");
     __shared__ __attribute__((aligned(16))) char smem[NS * STAGE];
@@ -405,50 +422,79 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
         a_off[j] = ch < a.Nout ? uint32_t(ch) * wrow_b + uint32_t((lane & 7) ^ fsw128(r)) * 16u : OOB;
     }
 
-    // per-lane fragment read offsets inside a stage (subtile i / j adds 2048 * i: fsw128 is 16-periodic)
-    uint32_t offA[2], offB[2];
+    // per-lane fragment read offsets inside a stage (subtile i / j adds MF * RB * i: fsw128 is 16-periodic).
+    // 16x16x32: lane (fc, fr) reads row fr of the subtile, 16-B chunk kk * 4 + fc of the 128-B row; 32x32x16: lane
+    // (h, p) reads row p, chunk kk * 4 + 2 s + h for K slice s (the operand layout of cdna_hip_programming.md §3)
+    uint32_t offA[2 * KS], offB[2 * KS];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-        const int ra = wr * (BN / WM) + fr, rb = wc * (BM / WN) + fr;
-        offA[kk] = uint32_t(ra * RB + (((kk * 4 + fc) ^ fsw128(ra)) << 4));
-        offB[kk] = uint32_t(BN * RB + rb * RB + (((kk * 4 + fc) ^ fsw128(rb)) << 4));
-    }
-    bf16x8 f0a[TM], f0b[TN], f1a[TM], f1b[TN];
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const int lr = MF == 16 ? fr : (lane & 31);
+            const int ch = MF == 16 ? kk * 4 + fc : kk * 4 + 2 * s + (lane >> 5);
+            const int ra = wr * (BN / WM) + lr, rb = wc * (BM / WN) + lr;
+            offA[kk * KS + s] = uint32_t(ra * RB + ((ch ^ fsw128(ra)) << 4));
+            offB[kk * KS + s] = uint32_t(BN * RB + rb * RB + ((ch ^ fsw128(rb)) << 4));
+        }
+    bf16x8 f0a[TM * KS], f0b[TN * KS], f1a[TM * KS], f1b[TN * KS];
     auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) {
-        const char* As = smem + buf * STAGE + offA[kk];
-        const char* Bs = smem + buf * STAGE + offB[kk];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(As + i * 16 * RB);
+        for (int s = 0; s < KS; ++s) {
+            const char* As = smem + buf * STAGE + offA[kk * KS + s];
+            const char* Bs = smem + buf * STAGE + offB[kk * KS + s];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(Bs + j * 16 * RB);
+            for (int i = 0; i < TM; ++i) fa[i * KS + s] = *reinterpret_cast<const bf16x8*>(As + i * MF * RB);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j * KS + s] = *reinterpret_cast<const bf16x8*>(Bs + j * MF * RB);
+        }
     };
-    f32x4 acc[TM][TN];
+    AccT acc[TM][TN];
     auto mma = [&](const bf16x8* fa, const bf16x8* fb) {
         if constexpr ((ABL & 2) != 0) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+            for (int i = 0; i < TM * KS; ++i) asm volatile("" ::"v"(fa[i]));
 #pragma unroll
-            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+            for (int j = 0; j < TN * KS; ++j) asm volatile("" ::"v"(fb[j]));
             return;
         }
 #pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const bf16x8 av = fa[i * KS + s], bv = fb[j * KS + s];
+                    if constexpr (MF == 16) {
+                        if constexpr (MODE == PF)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, av),
+                                                                                __builtin_bit_cast(f16x8, bv), acc[i][j],
+                                                                                0, 0, 0);
+                        else
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[i][j], 0, 0, 0);
+                    } else {
+                        if constexpr (MODE == PF)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, av),
+                                                                                __builtin_bit_cast(f16x8, bv), acc[i][j],
+                                                                                0, 0, 0);
+                        else
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i][j], 0, 0, 0);
+                    }
+                }
+    };
+    auto zero_acc = [&]() {
+#pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if constexpr (MODE == PF)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fa[i]),
-                                                                        __builtin_bit_cast(f16x8, fb[j]), acc[i][j], 0,
-                                                                        0, 0);
-                else
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-            }
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
     };
 
-    float ssum[TM][4], ssq[TM][4];
+    float ssum[TM][NR], ssq[TM][NR];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.f;
+        for (int r = 0; r < NR; ++r) ssum[i][r] = ssq[i][r] = 0.f;
 
     Issuer<BM, BN, NW, MODE, ABL, C1> is(a, wave, lane, mt_lo, qstride, ntile);
     is.start();
@@ -487,10 +533,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
                 c_tp += is.step_p;
                 if (c_tp >= is.ohw) { c_tp -= is.ohw; ++c_tn; }
             }
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            zero_acc();
         } else if (ck == 0) {
             const int mt = mt_lo + ct * qstride;
             const int c = cls_find(a, mt);
@@ -500,13 +543,15 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
             t_p = uint32_t(m0) - t_n * cc.OHW;
             inv_owc = 1.0f / float(cc.OWc);
             cnk = cc.ntap * kc;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            zero_acc();
         }
         read_frags(f1a, f1b, buf, 1);
         mma(f0a, f0b);
+        constexpr int MH = TM * TN * KS;                                            // MFMAs per half
+        if constexpr (RO == 1) {
+            __builtin_amdgcn_sched_group_barrier(0x100, (TM + TN) * KS, 0);        // this step's second-half reads
+            __builtin_amdgcn_sched_group_barrier(0x008, MH, 0);                     // first-half MFMAs
+        }
         // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight (every step issues DPS DMAs,
         // live or not, so the count is constant); in a tile's first step the previous tile's epilogue stores,
         // issued after stage g+2's pieces, may stay in flight too
@@ -520,13 +565,23 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
         is.issue_dma(smem + buf * STAGE, wres, a_off, g + NS < total);
         read_frags(f0a, f0b, nbuf, 0);
         mma(f1a, f1b);
+        if constexpr (RO == 1) {
+            __builtin_amdgcn_sched_group_barrier(0x100, (TM + TN) * KS, 0);        // next-stage reads first
 #pragma unroll
-        for (int d = 0; d < DPS; ++d) {
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                     // one DMA
-            __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (DPS + 1), 0);  // MFMAs
+            for (int d = 0; d < DPS; ++d) {
+                __builtin_amdgcn_sched_group_barrier(0x008, MH / (DPS + 1), 0);     // MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                 // one DMA
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, MH - DPS * (MH / (DPS + 1)), 0);
+        } else {
+#pragma unroll
+            for (int d = 0; d < DPS; ++d) {
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                 // one DMA
+                __builtin_amdgcn_sched_group_barrier(0x008, MH / (DPS + 1), 0);     // MFMAs
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, (TM + TN) * KS, 0);        // next-stage reads
+            __builtin_amdgcn_sched_group_barrier(0x008, MH - DPS * (MH / (DPS + 1)), 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);                   // next-stage reads
-        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - DPS * ((TM * TN) / (DPS + 1)), 0);
         is.advance();
         buf = nbuf;
         if (++ck < cnk) continue;
@@ -572,11 +627,19 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
                     if (pix >= is.ohw) { pix -= is.ohw; ++n; }
                     return uint32_t((int64_t(n) * e.r_bs + int64_t(pix) * e.r_ld + wch0) * 2);
                 };
-                epilogue_regs_x<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
-                                        &ee, res_off);
+                if constexpr (MF == 16)
+                    epilogue_regs_x<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off, pix_ok,
+                                            &ee, res_off);
+                else
+                    epilogue_regs32_x<TM, TN>(acc, ssum, ssq, false, lane, wch0, a.Nout, yres, true, false, pix_off,
+                                              pix_ok, &ee, res_off);
             } else {
-                epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
-                                      a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
+                if constexpr (MF == 16)
+                    epilogue_regs<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
+                                          a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok);
+                else
+                    epilogue_regs32_x<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
+                                              a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok, nullptr, pix_off);
             }
         }
     }
@@ -589,15 +652,17 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < NR; ++r) {
                 float s = ssum[i][r], sq = ssq[i][r];
+                // over the lanes holding other pixels of the same channel: 16 (16x16 layout) or 32 (32x32)
 #pragma unroll
-                for (int o = 1; o < 16; o <<= 1) {
+                for (int o = 1; o < MF; o <<= 1) {
                     s += __shfl_xor(s, o, 64);
                     sq += __shfl_xor(sq, o, 64);
                 }
-                if (fr == 0) {
-                    const int cl = wr * (BN / WM) + i * 16 + fc * 4 + r;
+                if ((lane & (MF - 1)) == 0) {
+                    const int cl = MF == 16 ? wr * (BN / WM) + i * 16 + fc * 4 + r
+                                            : wr * (BN / WM) + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3);
                     red[0][wc][cl] = s;
                     red[1][wc][cl] = sq;
                 }
@@ -632,6 +697,16 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}, {256, 128}};
 // of 64 x 64, 1.5x the fragment reads, but while some waves of a SIMD issue their DMA pieces or wait at
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
+// cfg 0 / 1 / 2 tiles (kCfg) of one control path (C1), MFMA shape (MF) and issue order (RO)
+template <int MODE, bool C1, int MF, int RO>
+void launch_tiles(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
+    switch (cfg) {
+        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
+        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+    }
+}
+
 template <int MODE>
 void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     const bool c1 = a.ncls == 1 && int64_t(a.OH) * a.OW >= kCfg[cfg].bm && g_pipe_exp != 20;
@@ -645,24 +720,30 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
         }
     }
 #endif
+    const int mf = g_pipe_mfma, ro = g_pipe_order;
+    const int c = mf == 2 && cfg == 0 ? 2 : cfg;
     if (c1) {
-        switch (cfg) {
-            case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
-            case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
-            default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, true><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        if (mf != 0) {
+            if (ro) launch_tiles<MODE, true, 32, 1>(c, a, grid, st);
+            else launch_tiles<MODE, true, 32, 0>(c, a, grid, st);
+        } else {
+            if (ro) launch_tiles<MODE, true, 16, 1>(c, a, grid, st);
+            else launch_tiles<MODE, true, 16, 0>(c, a, grid, st);
         }
         return;
     }
-    switch (cfg) {
-        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
-        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
-        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
-    }
+    if (mf != 0) launch_tiles<MODE, false, 32, 0>(c, a, grid, st);
+    else launch_tiles<MODE, false, 16, 0>(c, a, grid, st);
 }
 
 // the eval instance (EV): cfg 1 / 2 tiles on 8 waves (the 16-wave 256 x 128 tile's 127 VGPRs leave no room for the
 // eval epilogue at four waves per SIMD; cfg 0 runs as the 8-wave cfg 2)
 void launch_eval(int cfg, const PipeArgs& a, const EvalArgs& e, int grid, hipStream_t st) {
+    if (g_pipe_mfma != 0) {
+        if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true, 32><<<dim3(grid), dim3(512), 0, st>>>(a, e);
+        else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true, 32><<<dim3(grid), dim3(512), 0, st>>>(a, e);
+        return;
+    }
     if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
     else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
 }
@@ -717,6 +798,16 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     p.rows = grid / ntiles;
     p.ok = 1;
     return p;
+}
+
+extern "C" int ym_conv_set_pipe_order(int mode) {
+    // K-step issue order of the pipelined kernel (conv_pipe_kernel RO: 0 default, 1 fragment reads pinned first)
+    return g_pipe_order.set(mode < 0 || mode > 1 ? 0 : mode);
+}
+
+extern "C" int ym_conv_set_pipe_mfma(int mode) {
+    // MFMA shape of the pipelined implicit GEMM (see g_pipe_mfma); out of range restores the default 0
+    return g_pipe_mfma.set(mode < 0 || mode > 2 ? 0 : mode);
 }
 
 #ifdef YM_EXPERIMENTS
