@@ -51,14 +51,6 @@ int ym_conv_set_direct(int mode);
  * each 64-channel chunk of the 18x18 input halo staged once for all nine taps): -1 default, 0 never,
  * 1 the weight-resident 64 -> 64 layers with >= 512 tiles (default), 2 every eligible layer; returns the previous setting. */
 int ym_conv_set_hpipe(int mode);
-/* MFMA shape of the persistent pipelined implicit GEMM (round 6): 0 (default) v_mfma_f32_16x16x32 on the shipped tiles,
- * 1 v_mfma_f32_32x32x16 on the same tiles, 2 v_mfma_f32_32x32x16 with the 256 x 128 tile on 8 waves of 64 x 64 instead
- * of 16 of 32 x 64.  Returns the previous setting. */
-int ym_conv_set_pipe_mfma(int mode);
-/* K-step issue order of the pipelined implicit GEMM (round 6): 0 (default) stage DMAs first after the barrier, the next
- * stage's fragment reads late; 1 every fragment read pinned ahead of the half step of MFMAs it covers.  Returns the
- * previous setting. */
-int ym_conv_set_pipe_order(int mode);
 /* Workgroups per weight-gradient launch the split-K plan aims for (default 256, tuned in the training step where
  * the weight gradients share the GPU with the data gradients; <= 0 restores it).  Returns the previous setting.
  * Process-wide, like ym_conv_set_halo; a workspace size queried under one setting serves only that setting. */
@@ -96,6 +88,14 @@ int ym_bn_set_bwd_fold(int mode);
  * conv_pipe experiment instances — 1 the 8-wave 256x128 tile, 10-13 ablations that skip DMAs or MFMAs (WRONG results
  * by design, for timing only), 20 the generic control path.  0 restores the shipped kernels. */
 int ym_pipe_set_exp(int v);
+/* MFMA shape of the persistent pipelined implicit GEMM (round 6, measured slower: profiles/r06/pipe_mfma_order_ab.txt):
+ * 0 (default) v_mfma_f32_16x16x32 on the shipped tiles, 1 v_mfma_f32_32x32x16 on the same tiles, 2 v_mfma_f32_32x32x16 with the 256 x 128 tile on 8 waves of 64 x 64 instead
+ * of 16 of 32 x 64.  Returns the previous setting. */
+int ym_conv_set_pipe_mfma(int mode);
+/* K-step issue order of the pipelined kernels (round 6, measured slower: profiles/r06/pipe_mfma_order_ab.txt):
+ * 0 (default) stage DMAs first after the barrier, the next stage's fragment reads late; 1 every fragment read pinned ahead of the half step of MFMAs it covers.  Returns the
+ * previous setting. */
+int ym_conv_set_pipe_order(int mode);
 #endif
 
 #ifdef __cplusplus

@@ -201,20 +201,13 @@ PIPE = [
 ]
 
 
-@pytest.mark.parametrize("mfma,order", [(0, 0), (1, 0), (2, 0), (0, 1), (2, 1)],
-                         ids=["mf16", "mf32", "mf32w8", "mf16ro1", "mf32w8ro1"])
 @pytest.mark.parametrize("shape", PIPE, ids=[f"n{s[0]}h{s[1]}w{s[2]}c{s[3]}o{s[4]}k{s[5]}s{s[6]}" for s in PIPE])
-def test_pipe_kernel_vs_torch(shape, mfma, order):
-    """fp16 forward (+ BN statistic partials), bf16 data gradient (overwrite, then accumulate); each MFMA shape of
-    ym_conv_set_pipe_mfma (0: 16x16x32, 1: 32x32x16 on the same tiles, 2: 32x32x16 with 8 waves of 64 x 64) and K-step
-    issue order of ym_conv_set_pipe_order."""
+def test_pipe_kernel_vs_torch(shape):
+    """fp16 forward (+ BN statistic partials), bf16 data gradient (overwrite, then accumulate).  (The round-6
+    32x32x16-MFMA and reads-first variants, measurement library only, passed this test on every shape:
+    profiles/r06/pytest_pipe_variants.log.)"""
     from yolomi._lib import lib
-    prev = lib().ym_conv_set_pipe_mfma(mfma), lib().ym_conv_set_pipe_order(order)
-    try:
-        _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
-    finally:
-        lib().ym_conv_set_pipe_mfma(prev[0])
-        lib().ym_conv_set_pipe_order(prev[1])
+    _views_fwd_dgrad_check(shape, lib().ym_conv_set_pipe, 2, 2)
 
 
 # halo-staged PIPELINED 3x3 stride-1 kernel (conv_hpipe.hip), forced on with ym_conv_set_hpipe(2): 16x16-pixel

@@ -29,6 +29,7 @@
 #include "common.h"
 #include "conv_epi.h"
 #include "conv_hpipe.h"
+#include "conv_pipe.h"
 #include "tile.h"
 
 namespace ym {
@@ -107,7 +108,9 @@ __device__ __forceinline__ void step_barrier() {
 // WRES (64 -> 64 channels, one 64-channel chunk): the layer's whole weight tensor (9 taps x 64 x 64, 72 KB)
 // is staged into LDS once per workgroup and stays resident; the K loop then stages only the halo (41 pieces
 // per 9 K steps) and waits only before a chunk's first step for its halo
-template <int BN, int WM, int WN, int MODE, bool WRES = false>
+// RO: K-step issue order as conv_pipe_kernel's (ym_conv_set_pipe_order): 1 pins every fragment read ahead of the half
+// step of MFMAs it covers (the next step's first-half reads right after the barrier, before the DMAs)
+template <int BN, int WM, int WN, int MODE, bool WRES = false, int RO = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
     constexpr int NS = WRES ? 9 : 4;          // weight ring: slot of step g computing, g+1..g+3 in flight (WRES:
                                               // the 9 taps, resident)
@@ -282,6 +285,10 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         }
         read_frags(f1a, f1b, pos, 1);
         mma(f0a, f0b);
+        if constexpr (RO == 1) {
+            __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);               // this step's second-half reads
+            __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);               // first-half MFMAs
+        }
         // stage g+1 must have landed (own DMAs); stages g+2 and g+3 may stay in flight, and so may halos
         // issued in steps g-2 and g-1 (after stage g+1, when those steps began a chunk with a successor)
         if (WRES) {
@@ -304,7 +311,19 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_hpipe_kernel(HArgs a) {
         pos = npos;
         if (++c9 == 9) { c9 = 0; ++hc; }
         mma(f1a, f1b);
-        if constexpr (!WRES) {
+        if constexpr (RO == 1) {
+            __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);               // next-step reads first
+            if constexpr (!WRES) {
+#pragma unroll
+                for (int d = 0; d < AI; ++d) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, (TM * TN) / (AI + 1), 0);  // MFMAs
+                    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // one weight DMA
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN - AI * ((TM * TN) / (AI + 1)), 0);
+            } else {
+                __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+            }
+        } else if constexpr (!WRES) {
 #pragma unroll
             for (int d = 0; d < AI; ++d) {
                 __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                    // one weight DMA
@@ -437,6 +456,13 @@ int hpipe_launch(const HPipePlan& p, const ym_conv_desc* d, int dgrad, const uin
     a.tpi = (a.H / TS) * a.tpr;
     a.mt_total = a.N * a.tpi;
     if (p.cfg == 2) {
+#ifdef YM_EXPERIMENTS
+        if (g_pipe_order) {
+            if (!dgrad) conv_hpipe_kernel<64, 1, 8, HF, true, 1><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+            else conv_hpipe_kernel<64, 1, 8, HD, true, 1><<<dim3(p.grid), dim3(512), 0, st>>>(a);
+            return 0;
+        }
+#endif
         if (!dgrad) conv_hpipe_kernel<64, 1, 8, HF, true><<<dim3(p.grid), dim3(512), 0, st>>>(a);
         else conv_hpipe_kernel<64, 1, 8, HD, true><<<dim3(p.grid), dim3(512), 0, st>>>(a);
         return 0;

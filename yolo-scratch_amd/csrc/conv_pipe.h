@@ -17,6 +17,9 @@ struct PipePlan {
 // -1: default policy (3); 0 never; 1 layers of >= 1024 tiles, >= 128 channels; 2 >= 256
 // tiles; 3 the wider rule of pipe_plan (ym_conv_set_pipe)
 extern Policy g_pipe_force;
+#ifdef YM_EXPERIMENTS
+extern Policy g_pipe_order;     // K-step issue order of the pipelined kernels (conv_pipe / conv_hpipe RO; measurement only)
+#endif
 
 // dgrad = 0: forward conv described by d; 1: its data gradient
 PipePlan pipe_plan(const ym_conv_desc* d, int dgrad);

@@ -45,12 +45,13 @@ Policy g_pipe_force{-1};
 // 10-13 ablations of the 16-wave tile (conv_pipe_kernel ABL 1, 2, 4, 8: wrong results by design); 20 the generic
 // (class-search) control path.  Built only into the measurement library (make exp: -DYM_EXPERIMENTS,
 // libyolomi_exp.so); the shipping libyolomi.so has neither the setter nor the ablation instances.
-// MFMA shape of the pipelined kernel (ym_conv_set_pipe_mfma): 0 16x16x32 on the shipped tiles; 1 32x32x16 on the same
-// tiles; 2 32x32x16 with the 256 x 128 layers on 8 waves of 64 x 64 (cfg 2) instead of 16 of 32 x 64
-Policy g_pipe_mfma{0};
-// K-step issue order of the pipelined kernel's single-class instances (ym_conv_set_pipe_order; conv_pipe_kernel RO)
-Policy g_pipe_order{0};
+// Measured and rejected in round 6, built into the measurement library only (profiles/r06/pipe_mfma_order_ab.txt):
+// the MFMA shape (ym_conv_set_pipe_mfma: 0 16x16x32 shipped; 1 32x32x16 on the same tiles, +8..+23 % per layer;
+// 2 32x32x16 on 8 waves of 64 x 64, +1..+14 %) and the K-step issue order (ym_conv_set_pipe_order / conv_pipe_kernel
+// RO: 1 pins every fragment read ahead of the MFMAs it covers, -3..+7 %)
 #ifdef YM_EXPERIMENTS
+Policy g_pipe_mfma{0};
+Policy g_pipe_order{0};   // also conv_hpipe.hip (conv_pipe.h)
 Policy g_pipe_exp{0};
 #else
 constexpr int g_pipe_exp = 0;
@@ -720,6 +721,7 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
         }
     }
 #endif
+#ifdef YM_EXPERIMENTS
     const int mf = g_pipe_mfma, ro = g_pipe_order;
     const int c = mf == 2 && cfg == 0 ? 2 : cfg;
     if (c1) {
@@ -734,16 +736,22 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     }
     if (mf != 0) launch_tiles<MODE, false, 32, 0>(c, a, grid, st);
     else launch_tiles<MODE, false, 16, 0>(c, a, grid, st);
+#else
+    if (c1) launch_tiles<MODE, true, 16, 0>(cfg, a, grid, st);
+    else launch_tiles<MODE, false, 16, 0>(cfg, a, grid, st);
+#endif
 }
 
 // the eval instance (EV): cfg 1 / 2 tiles on 8 waves (the 16-wave 256 x 128 tile's 127 VGPRs leave no room for the
 // eval epilogue at four waves per SIMD; cfg 0 runs as the 8-wave cfg 2)
 void launch_eval(int cfg, const PipeArgs& a, const EvalArgs& e, int grid, hipStream_t st) {
+#ifdef YM_EXPERIMENTS
     if (g_pipe_mfma != 0) {
         if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true, 32><<<dim3(grid), dim3(512), 0, st>>>(a, e);
         else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true, 32><<<dim3(grid), dim3(512), 0, st>>>(a, e);
         return;
     }
+#endif
     if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
     else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
 }
@@ -800,6 +808,7 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
     return p;
 }
 
+#ifdef YM_EXPERIMENTS
 extern "C" int ym_conv_set_pipe_order(int mode) {
     // K-step issue order of the pipelined kernel (conv_pipe_kernel RO: 0 default, 1 fragment reads pinned first)
     return g_pipe_order.set(mode < 0 || mode > 1 ? 0 : mode);
@@ -810,7 +819,6 @@ extern "C" int ym_conv_set_pipe_mfma(int mode) {
     return g_pipe_mfma.set(mode < 0 || mode > 2 ? 0 : mode);
 }
 
-#ifdef YM_EXPERIMENTS
 extern "C" int ym_pipe_set_exp(int v) {
     return g_pipe_exp.set(v);
 }

@@ -72,8 +72,6 @@ SIGNATURES = {
     "ym_conv_set_pipe": (R, [INT]),
     "ym_conv_set_direct": (R, [INT]),
     "ym_conv_set_hpipe": (R, [INT]),
-    "ym_conv_set_pipe_mfma": (R, [INT]),
-    "ym_conv_set_pipe_order": (R, [INT]),
     "ym_conv_fwd": (R, [P, P, P, P, P, P, P, P]),
     "ym_conv_dgrad": (R, [P, P, P, P, P]),
     "ym_conv_wgrad_workspace_size": (SZ, [P]),
