@@ -6,6 +6,8 @@ set -o pipefail
 O=gpurun_out/r06_diag1
 rm -rf $O; mkdir -p $O
 export TMPDIR=/tmp
+# the MFMA-shape setter lives in the measurement library (make -C yolo-scratch_amd/csrc exp)
+export YOLOMI_LIB=$PWD/yolo-scratch_amd/libyolomi_exp.so
 for v in 0 1 2; do
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
       SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT --output-format csv -d $O/pmc_v$v -o run -- \
@@ -14,6 +16,7 @@ for v in 0 1 2; do
       SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/pmc2_v$v -o run -- \
       python3 tools/layer_bench.py --only 6 73 --reps 3 --set ym_conv_set_pipe_mfma=$v > $O/pmc2_v$v.log 2>&1 || exit 3
 done
+unset YOLOMI_LIB
 echo counters done
 timeout -k 10 400 python -u tools/step_ablate.py --steps 20 --rounds 3 > $O/ablate.txt 2>&1 || { tail -20 $O/ablate.txt; exit 4; }
 cat $O/ablate.txt
