@@ -11,7 +11,13 @@ the curve chaotic in the rounding: 16-bit storage alone moves single steps of th
 ~6 %, and any change of summation order (a different reduction split, a different kernel for one
 layer) moves the GPU curve by a similar amount at a few steps while its mean stays ~1 % — so the
 per-step bound follows the emulated oracle's own spread and the mean carries the parity claim.
-(The GPU step itself is bit-reproducible: tests/test_gpu_determinism.py.)"""
+(The GPU step itself is bit-reproducible: tests/test_gpu_determinism.py.)
+
+Run twice: with torch.optim.AdamW + clip_grad_norm_ (the reference's own optimizer tail, so the curve isolates the
+forward / loss / backward), and with the product optimizer, yolomi.optim.FusedAdamW(max_grad_norm=10) — the device
+norm + clip + AdamW launches train_yolo11_cuda.py uses — against the same bounds."""
+import functools
+
 import numpy as np
 import pytest
 import torch
@@ -19,16 +25,23 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(model, loss_fn, steps, dev):
+def _run(model, loss_fn, steps, dev, fused):
     from datasets.synthetic import synth_batch
-    opt = torch.optim.AdamW([p for p in model.parameters() if p.requires_grad], lr=1e-3, weight_decay=5e-4)
+    params = [p for p in model.parameters() if p.requires_grad]
+    if fused:
+        from yolomi.optim import FusedAdamW
+        opt = FusedAdamW(params, lr=1e-3, weight_decay=5e-4, max_grad_norm=10.0)
+        assert opt.fuses_clip
+    else:
+        opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
     out = []
     for step in range(steps):
         b = {k: v.to(dev) for k, v in synth_batch(4, 320, seed=100 + step).items()}
         opt.zero_grad(set_to_none=True)
         loss = loss_fn(model, b)
         loss.backward()
-        torch.nn.utils.clip_grad_norm_([p for p in model.parameters() if p.requires_grad], max_norm=10.0)
+        if not fused:
+            torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
         opt.step()
         out.append(float(loss))
     return np.asarray(out)
@@ -37,10 +50,36 @@ def _run(model, loss_fn, steps, dev):
 EMU_SAMPLES = 3
 
 
-def test_loss_curve_20_steps_vs_reference(golden):
+@functools.lru_cache(maxsize=None)
+def _emulated(steps, jitter):
+    """The loop on the CPU oracle under the HIP storage-rounding model (shared by both optimizer runs)."""
     from oracle import model as om
     from oracle import loss as ol
     from oracle.precision import hip_storage_rounding
+    from datasets.synthetic import synth_batch
+    torch.set_num_threads(8)
+    cfg = om.load_cfg("n")
+    layers, save, P2 = om.build(cfg)
+    params = [v.requires_grad_(True) for k, v in P2.items()
+              if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")]
+    opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
+    emu = []
+    for step in range(steps):
+        b = synth_batch(4, 320, seed=100 + step)
+        opt.zero_grad(set_to_none=True)
+        with hip_storage_rounding(jitter=jitter):
+            heads = om.forward(P2, layers, save, b["img"], training=True)
+        loss = ol.v8_loss(heads, b)[0]
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
+        opt.step()
+        emu.append(float(loss))
+    return np.asarray(emu)
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["torch_adamw", "fused_adamw"])
+def test_loss_curve_20_steps_vs_reference(golden, fused):
+    from oracle import model as om
     from models import build_yolo11
     from losses import v8DetectionLoss
     d = golden("curve.npz")
@@ -53,33 +92,11 @@ def test_loss_curve_20_steps_vs_reference(golden):
     m.load_state_dict(P)
     m = m.cuda().train()
     crit = v8DetectionLoss(m, tal_topk=10)
-    gpu = _run(m, lambda mod, b: crit(mod(b["img"]), b)[0], steps, torch.device("cuda"))
-
-    # the same loop on the CPU oracle under the HIP storage-rounding model
-    from datasets.synthetic import synth_batch
-    torch.set_num_threads(8)
-
-    def emulated(jitter):
-        layers, save, P2 = om.build(cfg)
-        params = [v.requires_grad_(True) for k, v in P2.items()
-                  if v.is_floating_point() and "running" not in k and not k.endswith("dfl.conv.weight")]
-        opt = torch.optim.AdamW(params, lr=1e-3, weight_decay=5e-4)
-        emu = []
-        for step in range(steps):
-            b = synth_batch(4, 320, seed=100 + step)
-            opt.zero_grad(set_to_none=True)
-            with hip_storage_rounding(jitter=jitter):
-                heads = om.forward(P2, layers, save, b["img"], training=True)
-            loss = ol.v8_loss(heads, b)[0]
-            loss.backward()
-            torch.nn.utils.clip_grad_norm_(params, max_norm=10.0)
-            opt.step()
-            emu.append(float(loss))
-        return np.asarray(emu)
+    gpu = _run(m, lambda mod, b: crit(mod(b["img"]), b)[0], steps, torch.device("cuda"), fused)
 
     # the rounding model's spread over EMU_SAMPLES draws (oracle/precision.py: the curve is a chaotic
     # function of last-bit differences after a few steps), worst per step
-    emus = [emulated(j) for j in range(EMU_SAMPLES)]
+    emus = [_emulated(steps, j) for j in range(EMU_SAMPLES)]
     err = np.abs(gpu - ref) / ref
     err_emu = np.max([np.abs(e - ref) / ref for e in emus], axis=0)
     print("gpu rel err", np.round(err, 4).tolist())

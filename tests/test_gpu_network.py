@@ -383,3 +383,23 @@ def test_model_ch3_train_step_vs_oracle():
         y, _ = m(gb["img"])
         ry, _ = om.forward(P, layers, save, b["img"], training=False)
     assert rel(y, ry) < 1e-2, rel(y, ry)
+
+
+def test_model_non_square_odd_batch_train_step_vs_oracle():
+    """A non-square input (96 x 160, multiples of the 32-pixel stride) at an odd batch (3) through a whole s-scale
+    training step against the CPU oracle by check_network — the shapes test_gpu_scales.py covers only for finiteness.
+    The loss scales the normalized targets by the first level's (H, W) * stride repeated, [H, W, H, W], exactly as the
+    reference's preprocess does (yolo_v8_loss.py:400, 514: its comment says [W, H, W, H]); the oracle restates that."""
+    from losses import v8DetectionLoss
+    from datasets.synthetic import synth_batch
+    b = synth_batch(3, 128, seed=19)
+    b["img"] = torch.rand(3, 1, 96, 160, generator=torch.Generator().manual_seed(19))
+    m = _seeded_model("s").train()
+    gb = {k: v.cuda() for k, v in b.items()}
+    heads = m(gb["img"])
+    assert tuple(heads[0].shape[2:]) == (12, 20)
+    loss, items = v8DetectionLoss(m)(heads, gb)
+    ref_heads, rl, ri, ref_norm, full = _oracle_step("s", b, full_keys=("model.0.conv.weight",))
+    worst = check_network("s", heads, loss, items, m, ref_heads, rl, ri, ref_norm, full, b["img"],
+                          {k: v for k, v in b.items() if k != "img"}, emu_samples=3)
+    print("worst err/tol", worst)
