@@ -96,6 +96,10 @@ int ym_conv_set_pipe_mfma(int mode);
  * 0 (default) stage DMAs first after the barrier, the next stage's fragment reads late; 1 every fragment read pinned ahead of the half step of MFMAs it covers.  Returns the
  * previous setting. */
 int ym_conv_set_pipe_order(int mode);
+/* Loop form of the pipelined kernel's single-class training instances (round 6): 0 one flat loop over the workgroup's K
+ * steps, 1 nested tiles x K steps with each tile's first step peeled, 2 (default, shipped) as 1 with the LDS ring slot
+ * carried as a byte offset.  Out of range restores 2.  Returns the previous setting. */
+int ym_conv_set_pipe_loop(int mode);
 #endif
 
 #ifdef __cplusplus

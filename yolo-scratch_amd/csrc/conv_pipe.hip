@@ -52,6 +52,7 @@ Policy g_pipe_force{-1};
 #ifdef YM_EXPERIMENTS
 Policy g_pipe_mfma{0};
 Policy g_pipe_order{0};   // also conv_hpipe.hip (conv_pipe.h)
+Policy g_pipe_loop{2};    // conv_pipe_kernel LP of the single-class path (2 shipped)
 Policy g_pipe_exp{0};
 #else
 constexpr int g_pipe_exp = 0;
@@ -364,14 +365,23 @@ struct Issuer {
 // second-half reads into the middle of the first half); 1: every fragment read is pinned ahead of the MFMAs it covers —
 // the second-half reads at the top of the step, the next stage's first-half reads right after the barrier, ahead of
 // the DMAs — so each read has a whole half (TM * TN * KS MFMAs per wave) of cover
+// LP: loop form of the single-class path (round 6).  0: one flat loop over the workgroup's K steps whose body tests for
+// a tile's first step (accumulator reset, the wait that leaves the previous epilogue's stores in flight) and last step
+// (epilogue) every iteration; 1: tiles x K steps as two nested loops — the tile's first step peeled with its own wait,
+// the inner loop a bare K step; 2 (shipped for the training instances since round 6): as 1 with the ring slot carried as
+// a byte offset (an add instead of a multiply) and the stream-end test against a hoisted limit.  ~22 instead of ~33
+// scalar instructions per common K step; same-process layer A/B (profiles/r06/pipe_loop_ab.txt) -1..-5 % on most
+// pipelined layers (op 71 fwd -11.6 %), op 73 fwd +1.5 %; the whole step within +-0.2 % (the launches overlap other
+// streams' work there).  The eval instance keeps 0 (not measured)
 template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false,
-          bool EV = false, int MF = 16, int RO = 0>
+          bool EV = false, int MF = 16, int RO = 0, int LP = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, EvalArgs e) {
     static_assert(!EV || (C1 && MODE == PF && ABL == 0), "the eval instance is a single-class forward");
     static_assert(MF == 16 || MF == 32, "MFMA shape");
     // NS: LDS ring of K stages — stage g computing, g+1 .. g+NS-1 in flight (3; 2 for the 64-KB+ stages of the
     // 256-channel / 512-pixel tiles)
     static_assert(NS == 2 || NS == 3, "ring depth");
+    static_assert(LP == 0 || C1, "the nested loop form is the single-class path's");
     constexpr int RB = 128;                   // 64 K x 2 B per LDS row
     constexpr int NW = WM * WN;
     constexpr int AI = BN / 8 / NW;           // weight DMA instructions per wave per stage
@@ -438,11 +448,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
             offB[kk * KS + s] = uint32_t(BN * RB + rb * RB + ((ch ^ fsw128(rb)) << 4));
         }
     bf16x8 f0a[TM * KS], f0b[TN * KS], f1a[TM * KS], f1b[TN * KS];
-    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int buf, int kk) {
+    auto read_frags = [&](bf16x8* fa, bf16x8* fb, int slot_off, int kk) {     // slot_off: the ring slot's byte offset
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
-            const char* As = smem + buf * STAGE + offA[kk * KS + s];
-            const char* Bs = smem + buf * STAGE + offB[kk * KS + s];
+            const char* As = smem + slot_off + offA[kk * KS + s];
+            const char* Bs = smem + slot_off + offB[kk * KS + s];
 #pragma unroll
             for (int i = 0; i < TM; ++i) fa[i * KS + s] = *reinterpret_cast<const bf16x8*>(As + i * MF * RB);
 #pragma unroll
@@ -510,6 +520,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
     vm_wait<(NS - 1) * DPS>();
     step_barrier();
     if (total > 0) read_frags(f0a, f0b, 0, 0);
+    int boff = 0;                             // LP 2: the computing slot's byte offset (buf * STAGE)
 
     // compute side: one K step per iteration; tiles end inside the stream
     int ct = 0, ck = 0, cnk = C1 ? a.KH * a.KW * kc : 0, buf = 0;
@@ -526,27 +537,12 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
         c_tp = uint32_t(c_m0) - uint32_t(c_tn) * is.ohw;
     }
     const int Mtot = a.N * int(is.ohw);
-    for (int g = 0; g < total; ++g) {
-        if (C1 && ck == 0) {
-            if (ct > 0) {
-                c_m0 += is.m_step;
-                c_tn += is.step_n;
-                c_tp += is.step_p;
-                if (c_tp >= is.ohw) { c_tp -= is.ohw; ++c_tn; }
-            }
-            zero_acc();
-        } else if (ck == 0) {
-            const int mt = mt_lo + ct * qstride;
-            const int c = cls_find(a, mt);
-            cc = cls_of(a, c);
-            m0 = int64_t(mt - a.mt_pre[c]) * BM;
-            t_n = uint32_t(m0) / cc.OHW;
-            t_p = uint32_t(m0) - t_n * cc.OHW;
-            inv_owc = 1.0f / float(cc.OWc);
-            cnk = cc.ntap * kc;
-            zero_acc();
-        }
-        read_frags(f1a, f1b, buf, 1);
+    // one K step: the second half's fragments read and the first half's MFMAs; the wait and barrier; stage g+NS's DMAs
+    // into the freed slot between the second half's MFMAs; the next stage's first-half reads.  keep_epi: a tile's
+    // first step after an epilogue, whose stores may stay in flight across the wait; live: stage g+NS is in the stream
+    auto kstep = [&](bool keep_epi, bool live) __attribute__((always_inline)) {
+        const int cur = LP == 2 ? boff : buf * STAGE;
+        read_frags(f1a, f1b, cur, 1);
         mma(f0a, f0b);
         constexpr int MH = TM * TN * KS;                                            // MFMAs per half
         if constexpr (RO == 1) {
@@ -556,15 +552,16 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
         // stage g+1 must have landed (own DMAs); stage g+2 may stay in flight (every step issues DPS DMAs,
         // live or not, so the count is constant); in a tile's first step the previous tile's epilogue stores,
         // issued after stage g+2's pieces, may stay in flight too
-        if (EPI == 2 && ck == 0 && ct > 0) vm_wait<(NS - 2) * DPS + EPS>();
+        if (keep_epi) vm_wait<(NS - 2) * DPS + EPS>();
         else vm_wait<(NS - 2) * DPS>();
         step_barrier();
         // the slot of stage g is free again (every wave's reads of it returned before the barrier): stage
         // g+3's DMAs go out one at a time between the second half's MFMAs (issued in a burst they held both
         // waves of a SIMD off the MFMA pipe for the whole burst), then the next stage's first-half reads
         const int nbuf = buf == NS - 1 ? 0 : buf + 1;
-        is.issue_dma(smem + buf * STAGE, wres, a_off, g + NS < total);
-        read_frags(f0a, f0b, nbuf, 0);
+        const int nboff = boff == (NS - 1) * STAGE ? 0 : boff + STAGE;
+        is.issue_dma(smem + cur, wres, a_off, live);
+        read_frags(f0a, f0b, LP == 2 ? nboff : nbuf * STAGE, 0);
         mma(f1a, f1b);
         if constexpr (RO == 1) {
             __builtin_amdgcn_sched_group_barrier(0x100, (TM + TN) * KS, 0);        // next-stage reads first
@@ -584,11 +581,11 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
             __builtin_amdgcn_sched_group_barrier(0x008, MH - DPS * (MH / (DPS + 1)), 0);
         }
         is.advance();
-        buf = nbuf;
-        if (++ck < cnk) continue;
-        ck = 0;
-        ++ct;
-
+        if constexpr (LP == 2) boff = nboff;
+        else buf = nbuf;
+    };
+    // the tile's epilogue
+    auto epilogue = [&]() __attribute__((always_inline)) {
         // epilogue: D[channel][pixel] (a lane holds 4 consecutive channels of one pixel per subtile) is
         // transposed in registers (conv_epi.h epilogue_regs: pairs of 16-pixel subtiles exchanged with
         // v_permlane16_swap), so every store is a 16-B piece of a pixel's contiguous channel run, issued as
@@ -642,6 +639,56 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
                     epilogue_regs32_x<TM, TN>(acc, ssum, ssq, a.st_sum != nullptr, lane, wch0, a.Nout, yres,
                                               a.out_f32 == 2, a.accumulate != 0, pix_off, pix_ok, nullptr, pix_off);
             }
+        }
+    };
+    if constexpr (LP >= 1) {
+        int g = 0;
+        for (int t = 0; t < ntile; ++t) {
+            if (t > 0) {
+                c_m0 += is.m_step;
+                c_tn += is.step_n;
+                c_tp += is.step_p;
+                if (c_tp >= is.ohw) { c_tp -= is.ohw; ++c_tn; }
+            }
+            zero_acc();
+            kstep(EPI == 2 && t > 0, g + NS < total);
+            ++g;
+            if constexpr (LP == 2) {
+                // the stream's last NS stages fetch nothing: live while g < glim
+                const int glim = total - NS;
+                for (int k = 1; k < cnk; ++k, ++g) kstep(false, g < glim);
+            } else {
+                for (int k = 1; k < cnk; ++k, ++g) kstep(false, g + NS < total);
+            }
+            epilogue();
+        }
+    } else {
+        for (int g = 0; g < total; ++g) {
+            if (C1 && ck == 0) {
+                if (ct > 0) {
+                    c_m0 += is.m_step;
+                    c_tn += is.step_n;
+                    c_tp += is.step_p;
+                    if (c_tp >= is.ohw) { c_tp -= is.ohw; ++c_tn; }
+                }
+                zero_acc();
+            } else if (ck == 0) {
+                const int mt = mt_lo + ct * qstride;
+                const int c = cls_find(a, mt);
+                cc = cls_of(a, c);
+                m0 = int64_t(mt - a.mt_pre[c]) * BM;
+                t_n = uint32_t(m0) / cc.OHW;
+                t_p = uint32_t(m0) - t_n * cc.OHW;
+                inv_owc = 1.0f / float(cc.OWc);
+                cnk = cc.ntap * kc;
+                zero_acc();
+            }
+            kstep(EPI == 2 && ck == 0 && ct > 0, g + NS < total);
+            if (++ck < cnk) continue;
+            ck = 0;
+            ++ct;
+
+            epilogue();
         }
     }
 
@@ -699,12 +746,12 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}, {256, 128}};
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
 // cfg 0 / 1 / 2 tiles (kCfg) of one control path (C1), MFMA shape (MF) and issue order (RO)
-template <int MODE, bool C1, int MF, int RO>
+template <int MODE, bool C1, int MF, int RO, int LP = 0>
 void launch_tiles(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     switch (cfg) {
-        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
-        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
-        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, C1, false, MF, RO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
+        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
     }
 }
 
@@ -730,14 +777,16 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
             else launch_tiles<MODE, true, 32, 0>(c, a, grid, st);
         } else {
             if (ro) launch_tiles<MODE, true, 16, 1>(c, a, grid, st);
-            else launch_tiles<MODE, true, 16, 0>(c, a, grid, st);
+            else if (g_pipe_loop == 0) launch_tiles<MODE, true, 16, 0, 0>(c, a, grid, st);
+            else if (g_pipe_loop == 1) launch_tiles<MODE, true, 16, 0, 1>(c, a, grid, st);
+            else launch_tiles<MODE, true, 16, 0, 2>(c, a, grid, st);
         }
         return;
     }
     if (mf != 0) launch_tiles<MODE, false, 32, 0>(c, a, grid, st);
     else launch_tiles<MODE, false, 16, 0>(c, a, grid, st);
 #else
-    if (c1) launch_tiles<MODE, true, 16, 0>(cfg, a, grid, st);
+    if (c1) launch_tiles<MODE, true, 16, 0, 2>(cfg, a, grid, st);
     else launch_tiles<MODE, false, 16, 0>(cfg, a, grid, st);
 #endif
 }
@@ -812,6 +861,12 @@ PipePlan pipe_plan(const ym_conv_desc* d, int dgrad) {
 extern "C" int ym_conv_set_pipe_order(int mode) {
     // K-step issue order of the pipelined kernel (conv_pipe_kernel RO: 0 default, 1 fragment reads pinned first)
     return g_pipe_order.set(mode < 0 || mode > 1 ? 0 : mode);
+}
+
+extern "C" int ym_conv_set_pipe_loop(int mode) {
+    // loop form of the pipelined kernel's single-class path (conv_pipe_kernel LP: 0 flat, 1 nested tiles x K steps,
+    // 2 nested with the slot offset carried)
+    return g_pipe_loop.set(mode < 0 || mode > 2 ? 2 : mode);
 }
 
 extern "C" int ym_conv_set_pipe_mfma(int mode) {
