@@ -1,4 +1,4 @@
-"""Per-kernel-family dynamic instruction mix from a rocprofv3 --pmc CSV (tools/r05_insts.sh): summed over all
+"""Per-kernel-family dynamic instruction mix from a rocprofv3 --pmc CSV (tools/r05/insts.sh): summed over all
 dispatches of each kernel template, instructions per MFMA (or per wave where a kernel has no MFMA) and time."""
 import collections
 import csv

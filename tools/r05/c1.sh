@@ -3,7 +3,7 @@
 # parity (conv kernel tests + per-layer teacher-forced test), same-process A/B against the generic control path
 # (ym_pipe_set_exp 20) and hpipe vs pipe on the 128-channel 3x3 layers (ym_conv_set_hpipe 2), instruction counts.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r05_c1; mkdir -p $OUT
 rm -f $OUT/*.log $OUT/*.txt
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # round 5: parity of the new conv control paths (kernel tests, per-layer teacher-forced test at the bench's kernel
 # selection) and a bench line
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r05_c1b; mkdir -p $OUT
 export TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"

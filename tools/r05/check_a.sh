@@ -3,7 +3,7 @@
 # the new BatchNorm tests (m*c >= 2^26 reduce + finalize vs fp64; fold vs two launches on in-model inputs) and the
 # headline-geometry network test (s@640 bs64 vs the CPU oracle), then a default bench line.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 mkdir -p gpurun_out/r05a
 T="python -u -m pytest -v -s --timeout 120 --timeout-method thread"
 timeout -k 10 200 $T tests/test_gpu_bn.py -k in_model > gpurun_out/r05a/fold.log 2>&1

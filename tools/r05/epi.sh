@@ -3,7 +3,7 @@
 # and soffset DMAs, conv_gemm's float-reciprocal pixel decompositions — parity, then same-box per-layer A/B against the
 # library before these changes (ab/libyolomi_base.so = commit fcbffaf), then a bench line
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r05_epi; mkdir -p $OUT
 export TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 300 --timeout-method thread"

@@ -2,7 +2,7 @@
 # round 5: what bounds conv_pipe — same-process ablations (ym_pipe_set_exp 10: every stage DMA out of range, 11: no
 # MFMAs, 12: only the input's DMAs out of range, 13: only the weights') and memory-path counters of op 73's forward.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r05_pipe_abl; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/pipe_ab.py ym_pipe_set_exp --only 10 52 73 78 11 6 \

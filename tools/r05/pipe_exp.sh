@@ -3,7 +3,7 @@
 # tile (32 x 64 per wave) against 8 waves of 64 x 64 (ym_pipe_set_exp 1), and SQ counter passes (LDS activity,
 # MFMA busy, wave states) over ops 73 / 6 for both.
 set -o pipefail
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 OUT=gpurun_out/r05_pipe_exp; mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/pipe_ab.py ym_pipe_set_exp --only 6 10 11 20 47 48 52 73 74 78 79 \
