@@ -336,14 +336,14 @@ def test_model_80_classes_train_step_vs_oracle():
         np.testing.assert_array_equal(g["labels"].cpu().numpy(), rlab)
 
 
-@pytest.mark.parametrize("scale,imgsz", [("l", 128)])
+@pytest.mark.parametrize("scale,imgsz", [("l", 256), ("x", 256)])
 def test_model_l_x_train_step_vs_oracle(scale, imgsz):
-    """The l scale of the reference's yaml (configs/yolo11n_crater.yaml `scales`) through a whole training step at
-    128x128 bs2 against the CPU oracle by check_network — the scales test_gpu_scales.py covers only for finiteness.
-    (x@128 bs2 was run here too: heads, loss / items and every gradient but one pass; the stem weight gradient is 0.305
-    from the oracle at the GPU's heads, above NET_CAP 0.3 and within the rounding model's own spread — the backbone's
-    SPPF-routing chaos at 4x4 maps.  x is pinned layer by layer instead: test_gpu_layers.py's x@128 teacher-forced case
-    at 1e-2.)"""
+    """The l and x scales of the reference's yaml (configs/yolo11n_crater.yaml `scales`) through a whole training step at
+    256x256 bs2 against the CPU oracle by check_network — the scales test_gpu_scales.py covers only for finiteness.
+    256, not 128: at 128 the deepest maps are 4x4 and the backbone's SPPF max-pool routing makes single gradients
+    chaotic in last-bit differences — l@128 measured 0.303 (model.22.m.1.m.0.cv1.conv.weight) and x@128 0.305 (the stem
+    weight) against NET_CAP 0.3, each inside the rounding model's own spread; at 256 the largest are 0.254 (l) and 0.295
+    (x).  Both scales stay pinned layer by layer too (test_gpu_layers.py x@128, 1e-2)."""
     from losses import v8DetectionLoss
     from datasets.synthetic import synth_batch
     b = synth_batch(2, imgsz, seed=90)
