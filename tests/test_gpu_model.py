@@ -290,11 +290,11 @@ def test_sppf_fused_chain_bit_identical(H, W, C, B):
     assert torch.equal(gbuf, gref)
 
 
-def _emulated_heads(scale, img, nc=5, ch=1):
+def _emulated_heads(scale, img, nc=5, ch=1, jitter=0):
     from oracle import model as om
     from oracle.precision import hip_storage_rounding
     layers, save, P = om.build(om.load_cfg(scale), ch=ch, nc=nc)
-    with torch.no_grad(), hip_storage_rounding():
+    with torch.no_grad(), hip_storage_rounding(jitter=jitter):
         return om.forward(P, layers, save, torch.as_tensor(img), training=True)
 
 

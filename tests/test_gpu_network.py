@@ -67,12 +67,22 @@ def check_network(scale, heads, loss, items, model, ref_heads, ref_loss, ref_ite
         r = rel(heads[i], ref_heads[i])
         bound = max(1e-2, 1.2 * rel(emu_h[i], ref_heads[i]))
         assert r < bound, ("head", i, r, bound)
-    # loss / items: 1e-2, or 1.2 x the rounding model's own error where that is larger (the loss is a discrete function of
-    # the heads — assignment, IoU^4-weighted targets — so head rounding moves it; seen at l@128: cls item 1.4 %)
-    emu_l, emu_i = ol.v8_loss([h.detach() for h in emu_h], batch_cpu, nc=nc)
-    lb = max(1e-2, 1.2 * abs(float(emu_l) - float(ref_loss)) / abs(float(ref_loss)))
+    # loss / items, twice.  (a) the fused loss itself: against the oracle's loss (oracle/loss.py, fp32) evaluated on the
+    # GPU's own head maps, 1e-3 — this pins the assigner + CIoU / DFL / BCE path exactly, whatever the heads' rounding.
+    # (b) against the reference's loss on the reference's heads: the loss is a discrete function of the heads
+    # (assignment, IoU^4-weighted targets), so head rounding moves it — bound 1e-2 for the total and 2e-2 for the items
+    # vector, or 1.2 x the rounding model's own error where larger (its worst over the unperturbed draw and
+    # emu_samples - 1 jittered ones).  Measured (profiles/r06/non_square_items_diag.txt): the class item of s at
+    # 160x96 bs3 is 2.3 % off in one rounding-model draw and 0.02 % in another; the GPU's is 0.06 % there and 1.2 % at
+    # 96x160 with heads as close to the oracle as the rounding model's; l@128's 1.4 %
+    gl, gi = ol.v8_loss([h.detach().cpu().float() for h in heads], batch_cpu, nc=nc)
+    assert abs(float(loss) - float(gl)) <= 1e-3 * abs(float(gl)), (float(loss), float(gl))
+    assert rel(items, gi) < 1e-3, (items.tolist(), gi.tolist())
+    emu_all = [emu_h] + [_emulated_heads(scale, img, jitter=j, **bk) for j in range(1, emu_samples)]
+    emu_li = [ol.v8_loss([h.detach() for h in e], batch_cpu, nc=nc) for e in emu_all]
+    lb = max(1e-2, 1.2 * max(abs(float(el) - float(ref_loss)) / abs(float(ref_loss)) for el, _ in emu_li))
     assert abs(float(loss) - float(ref_loss)) / abs(float(ref_loss)) < lb, (float(loss), float(ref_loss), lb)
-    ib = max(1e-2, 1.2 * rel(emu_i, ref_items))
+    ib = max(2e-2, 1.2 * max(rel(ei, ref_items) for _, ei in emu_li))
     assert rel(items, ref_items) < ib, (items.tolist(), list(ref_items), ib)
     loss.backward()
     hg = [h.detach().cpu().clone().requires_grad_(True) for h in heads]
