@@ -100,6 +100,9 @@ int ym_conv_set_pipe_order(int mode);
  * steps, 1 nested tiles x K steps with each tile's first step peeled, 2 (default, shipped) as 1 with the LDS ring slot
  * carried as a byte offset.  Out of range restores 2.  Returns the previous setting. */
 int ym_conv_set_pipe_loop(int mode);
+/* Tap lookahead of the 3x3 weight-gradient kernel (round 6): 0 each tap's input fragments read right before its MFMAs,
+ * 1 one tap ahead.  Out of range restores the shipped setting.  Returns the previous setting. */
+int ym_wgrad_set_lookahead(int la);
 #endif
 
 #ifdef __cplusplus

@@ -83,7 +83,11 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* p_lo, const char* p_hi) {
 // t + 1 and t + 2 are in flight.
 // DB: two LDS buffers — the next unit is written into the other buffer while this one is multiplied, one
 // barrier per unit (single buffer: the store between two barriers, every wave off the MFMA pipe meanwhile).
-template <int S, int TCO, int TCI, int WCO, int WCI, int TW, int TH, bool DEEP, bool DB = false>
+// LA: tap lookahead in the multiply (round 6).  0: each tap's ci fragments are read right before its TI x TJ MFMAs (hipcc
+// keeps one fragment set live: every tap waits lgkmcnt(0) for its own reads, 18 exposed LDS round trips per unit);
+// 1: tap t+1's fragments are read ahead of tap t's MFMAs into a second set (TJ x 4 more VGPRs), so each read has one
+// tap of MFMAs to land behind
+template <int S, int TCO, int TCI, int WCO, int WCI, int TW, int TH, bool DEEP, bool DB = false, int LA = 0>
 __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(WgArgs a) {
     constexpr int NWC = TCI / WCI;            // waves along ci
     constexpr int NWV = (TCO / WCO) * NWC;
@@ -212,6 +216,33 @@ __global__ void __launch_bounds__((TCO / WCO) * (TCI / WCI) * 64) wgrad3_kernel(
             for (int i = 0; i < TI; ++i) {
                 const int col = (wr * WCO + i * 16 + 4 * pp) * 2;
                 af[i] = tr_frag(Dz + (kk * 32 + 4 * g + q) * RSD + col, Dz + (kk * 32 + 16 + 4 * g + q) * RSD + col);
+            }
+            if constexpr (LA == 1) {
+                auto read_tap = [&](bf16x8 (&bfr)[TJ], int tap) {
+                    const int toff = (tap / 3) * HW + tap % 3;
+#pragma unroll
+                    for (int j = 0; j < TJ; ++j) {
+                        const int col = (wc * WCI + j * 16 + 4 * pp) * 2;
+                        bfr[j] = tr_frag(Xh + (hl[kk] + toff) * RSX + col, Xh + (hh[kk] + toff) * RSX + col);
+                    }
+                };
+                bf16x8 bq[2][TJ];
+                read_tap(bq[0], 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2 * TI + 2 * TJ, 0);  // the co fragments and tap 0's
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap) {
+                    if (tap + 1 < 9) read_tap(bq[(tap + 1) & 1], tap + 1);
+#pragma unroll
+                    for (int i = 0; i < TI; ++i)
+#pragma unroll
+                        for (int j = 0; j < TJ; ++j)
+                            acc[tap][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bq[tap & 1][j], acc[tap][i][j],
+                                                                                      0, 0, 0);
+                    // the next tap's reads go out ahead of this tap's MFMAs
+                    if (tap + 1 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 2 * TJ, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, TI * TJ, 0);
+                }
+                continue;
             }
 #pragma unroll
             for (int kh = 0; kh < 3; ++kh)
@@ -593,6 +624,12 @@ struct WgPlan {
 // 0.161, profiles/r05/at_589d336): kept at 256, the gain inside the run-to-run spread
 Policy g_wg_target{256};
 
+// tap lookahead of the shipped wgrad3 instances (wgrad3_kernel LA)
+constexpr int kWgLA = 0;
+#ifdef YM_EXPERIMENTS
+Policy g_wg_la{kWgLA};
+#endif
+
 WgPlan wg_plan(const ym_conv_desc* d) {
     WgPlan p{};
     const int64_t M = int64_t(d->n) * d->oh * d->ow;
@@ -647,10 +684,52 @@ WgPlan wg_plan(const ym_conv_desc* d) {
 
 }  // namespace
 
+#ifdef YM_EXPERIMENTS
+extern "C" int ym_wgrad_set_lookahead(int la) {
+    // wgrad3_kernel LA: 0 each tap's fragments read right before its MFMAs, 1 one tap ahead; out of range restores the
+    // shipped setting; returns the previous one
+    return g_wg_la.set(la < 0 || la > 1 ? kWgLA : la);
+}
+#endif
+
 extern "C" int ym_wgrad_set_target(int wgs) {
     // workgroups per weight-gradient launch the split-K plan aims for (default 256; <= 0 restores it); returns the
     // previous setting
     return g_wg_target.set(wgs <= 0 ? 256 : wgs);
+}
+
+template <int LA>
+void wg3_launch(const ym_conv_desc* d, const WgPlan& p, const WgArgs& a, dim3 grid, hipStream_t st) {
+    const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
+#define WG3_LAUNCH(S_, D_, B_)                                                                                    \
+        if (p.tw == 20) {                                                                                   \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 20, 3, false, B_, LA>), grid, dim3(512), 0, st, a); \
+        } else if (p.tw == 10) {                                                                            \
+            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 10, 6, false, B_, LA>), grid, dim3(512), 0, st, a); \
+        } else {                                                                                            \
+            switch (tc) {                                                                                   \
+                case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 8, 8, D_, B_, LA>), grid, dim3(512), 0, st, a); break; \
+                case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 64, 16, 16, 8, 8, D_, B_, LA>), grid, dim3(512), 0, st, a); break; \
+                case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 32, 32, 16, 8, 8, D_, B_, LA>), grid, dim3(256), 0, st, a); break; \
+                default: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 32, 16, 16, 8, 8, D_, B_, LA>), grid, dim3(256), 0, st, a); break; \
+            }                                                                                               \
+        }
+    // two LDS buffers on the stride-1 layers and the deep stride-2 ones (same-process A/B: -4..-10 % on the
+    // 80x80 / 160x160 layers, +3.5..+4.8 % on the narrow stride-2 maps; profiles/r04/wgrad3_db_ab.txt)
+    if (d->stride == 1 || p.deep) {
+        if (d->stride == 1) {
+            if (p.deep) { WG3_LAUNCH(1, true, true) } else { WG3_LAUNCH(1, false, true) }
+        } else {
+            if (p.deep) { WG3_LAUNCH(2, true, true) } else { WG3_LAUNCH(2, false, true) }
+        }
+    } else {
+        if (d->stride == 1) {
+            if (p.deep) { WG3_LAUNCH(1, true, false) } else { WG3_LAUNCH(1, false, false) }
+        } else {
+            if (p.deep) { WG3_LAUNCH(2, true, false) } else { WG3_LAUNCH(2, false, false) }
+        }
+    }
+#undef WG3_LAUNCH
 }
 
 int wgrad_kernel(const ym_conv_desc* d, char* name, size_t len) {
@@ -715,36 +794,12 @@ extern "C" int ym_conv_wgrad(const ym_conv_desc* d, const uint16_t* dz, const ui
     } else if (p.kind == 3) {
         YM_CHECK_ARG(int64_t(d->h) * d->w * d->x_ld * 2 < (int64_t(1) << 31), "ym_conv_wgrad: image too large");
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
-        const int tc = (p.T == 32 ? 1 : 0) | (p.T2 == 32 ? 2 : 0);     // bit 0: 32-co, bit 1: 32-ci tile
-#define WG3_LAUNCH(S_, D_, B_)                                                                                    \
-        if (p.tw == 20) {                                                                                   \
-            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 20, 3, false, B_>), grid, dim3(512), 0, st, a); \
-        } else if (p.tw == 10) {                                                                            \
-            hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 10, 6, false, B_>), grid, dim3(512), 0, st, a); \
-        } else {                                                                                            \
-            switch (tc) {                                                                                   \
-                case 0: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 64, 32, 16, 8, 8, D_, B_>), grid, dim3(512), 0, st, a); break; \
-                case 1: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 64, 16, 16, 8, 8, D_, B_>), grid, dim3(512), 0, st, a); break; \
-                case 2: hipLaunchKernelGGL((wgrad3_kernel<S_, 64, 32, 32, 16, 8, 8, D_, B_>), grid, dim3(256), 0, st, a); break; \
-                default: hipLaunchKernelGGL((wgrad3_kernel<S_, 32, 32, 16, 16, 8, 8, D_, B_>), grid, dim3(256), 0, st, a); break; \
-            }                                                                                               \
-        }
-        // two LDS buffers on the stride-1 layers and the deep stride-2 ones (same-process A/B: -4..-10 % on the
-        // 80x80 / 160x160 layers, +3.5..+4.8 % on the narrow stride-2 maps; profiles/r04/wgrad3_db_ab.txt)
-        if (d->stride == 1 || p.deep) {
-            if (d->stride == 1) {
-                if (p.deep) { WG3_LAUNCH(1, true, true) } else { WG3_LAUNCH(1, false, true) }
-            } else {
-                if (p.deep) { WG3_LAUNCH(2, true, true) } else { WG3_LAUNCH(2, false, true) }
-            }
-        } else {
-            if (d->stride == 1) {
-                if (p.deep) { WG3_LAUNCH(1, true, false) } else { WG3_LAUNCH(1, false, false) }
-            } else {
-                if (p.deep) { WG3_LAUNCH(2, true, false) } else { WG3_LAUNCH(2, false, false) }
-            }
-        }
-#undef WG3_LAUNCH
+#ifdef YM_EXPERIMENTS
+        if (g_wg_la == 0) wg3_launch<0>(d, p, a, grid, st);
+        else wg3_launch<1>(d, p, a, grid, st);
+#else
+        wg3_launch<kWgLA>(d, p, a, grid, st);
+#endif
     } else if (p.kind == 1) {
         const dim3 grid(unsigned(p.co_t * p.ci_t * splits));
         if (p.T == 128)
