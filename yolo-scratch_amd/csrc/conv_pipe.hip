@@ -53,6 +53,7 @@ Policy g_pipe_force{-1};
 Policy g_pipe_mfma{0};
 Policy g_pipe_order{0};   // also conv_hpipe.hip (conv_pipe.h)
 Policy g_pipe_loop{2};    // conv_pipe_kernel LP of the single-class path (2 shipped)
+Policy g_pipe_taporder{0};   // conv_pipe_kernel TO of the single-class path (0 shipped)
 Policy g_pipe_exp{0};
 #else
 constexpr int g_pipe_exp = 0;
@@ -160,7 +161,11 @@ __device__ __forceinline__ void step_barrier() {
 // buffer resource over the tile's images is built once per tile.  (Round 5: the generic form spent ~3.8 SALU
 // and ~3.5 VALU per MFMA, SQ_INSTS_* over op 73, much of it the per-tile class search and 32-bit divisions of
 // both the issue and the compute side; its no-MFMA ablation alone ran 107 of the layer's 145 us.)
-template <int BM, int BN, int NW, int MODE, int ABL = 0, bool C1 = false>
+// TO (round 6, single-class path only): K order of the stage stream.  0: channel chunk innermost — (tap 0, chunk 0),
+// (tap 0, chunk 1), .., (tap 1, chunk 0), ..; 1: tap innermost — every tap of channel chunk 0, then of chunk 1, so
+// the taps that re-read the same input pixels run back to back and their overlap comes from L2 (one 64-channel
+// chunk's footprint per tile instead of every chunk's)
+template <int BM, int BN, int NW, int MODE, int ABL = 0, bool C1 = false, int TO = 0>
 struct Issuer {
     static constexpr int AI = BN / 8 / NW, BI = BM / 8 / NW, RB = 128;
     const PipeArgs& a;
@@ -326,6 +331,27 @@ struct Issuer {
 
     // advance the stream position by one stage (new tap: its gather offsets; new tile: its pixels)
     __device__ __forceinline__ void advance() {
+        if constexpr (TO == 1) {
+            static_assert(C1, "tap-innermost order: single-class path");
+            if (++tj == nkw) {
+                tj = 0;
+                if (++ti == nrows) {
+                    ti = 0;
+                    if (++kci == kc) {
+                        kci = 0;
+                        if (++i < ntile) {
+                            m0 += m_step;
+                            tn += step_n;
+                            tp += step_p;
+                            if (tp >= ohw) { tp -= ohw; ++tn; }
+                            tile_setup();
+                        }
+                    }
+                }
+            }
+            tap_setup();
+            return;
+        }
         if (++kci == kc) {
             kci = 0;
             if (++tj == nkw) {
@@ -374,7 +400,7 @@ struct Issuer {
 // pipelined layers (op 71 fwd -11.6 %), op 73 fwd +1.5 %; the whole step within +-0.2 % (the launches overlap other
 // streams' work there).  The eval instance keeps 0 (not measured)
 template <int BM, int BN, int WM, int WN, int MODE, int EPI = 2, int NS = 3, int ABL = 0, bool C1 = false,
-          bool EV = false, int MF = 16, int RO = 0, int LP = 0>
+          bool EV = false, int MF = 16, int RO = 0, int LP = 0, int TO = 0>
 __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, EvalArgs e) {
     static_assert(!EV || (C1 && MODE == PF && ABL == 0), "the eval instance is a single-class forward");
     static_assert(MF == 16 || MF == 32, "MFMA shape");
@@ -507,7 +533,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(PipeArgs a, 
 #pragma unroll
         for (int r = 0; r < NR; ++r) ssum[i][r] = ssq[i][r] = 0.f;
 
-    Issuer<BM, BN, NW, MODE, ABL, C1> is(a, wave, lane, mt_lo, qstride, ntile);
+    Issuer<BM, BN, NW, MODE, ABL, C1, TO> is(a, wave, lane, mt_lo, qstride, ntile);
     is.start();
 
     // prologue: stages 0..2 in flight (stages past the stream's end fetch nothing); stage 0 landed
@@ -746,12 +772,12 @@ constexpr Cfg kCfg[] = {{256, 128}, {256, 64}, {256, 128}};
 // the barrier others issue MFMAs — same-process A/B against 8 waves: fwd / dgrad 0-7 % faster on every
 // layer measured (1x1 80x80 192->256 -6.8 / -6.2 %, 3x3 40x40 128->128 -3.3 / -6.7 %, stride-2 80x80 equal)
 // cfg 0 / 1 / 2 tiles (kCfg) of one control path (C1), MFMA shape (MF) and issue order (RO)
-template <int MODE, bool C1, int MF, int RO, int LP = 0>
+template <int MODE, bool C1, int MF, int RO, int LP = 0, int TO = 0>
 void launch_tiles(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     switch (cfg) {
-        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
-        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
-        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        case 0: conv_pipe_kernel<256, 128, 4, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP, TO><<<dim3(grid), dim3(1024), 0, st>>>(a, EvalArgs{}); break;
+        case 1: conv_pipe_kernel<256, 64, 1, 8, MODE, 2, 3, 0, C1, false, MF, RO, LP, TO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
+        default: conv_pipe_kernel<256, 128, 2, 4, MODE, 2, 3, 0, C1, false, MF, RO, LP, TO><<<dim3(grid), dim3(512), 0, st>>>(a, EvalArgs{}); break;
     }
 }
 
@@ -777,6 +803,7 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
             else launch_tiles<MODE, true, 32, 0>(c, a, grid, st);
         } else {
             if (ro) launch_tiles<MODE, true, 16, 1>(c, a, grid, st);
+            else if (g_pipe_taporder) launch_tiles<MODE, true, 16, 0, 2, 1>(c, a, grid, st);
             else if (g_pipe_loop == 0) launch_tiles<MODE, true, 16, 0, 0>(c, a, grid, st);
             else if (g_pipe_loop == 1) launch_tiles<MODE, true, 16, 0, 1>(c, a, grid, st);
             else launch_tiles<MODE, true, 16, 0, 2>(c, a, grid, st);
@@ -867,6 +894,11 @@ extern "C" int ym_conv_set_pipe_loop(int mode) {
     // loop form of the pipelined kernel's single-class path (conv_pipe_kernel LP: 0 flat, 1 nested tiles x K steps,
     // 2 nested with the slot offset carried)
     return g_pipe_loop.set(mode < 0 || mode > 2 ? 2 : mode);
+}
+
+extern "C" int ym_conv_set_pipe_taporder(int mode) {
+    // K order of the pipelined kernel's single-class path (conv_pipe_kernel TO: 0 chunk innermost, 1 tap innermost)
+    return g_pipe_taporder.set(mode < 0 || mode > 1 ? 0 : mode);
 }
 
 extern "C" int ym_conv_set_pipe_mfma(int mode) {
