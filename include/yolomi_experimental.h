@@ -103,8 +103,9 @@ int ym_conv_set_pipe_loop(int mode);
 /* Tap lookahead of the 3x3 weight-gradient kernel (round 6): 0 each tap's input fragments read right before its MFMAs,
  * 1 one tap ahead.  Out of range restores the shipped setting.  Returns the previous setting. */
 int ym_wgrad_set_lookahead(int la);
-/* K order of the pipelined kernel's single-class path (round 6): 0 (default) channel chunk innermost, 1 tap innermost
- * (the taps that re-read the same input pixels back to back).  Returns the previous setting. */
+/* K order of the pipelined kernel's single-class forward (round 6): 0 channel chunk innermost everywhere, 1 tap
+ * innermost everywhere (the taps that re-read the same input pixels back to back), anything else (default) the shipped
+ * rule — tap innermost on the stride-2 3x3 forwards reading maps >= 128 wide.  Returns the previous setting. */
 int ym_conv_set_pipe_taporder(int mode);
 #endif
 

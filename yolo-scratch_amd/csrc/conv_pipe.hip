@@ -53,7 +53,7 @@ Policy g_pipe_force{-1};
 Policy g_pipe_mfma{0};
 Policy g_pipe_order{0};   // also conv_hpipe.hip (conv_pipe.h)
 Policy g_pipe_loop{2};    // conv_pipe_kernel LP of the single-class path (2 shipped)
-Policy g_pipe_taporder{0};   // conv_pipe_kernel TO of the single-class path (0 shipped)
+Policy g_pipe_taporder{-1};  // conv_pipe_kernel TO of the single-class forward: -1 the shipped rule (tap_inner), 0 / 1 forced
 Policy g_pipe_exp{0};
 #else
 constexpr int g_pipe_exp = 0;
@@ -781,6 +781,12 @@ void launch_tiles(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     }
 }
 
+// the tap-innermost K order (Issuer TO 1) where it measured faster: stride-2 3x3 forwards reading maps >= 128 wide (op 6,
+// 128 -> 128 at 160x160 -> 80x80: -12 % time, -27 % HBM fetch; profiles/r06/pipe_taporder_ab.txt) — there one tile's
+// input over every channel chunk overflows its share of the XCD's L2, one chunk's does not.  Elsewhere it measured
+// 0..+5 % slower (a tap_setup per K step, and the footprint fits L2 either way)
+inline bool tap_inner(const PipeArgs& a) { return a.stride == 2 && a.KH == 3 && a.GW >= 128; }
+
 template <int MODE>
 void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     const bool c1 = a.ncls == 1 && int64_t(a.OH) * a.OW >= kCfg[cfg].bm && g_pipe_exp != 20;
@@ -803,7 +809,9 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
             else launch_tiles<MODE, true, 32, 0>(c, a, grid, st);
         } else {
             if (ro) launch_tiles<MODE, true, 16, 1>(c, a, grid, st);
-            else if (g_pipe_taporder) launch_tiles<MODE, true, 16, 0, 2, 1>(c, a, grid, st);
+            else if (MODE == PF && (g_pipe_taporder == 1 || (g_pipe_taporder < 0 && tap_inner(a)))) {
+                if constexpr (MODE == PF) launch_tiles<MODE, true, 16, 0, 2, 1>(c, a, grid, st);
+            }
             else if (g_pipe_loop == 0) launch_tiles<MODE, true, 16, 0, 0>(c, a, grid, st);
             else if (g_pipe_loop == 1) launch_tiles<MODE, true, 16, 0, 1>(c, a, grid, st);
             else launch_tiles<MODE, true, 16, 0, 2>(c, a, grid, st);
@@ -813,8 +821,17 @@ void launch_mode(int cfg, const PipeArgs& a, int grid, hipStream_t st) {
     if (mf != 0) launch_tiles<MODE, false, 32, 0>(c, a, grid, st);
     else launch_tiles<MODE, false, 16, 0>(c, a, grid, st);
 #else
-    if (c1) launch_tiles<MODE, true, 16, 0, 2>(cfg, a, grid, st);
-    else launch_tiles<MODE, false, 16, 0>(cfg, a, grid, st);
+    if (c1) {
+        if constexpr (MODE == PF) {
+            if (tap_inner(a)) {
+                launch_tiles<MODE, true, 16, 0, 2, 1>(cfg, a, grid, st);
+                return;
+            }
+        }
+        launch_tiles<MODE, true, 16, 0, 2>(cfg, a, grid, st);
+    } else {
+        launch_tiles<MODE, false, 16, 0>(cfg, a, grid, st);
+    }
 #endif
 }
 
@@ -897,8 +914,9 @@ extern "C" int ym_conv_set_pipe_loop(int mode) {
 }
 
 extern "C" int ym_conv_set_pipe_taporder(int mode) {
-    // K order of the pipelined kernel's single-class path (conv_pipe_kernel TO: 0 chunk innermost, 1 tap innermost)
-    return g_pipe_taporder.set(mode < 0 || mode > 1 ? 0 : mode);
+    // K order of the pipelined kernel's single-class forward (conv_pipe_kernel TO): 0 chunk innermost, 1 tap innermost,
+    // anything else the shipped rule (tap_inner)
+    return g_pipe_taporder.set(mode < 0 || mode > 1 ? -1 : mode);
 }
 
 extern "C" int ym_conv_set_pipe_mfma(int mode) {
