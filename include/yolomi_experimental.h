@@ -107,6 +107,9 @@ int ym_wgrad_set_lookahead(int la);
  * innermost everywhere (the taps that re-read the same input pixels back to back), anything else (default) the shipped
  * rule — tap innermost on the stride-2 3x3 forwards reading maps >= 128 wide.  Returns the previous setting. */
 int ym_conv_set_pipe_taporder(int mode);
+/* Loop form of the pipelined kernel's eval instance (round 6): 2 the nested form the training instances ship, anything
+ * else (default) the flat loop.  Returns the previous setting. */
+int ym_conv_set_pipe_eval_loop(int mode);
 #endif
 
 #ifdef __cplusplus

@@ -58,7 +58,8 @@ def main():
 
     dev = torch.device("cuda", 0)
     st = torch.cuda.current_stream(dev)
-    # A/B of a library policy: YM_LIB_SET="ym_conv_set_eval_cfg=2 ..." (process-wide setters, include/yolomi.h)
+    # A/B of a library policy: YM_LIB_SET="ym_conv_set_eval_cfg=2 ..." (process-wide setters, include/yolomi_experimental.h;
+    # the measurement-library ones need YOLOMI_LIB=.../libyolomi_exp.so)
     if os.environ.get("YM_LIB_SET"):
         from yolomi._lib import lib as _yl0
         for kv in os.environ["YM_LIB_SET"].split():

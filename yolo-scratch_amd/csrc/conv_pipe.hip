@@ -53,6 +53,7 @@ Policy g_pipe_force{-1};
 Policy g_pipe_mfma{0};
 Policy g_pipe_order{0};   // also conv_hpipe.hip (conv_pipe.h)
 Policy g_pipe_loop{2};    // conv_pipe_kernel LP of the single-class path (2 shipped)
+Policy g_pipe_eval_loop{0};  // conv_pipe_kernel LP of the eval instance (0 shipped, 2 the nested loop)
 Policy g_pipe_taporder{-1};  // conv_pipe_kernel TO of the single-class forward: -1 the shipped rule (tap_inner), 0 / 1 forced
 Policy g_pipe_exp{0};
 #else
@@ -844,6 +845,13 @@ void launch_eval(int cfg, const PipeArgs& a, const EvalArgs& e, int grid, hipStr
         else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true, 32><<<dim3(grid), dim3(512), 0, st>>>(a, e);
         return;
     }
+    if (g_pipe_eval_loop == 2) {
+        // the nested loop form of the training instances: inference bs 1 / 8 / 128 within the run-to-run spread of the
+        // flat form (profiles/r06/pipe_eval_loop_ab.txt), so the eval instance keeps the flat loop
+        if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true, 16, 0, 2><<<dim3(grid), dim3(512), 0, st>>>(a, e);
+        else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true, 16, 0, 2><<<dim3(grid), dim3(512), 0, st>>>(a, e);
+        return;
+    }
 #endif
     if (cfg == 1) conv_pipe_kernel<256, 64, 1, 8, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
     else conv_pipe_kernel<256, 128, 2, 4, PF, 2, 3, 0, true, true><<<dim3(grid), dim3(512), 0, st>>>(a, e);
@@ -911,6 +919,11 @@ extern "C" int ym_conv_set_pipe_loop(int mode) {
     // loop form of the pipelined kernel's single-class path (conv_pipe_kernel LP: 0 flat, 1 nested tiles x K steps,
     // 2 nested with the slot offset carried)
     return g_pipe_loop.set(mode < 0 || mode > 2 ? 2 : mode);
+}
+
+extern "C" int ym_conv_set_pipe_eval_loop(int mode) {
+    // loop form of the pipelined kernel's eval instance (conv_pipe_kernel LP: 0 flat, 2 nested); returns the previous
+    return g_pipe_eval_loop.set(mode == 2 ? 2 : 0);
 }
 
 extern "C" int ym_conv_set_pipe_taporder(int mode) {
